@@ -1,0 +1,150 @@
+/* mcpt.h — C ABI of the MI355X path tracer (libmcpt.so).
+ *
+ * Drop-in boundary for the reference's hot path.  Two halves:
+ *
+ *  1. Device renderer — replaces the GL program `prg_ray` (raytracer.vert +
+ *     raytracer_func.frag + tp/<variant>.frag + main.frag), its texture/uniform ABI
+ *     and the additive RGB32F FBO of MontecarloGPU/montecarlo.cpp:384-386, 408-477.
+ *  2. Host scene producer — replaces ScenePrimitives / BVH_KDtree / BVH_GPU_Scene
+ *     (bvh_gpu/scene.h:75-185, bvh.h:10-60, gpu_bvh_scene.h:35-121) and the canonical
+ *     camera (easycppogl/camera.cpp:53-95 + montecarlo.cpp:388-389, 404-405, 439-440).
+ *
+ * Conventions: plain pointers and sizes, no torch types.  Matrices are 16 floats,
+ * column-major (GL / Eigen storage).  Images are H rows × W pixels × RGB f32, row 0 =
+ * bottom (GL window coordinates).  Every function returns an int status: 0 = ok,
+ * negative = error (see mcpt_status); mcpt_error_string() describes it.  The caller
+ * owns host arrays; the library owns device copies.  One context per GPU; calls on
+ * one context are not thread-safe; contexts on different GPUs may run concurrently.
+ * There is NO CPU fallback: every render call runs the HIP kernel or fails.
+ */
+#ifndef MCPT_H_
+#define MCPT_H_
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum mcpt_status {
+  MCPT_OK = 0,
+  MCPT_ERR_INVALID_ARG = -1,
+  MCPT_ERR_NO_SCENE = -2,
+  MCPT_ERR_NO_TARGET = -3,
+  MCPT_ERR_HIP = -4,         /* a HIP runtime call failed (no GPU, launch failure ...) */
+  MCPT_ERR_NOT_FINALIZED = -5,
+  MCPT_ERR_BAD_SCENE = -6,
+};
+
+/* integrator variants: the SrcLoader list of MontecarloGPU/montecarlo.cpp:27 */
+enum mcpt_variant {
+  MCPT_MONTECARLO = 0,       /* tp/montecarlo.frag        */
+  MCPT_MAT = 1,              /* tp/montecarlo_mat.frag    */
+  MCPT_MAT_TR = 2,           /* tp/montecarlo_mat_tr.frag */
+};
+
+/* algorithmic-byte event counters, index order */
+enum mcpt_event {
+  MCPT_EV_NODE = 0, MCPT_EV_LEAF, MCPT_EV_PRIM, MCPT_EV_CAND, MCPT_EV_GEOM, MCPT_EV_COLMAT,
+  MCPT_EV_SAMPLE, MCPT_EV_TRAV, MCPT_EV_COUNT
+};
+
+typedef struct mcpt_ctx mcpt_ctx;
+typedef struct mcpt_scene mcpt_scene;
+
+const char* mcpt_error_string(int status);
+int mcpt_version(void);
+
+/* ---------------------------------------------------------------------------------
+ * 1. device renderer
+ * --------------------------------------------------------------------------------- */
+
+/* create a context on HIP device `device_ordinal` (replaces GLViewer ctx + prg_ray) */
+int mcpt_create(int device_ordinal, mcpt_ctx** out);
+int mcpt_destroy(mcpt_ctx* ctx);
+
+/* Upload a finalized scene in the reference's texture layouts:
+ *   prims  : n_prims × 64 f32 (16 RGBA texels per PrimData, scene.h:64-73)
+ *   nodes  : (2^(depth+1)-1) × 6 f32 (bbmin.xyz, bbmax.xyz)  — tex_bb, gpu_bvh_scene.cpp:39-41
+ *   leaves : 2^depth i32 (prim index or -1)                   — tex_ind, gpu_bvh_scene.cpp:143-144
+ * Replaces BVH_GPU_Scene::finalize's Texture2D uploads (gpu_bvh_scene.cpp:143-160) and
+ * the uniforms nb_prims(1), bvh_depth(2), nb_emissives(20).  Transforms must be affine
+ * (row 3 = 0,0,0,1: the shader only uses .xyz).  Synchronous. */
+int mcpt_upload_scene(mcpt_ctx* ctx, const float* prims, int n_prims, const float* nodes,
+                      const int* leaves, int depth, int nb_emissives);
+
+/* Set the framebuffer (replaces FBO RGB32F + resize_ogl, montecarlo.cpp:384-386, 616-626).
+ * Row-band sharding for multi-GPU: this context renders global rows y whose band
+ * (y / band_rows) satisfies band % world == rank; its accumulator holds only those
+ * "local" rows, in increasing y.  Single GPU: band_rows = any > 0, world = 1, rank = 0.
+ * Allocates and zeroes the accumulator; pass count reset to 0. */
+int mcpt_set_target(mcpt_ctx* ctx, int W, int H, int band_rows, int world, int rank);
+int mcpt_local_rows(mcpt_ctx* ctx, int* n_local_rows);
+
+/* Accumulate passes first_pass .. first_pass+n_passes-1 into the accumulator (the
+ * glDrawArrays loop of montecarlo.cpp:454-466 with blend ONE/ONE).  Uniform ABI:
+ * invPV(10), invV(6), numero_pass(4) = pass index, date(5), NB_BOUNCES(21),
+ * refract_ind(24); variant = tp/ shader.  Asynchronous on the context's stream. */
+int mcpt_render(mcpt_ctx* ctx, const float* invPV, const float* invV, int first_pass,
+                int n_passes, float date, int bounces, float refract_ind, int variant);
+
+/* Same, with the counting build of the kernel: adds MCPT_EV_COUNT event totals into
+ * events[] (algorithmic bytes = Σ events × mcpt_event_bytes).  Synchronous. */
+int mcpt_render_counted(mcpt_ctx* ctx, const float* invPV, const float* invV, int first_pass,
+                        int n_passes, float date, int bounces, float refract_ind, int variant,
+                        unsigned long long* events);
+int mcpt_event_bytes(int event);
+
+/* Copy the local accumulator (n_local_rows × W × 3 f32) to the host and report the
+ * number of passes accumulated (the caller divides: fs_frag, montecarlo.cpp:59-70).
+ * Synchronizes the context's stream. */
+int mcpt_read_accum(mcpt_ctx* ctx, float* rgb_out, int* pass_count);
+int mcpt_clear_accum(mcpt_ctx* ctx);
+
+/* Device pointer of the local accumulator (for an RCCL gather by the caller). */
+int mcpt_accum_device_ptr(mcpt_ctx* ctx, void** dev_ptr, size_t* bytes);
+
+/* Use an external hipStream_t (e.g. torch's current stream); NULL = library stream. */
+int mcpt_set_stream(mcpt_ctx* ctx, void* hip_stream);
+int mcpt_synchronize(mcpt_ctx* ctx);
+
+/* Device time (ms) of the kernel(s) of the last mcpt_render, from HIP events recorded
+ * on the launch stream around the launch.  Synchronizes on the end event. */
+int mcpt_last_render_ms(mcpt_ctx* ctx, float* ms);
+
+/* ---------------------------------------------------------------------------------
+ * 2. host scene producer (BVH_GPU_Scene-compatible)
+ *    material[7] = { r, g, b, a(opacity), shininess, roughness, emissivity }
+ *    (Material, bvh_gpu/scene.h:30-49; Material::light(col,e) = {col, 0, 0, e})
+ * --------------------------------------------------------------------------------- */
+int mcpt_scene_create(mcpt_scene** out);
+int mcpt_scene_destroy(mcpt_scene* s);
+int mcpt_scene_clear(mcpt_scene* s);                                            /* gpu_bvh_scene.cpp:76-85 */
+int mcpt_scene_add_sphere(mcpt_scene* s, const float* trf16, const float* material7);   /* scene.h:128-133 */
+int mcpt_scene_add_cube(mcpt_scene* s, const float* trf16, const float* material7);     /* scene.h:135-142 */
+int mcpt_scene_add_cylinder(mcpt_scene* s, const float* trf16, const float* material7); /* scene.h:144-152 */
+int mcpt_scene_add_cone(mcpt_scene* s, const float* trf16, const float* material7);     /* scene.h:154-163 */
+int mcpt_scene_add_oriented_quad(mcpt_scene* s, const float* trf16, const float* material7); /* scene.h:166-172 */
+/* sortEmissiveFirst + BVH_KDtree::compute (scene.cpp:70-88, bvh.cpp:34-93) */
+int mcpt_scene_finalize(mcpt_scene* s);
+int mcpt_scene_nb_prim(mcpt_scene* s, int* n);
+int mcpt_scene_depth(mcpt_scene* s, int* depth);
+int mcpt_scene_nb_emissives(mcpt_scene* s, int* n);
+/* copy the finalized buffers in the layouts mcpt_upload_scene takes */
+int mcpt_scene_get_buffers(mcpt_scene* s, float* prims, float* nodes, int* leaves);
+/* overwrite (shininess, roughness, emissivity) and colour of finalized prim i (BVH unchanged;
+ * emissivity must keep its sign class: the emissive-first order is fixed at finalize) */
+int mcpt_scene_set_material(mcpt_scene* s, int prim, const float* material7);
+/* the 8 scene builders of MontecarloGPU/montecarlo.cpp:629-795 (keys Q,W,E,R,T,Y,U,I = 1..8),
+ * with light_intensity_ (default 1.2, montecarlo.cpp:138).  Clears, builds, finalizes. */
+int mcpt_scene_build_reference(mcpt_scene* s, int scene_id, float light_intensity);
+
+/* canonical camera at aspect W/H: fov 0.78, scene radius 145, frame identity,
+ * view = modelview · rotateX(-80); outputs (P·V)^-1 and V^-1, column-major */
+int mcpt_camera_canonical(int W, int H, float* invPV16, float* invV16);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MCPT_H_ */

@@ -1,0 +1,318 @@
+// mcpt_capi.hip — C ABI, device half: context, scene upload (repack to device records),
+// framebuffer / row-band sharding, render launches, accumulator read-back.
+//
+// Replaces the GL state of the reference's render path: Texture2D uploads
+// (bvh_gpu/gpu_bvh_scene.cpp:143-160), the RGB32F FBO + blend (MontecarloGPU/montecarlo.cpp:
+// 384-386, 420-467), the uniform ABI (montecarlo.cpp:439-453) and the corner-ray vertex
+// shader (shaders/raytracer.vert:9-22, evaluated here once per launch on the host).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/mcpt.h"
+#include "mcpt_internal.h"
+
+static thread_local char g_last_error[256] = "";
+
+static int set_err(int status, const char* what, hipError_t e = hipSuccess) {
+  if (e != hipSuccess)
+    std::snprintf(g_last_error, sizeof(g_last_error), "%s: %s", what, hipGetErrorString(e));
+  else
+    std::snprintf(g_last_error, sizeof(g_last_error), "%s", what);
+  return status;
+}
+
+#define HIP_OR_RETURN(call)                                         \
+  do {                                                              \
+    hipError_t e_ = (call);                                         \
+    if (e_ != hipSuccess) return set_err(MCPT_ERR_HIP, #call, e_);  \
+  } while (0)
+
+struct mcpt_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  // scene (device records)
+  float4* d_nodes = nullptr;
+  int* d_leaves = nullptr;
+  int* d_ptype = nullptr;
+  float4* d_prims = nullptr;
+  int n_prims = 0, depth = 0, nb_emissive = 0;
+  bool has_scene = false;
+  // framebuffer
+  float* d_accum = nullptr;
+  size_t accum_bytes = 0;
+  int W = 0, H = 0, band_rows = 1, world = 1, rank = 0, n_local_rows = 0;
+  int pass_count = 0;
+  bool has_target = false;
+  unsigned long long* d_events = nullptr;
+  hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+  bool timed = false;
+};
+
+extern "C" {
+
+const char* mcpt_error_string(int status) {
+  switch (status) {
+    case MCPT_OK: return "ok";
+    case MCPT_ERR_INVALID_ARG: return "invalid argument";
+    case MCPT_ERR_NO_SCENE: return "no scene uploaded";
+    case MCPT_ERR_NO_TARGET: return "no render target (call mcpt_set_target)";
+    case MCPT_ERR_HIP: return g_last_error[0] ? g_last_error : "HIP runtime error";
+    case MCPT_ERR_NOT_FINALIZED: return "scene not finalized";
+    case MCPT_ERR_BAD_SCENE: return "malformed scene buffers";
+    default: return "unknown status";
+  }
+}
+
+int mcpt_version(void) { return 1; }
+
+int mcpt_create(int device_ordinal, mcpt_ctx** out) {
+  if (!out) return MCPT_ERR_INVALID_ARG;
+  *out = nullptr;
+  int n = 0;
+  HIP_OR_RETURN(hipGetDeviceCount(&n));
+  if (device_ordinal < 0 || device_ordinal >= n) return set_err(MCPT_ERR_INVALID_ARG, "device ordinal out of range");
+  HIP_OR_RETURN(hipSetDevice(device_ordinal));
+  mcpt_ctx* c = new (std::nothrow) mcpt_ctx();
+  if (!c) return MCPT_ERR_INVALID_ARG;
+  c->device = device_ordinal;
+  hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev_start);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev_stop);
+  if (e == hipSuccess) e = hipMalloc(&c->d_events, sizeof(unsigned long long) * mcpt::EV_COUNT);
+  if (e != hipSuccess) { mcpt_destroy(c); return set_err(MCPT_ERR_HIP, "mcpt_create", e); }
+  c->stream = c->own_stream;
+  *out = c;
+  return MCPT_OK;
+}
+
+static void free_scene(mcpt_ctx* c) {
+  (void)hipFree(c->d_nodes); (void)hipFree(c->d_leaves); (void)hipFree(c->d_ptype); (void)hipFree(c->d_prims);
+  c->d_nodes = nullptr; c->d_leaves = nullptr; c->d_ptype = nullptr; c->d_prims = nullptr;
+  c->has_scene = false;
+}
+
+int mcpt_destroy(mcpt_ctx* c) {
+  if (!c) return MCPT_OK;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  free_scene(c);
+  (void)hipFree(c->d_accum);
+  (void)hipFree(c->d_events);
+  if (c->ev_start) (void)hipEventDestroy(c->ev_start);
+  if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  delete c;
+  return MCPT_OK;
+}
+
+int mcpt_upload_scene(mcpt_ctx* c, const float* prims, int n_prims, const float* nodes, const int* leaves,
+                      int depth, int nb_emissives) {
+  if (!c || !prims || !nodes || !leaves || n_prims <= 0 || depth < 0 || depth > 24)
+    return set_err(MCPT_ERR_INVALID_ARG, "mcpt_upload_scene: bad arguments");
+  const int n_leaf = 1 << depth, n_node = 2 * n_leaf - 1;
+  for (int i = 0; i < n_leaf; ++i)
+    if (leaves[i] < -1 || leaves[i] >= n_prims) return set_err(MCPT_ERR_BAD_SCENE, "leaf id out of range");
+  // nodes → (centre, half-width, 1/half-width): raytracer_func.frag:319-320 hoisted to upload
+  std::vector<float4> hn((size_t)n_node * mcpt::kNodeF4);
+  for (int i = 0; i < n_node; ++i) {
+    const float* b = nodes + (size_t)i * 6;
+    float cx = (b[0] + b[3]) / 2.0f, cy = (b[1] + b[4]) / 2.0f, cz = (b[2] + b[5]) / 2.0f;
+    float wx = 0.5f * (b[3] - b[0]), wy = 0.5f * (b[4] - b[1]), wz = 0.5f * (b[5] - b[2]);
+    hn[(size_t)i * 3 + 0] = make_float4(cx, cy, cz, 0.0f);
+    hn[(size_t)i * 3 + 1] = make_float4(wx, wy, wz, 0.0f);
+    hn[(size_t)i * 3 + 2] = make_float4(1.0f / wx, 1.0f / wy, 1.0f / wz, 0.0f);
+  }
+  // prims → rows of the inverse and of the transform (the shader uses .xyz of mat4·v)
+  std::vector<int> ht(n_prims);
+  std::vector<float4> hp((size_t)n_prims * mcpt::kPrimF4);
+  for (int i = 0; i < n_prims; ++i) {
+    const float* r = prims + (size_t)i * 64;
+    float tcode = r[48];
+    if (!(tcode >= 0.0f && tcode <= 5.0f)) return set_err(MCPT_ERR_BAD_SCENE, "primitive type code not in 0..5");
+    ht[i] = (int)tcode;
+    float4* o = &hp[(size_t)i * mcpt::kPrimF4];
+    for (int row = 0; row < 3; ++row) {
+      const float* inv = r + 16;
+      o[row] = make_float4(inv[row], inv[4 + row], inv[8 + row], inv[12 + row]);
+      o[3 + row] = make_float4(r[row], r[4 + row], r[8 + row], r[12 + row]);
+    }
+    o[6] = make_float4(r[52], r[53], r[54], r[55]);
+    o[7] = make_float4(r[56], r[57], r[58], r[59]);
+  }
+  HIP_OR_RETURN(hipSetDevice(c->device));
+  HIP_OR_RETURN(hipStreamSynchronize(c->stream));
+  free_scene(c);
+  HIP_OR_RETURN(hipMalloc(&c->d_nodes, hn.size() * sizeof(float4)));
+  HIP_OR_RETURN(hipMalloc(&c->d_leaves, (size_t)n_leaf * sizeof(int)));
+  HIP_OR_RETURN(hipMalloc(&c->d_ptype, (size_t)n_prims * sizeof(int)));
+  HIP_OR_RETURN(hipMalloc(&c->d_prims, hp.size() * sizeof(float4)));
+  HIP_OR_RETURN(hipMemcpy(c->d_nodes, hn.data(), hn.size() * sizeof(float4), hipMemcpyHostToDevice));
+  HIP_OR_RETURN(hipMemcpy(c->d_leaves, leaves, (size_t)n_leaf * sizeof(int), hipMemcpyHostToDevice));
+  HIP_OR_RETURN(hipMemcpy(c->d_ptype, ht.data(), (size_t)n_prims * sizeof(int), hipMemcpyHostToDevice));
+  HIP_OR_RETURN(hipMemcpy(c->d_prims, hp.data(), hp.size() * sizeof(float4), hipMemcpyHostToDevice));
+  c->n_prims = n_prims; c->depth = depth; c->nb_emissive = nb_emissives;
+  c->has_scene = true;
+  return MCPT_OK;
+}
+
+static int count_local_rows(int H, int band_rows, int world, int rank) {
+  int n = 0;
+  for (int y = 0; y < H; ++y)
+    if ((y / band_rows) % world == rank) ++n;
+  return n;
+}
+
+int mcpt_set_target(mcpt_ctx* c, int W, int H, int band_rows, int world, int rank) {
+  if (!c || W <= 0 || H <= 0 || band_rows <= 0 || world <= 0 || rank < 0 || rank >= world)
+    return set_err(MCPT_ERR_INVALID_ARG, "mcpt_set_target: bad arguments");
+  HIP_OR_RETURN(hipSetDevice(c->device));
+  HIP_OR_RETURN(hipStreamSynchronize(c->stream));
+  int nl = count_local_rows(H, band_rows, world, rank);
+  size_t bytes = (size_t)nl * W * 3 * sizeof(float);
+  if (bytes != c->accum_bytes) {
+    (void)hipFree(c->d_accum);
+    c->d_accum = nullptr;
+    c->accum_bytes = 0;
+    if (bytes) HIP_OR_RETURN(hipMalloc(&c->d_accum, bytes));
+    c->accum_bytes = bytes;
+  }
+  c->W = W; c->H = H; c->band_rows = band_rows; c->world = world; c->rank = rank; c->n_local_rows = nl;
+  c->has_target = true;
+  return mcpt_clear_accum(c);
+}
+
+int mcpt_local_rows(mcpt_ctx* c, int* n) {
+  if (!c || !n) return MCPT_ERR_INVALID_ARG;
+  if (!c->has_target) return MCPT_ERR_NO_TARGET;
+  *n = c->n_local_rows;
+  return MCPT_OK;
+}
+
+int mcpt_clear_accum(mcpt_ctx* c) {
+  if (!c) return MCPT_ERR_INVALID_ARG;
+  if (!c->has_target) return MCPT_ERR_NO_TARGET;
+  HIP_OR_RETURN(hipSetDevice(c->device));
+  if (c->accum_bytes) HIP_OR_RETURN(hipMemsetAsync(c->d_accum, 0, c->accum_bytes, c->stream));
+  c->pass_count = 0;
+  return MCPT_OK;
+}
+
+// raytracer.vert:9-22 for the 4 strip corners: Ori = invV·(0,0,0,1), Dir = normalize(Q.xyz/Q.w − Ori)
+static void corner_rays(const float* invPV, const float* invV, mcpt::RenderParams& p) {
+  auto matvec = [](const float* m, const float v[4], float o[4]) {
+    for (int r = 0; r < 4; ++r)
+      o[r] = std::fma(m[12 + r], v[3], std::fma(m[8 + r], v[2], std::fma(m[4 + r], v[1], m[r] * v[0])));
+  };
+  const float origin[4] = {0.0f, 0.0f, 0.0f, 1.0f};
+  float o4[4];
+  matvec(invV, origin, o4);
+  p.ox = o4[0]; p.oy = o4[1]; p.oz = o4[2];
+  for (int v = 0; v < 4; ++v) {
+    float tcx = (float)(v % 2), tcy = (float)(v / 2);
+    float cv[4] = {2.0f * tcx - 1.0f, 2.0f * tcy - 1.0f, 1.0f, 1.0f};
+    float q[4];
+    matvec(invPV, cv, q);
+    float dx = q[0] / q[3] - o4[0], dy = q[1] / q[3] - o4[1], dz = q[2] / q[3] - o4[2];
+    float len2 = std::fma(dz, dz, std::fma(dy, dy, dx * dx));
+    float rn = 1.0f / std::sqrt(len2);
+    p.cd[3 * v + 0] = dx * rn; p.cd[3 * v + 1] = dy * rn; p.cd[3 * v + 2] = dz * rn;
+  }
+}
+
+static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_pass, int n_passes, float date,
+                  int bounces, float refract_ind, int variant, bool count, unsigned long long* events) {
+  if (!c || !invPV || !invV || n_passes < 0 || variant < 0 || variant > 2)
+    return set_err(MCPT_ERR_INVALID_ARG, "mcpt_render: bad arguments");
+  if (!c->has_scene) return set_err(MCPT_ERR_NO_SCENE, "no scene uploaded");
+  if (!c->has_target) return set_err(MCPT_ERR_NO_TARGET, "no render target");
+  HIP_OR_RETURN(hipSetDevice(c->device));
+  mcpt::RenderParams p;
+  std::memset(&p, 0, sizeof(p));
+  p.nodes = c->d_nodes; p.leaves = c->d_leaves; p.ptype = c->d_ptype; p.prims = c->d_prims;
+  p.accum = c->d_accum; p.events = c->d_events;
+  corner_rays(invPV, invV, p);
+  p.W = c->W; p.H = c->H; p.band_rows = c->band_rows; p.world = c->world; p.rank = c->rank;
+  p.n_local_rows = c->n_local_rows; p.depth = c->depth;
+  p.first_pass = first_pass; p.n_passes = n_passes; p.bounces = bounces; p.variant = variant;
+  p.date = date; p.ior = refract_ind;
+  if (count) HIP_OR_RETURN(hipMemsetAsync(c->d_events, 0, sizeof(unsigned long long) * mcpt::EV_COUNT, c->stream));
+  HIP_OR_RETURN(hipEventRecord(c->ev_start, c->stream));
+  HIP_OR_RETURN(mcpt_launch_render(p, count, c->stream));
+  HIP_OR_RETURN(hipEventRecord(c->ev_stop, c->stream));
+  c->timed = true;
+  c->pass_count += n_passes;
+  if (count) {
+    unsigned long long h[mcpt::EV_COUNT];
+    HIP_OR_RETURN(hipMemcpyAsync(h, c->d_events, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIP_OR_RETURN(hipStreamSynchronize(c->stream));
+    for (int e = 0; e < mcpt::EV_COUNT; ++e) events[e] += h[e];
+  }
+  return MCPT_OK;
+}
+
+int mcpt_render(mcpt_ctx* c, const float* invPV, const float* invV, int first_pass, int n_passes, float date,
+                int bounces, float refract_ind, int variant) {
+  return launch(c, invPV, invV, first_pass, n_passes, date, bounces, refract_ind, variant, false, nullptr);
+}
+
+int mcpt_render_counted(mcpt_ctx* c, const float* invPV, const float* invV, int first_pass, int n_passes,
+                        float date, int bounces, float refract_ind, int variant, unsigned long long* events) {
+  if (!events) return MCPT_ERR_INVALID_ARG;
+  return launch(c, invPV, invV, first_pass, n_passes, date, bounces, refract_ind, variant, true, events);
+}
+
+int mcpt_event_bytes(int e) {
+  if (e < 0 || e >= mcpt::EV_COUNT) return MCPT_ERR_INVALID_ARG;
+  return mcpt::kEventBytes[e];
+}
+
+int mcpt_read_accum(mcpt_ctx* c, float* rgb_out, int* pass_count) {
+  if (!c) return MCPT_ERR_INVALID_ARG;
+  if (!c->has_target) return MCPT_ERR_NO_TARGET;
+  HIP_OR_RETURN(hipSetDevice(c->device));
+  if (rgb_out && c->accum_bytes)
+    HIP_OR_RETURN(hipMemcpyAsync(rgb_out, c->d_accum, c->accum_bytes, hipMemcpyDeviceToHost, c->stream));
+  HIP_OR_RETURN(hipStreamSynchronize(c->stream));
+  if (pass_count) *pass_count = c->pass_count;
+  return MCPT_OK;
+}
+
+int mcpt_accum_device_ptr(mcpt_ctx* c, void** dev_ptr, size_t* bytes) {
+  if (!c || !dev_ptr) return MCPT_ERR_INVALID_ARG;
+  if (!c->has_target) return MCPT_ERR_NO_TARGET;
+  *dev_ptr = c->d_accum;
+  if (bytes) *bytes = c->accum_bytes;
+  return MCPT_OK;
+}
+
+int mcpt_set_stream(mcpt_ctx* c, void* s) {
+  if (!c) return MCPT_ERR_INVALID_ARG;
+  HIP_OR_RETURN(hipSetDevice(c->device));
+  HIP_OR_RETURN(hipStreamSynchronize(c->stream));
+  c->stream = s ? (hipStream_t)s : c->own_stream;
+  return MCPT_OK;
+}
+
+int mcpt_synchronize(mcpt_ctx* c) {
+  if (!c) return MCPT_ERR_INVALID_ARG;
+  HIP_OR_RETURN(hipSetDevice(c->device));
+  HIP_OR_RETURN(hipStreamSynchronize(c->stream));
+  return MCPT_OK;
+}
+
+int mcpt_last_render_ms(mcpt_ctx* c, float* ms) {
+  if (!c || !ms) return MCPT_ERR_INVALID_ARG;
+  if (!c->timed) return set_err(MCPT_ERR_INVALID_ARG, "no render timed yet");
+  HIP_OR_RETURN(hipSetDevice(c->device));
+  HIP_OR_RETURN(hipEventSynchronize(c->ev_stop));
+  HIP_OR_RETURN(hipEventElapsedTime(ms, c->ev_start, c->ev_stop));
+  return MCPT_OK;
+}
+
+}  // extern "C"

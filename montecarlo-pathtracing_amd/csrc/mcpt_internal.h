@@ -1,0 +1,47 @@
+// mcpt_internal.h — shared between the C-ABI host code and the HIP kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mcpt {
+
+// algorithmic-byte events; same order as the oracle's counters
+enum { EV_NODE = 0, EV_LEAF, EV_PRIM, EV_CAND, EV_GEOM, EV_COLMAT, EV_SAMPLE, EV_TRAV, EV_COUNT };
+
+// bytes per event in the reference's texel model
+constexpr int kEventBytes[EV_COUNT] = {
+    48,   // internal node visit: 2 child boxes × 2 RGB32F texels  (raytracer_func.frag:249-255)
+    4,    // leaf id R32I                                          (:243-247)
+    16 + 64,  // prim header texel + inverse transform (4 texels)  (:171-178, :199-207)
+    64,   // transform per accepted candidate                       (:409/426/457/498/563)
+    64,   // intersection_info transform                            (:816/825/837/867)
+    32,   // colour + material texels                               (:899-907)
+    24,   // accumulate: RGB32F read + write (blend)                (montecarlo.cpp:450-452)
+    0,    // traversal count (no bytes of its own)
+};
+
+// device record layout (built by mcpt_upload_scene from the reference texture layout)
+//   node  : 3 × float4  (centre.xyz,0) (halfwidth.xyz,0) (1/halfwidth.xyz,0)
+//   prim  : 8 × float4  inverse rows 0..2, transform rows 0..2, colour, material
+constexpr int kNodeF4 = 3;
+constexpr int kPrimF4 = 8;
+
+struct RenderParams {
+  const float4* nodes;
+  const int* leaves;
+  const int* ptype;
+  const float4* prims;
+  float* accum;                 // n_local_rows × W × 3 (local rows of this shard)
+  unsigned long long* events;   // EV_COUNT counters (counting build only)
+  float ox, oy, oz;             // camera origin (invV · (0,0,0,1))
+  float cd[12];                 // 4 normalized corner directions (raytracer.vert:19)
+  int W, H;
+  int band_rows, world, rank, n_local_rows;
+  int depth;
+  int first_pass, n_passes, bounces, variant;
+  float date, ior;
+};
+
+}  // namespace mcpt
+
+hipError_t mcpt_launch_render(const mcpt::RenderParams& p, bool count, hipStream_t stream);

@@ -1,0 +1,465 @@
+// mcpt_kernel.hip — the per-pixel Monte Carlo sampling loop for CDNA4 (gfx950).
+//
+// Replaces the reference's fragment program prg_ray = raytracer.vert +
+// raytracer_func.frag + tp/<variant>.frag + main.frag (MontecarloGPU/montecarlo.cpp:345-347)
+// and its additive ONE/ONE blend into the RGB32F FBO (montecarlo.cpp:450-466).
+//
+// Design:
+//  * one lane = one pixel for ALL passes of a launch; a lane whose path terminates
+//    immediately regenerates the next pass's path (persistent-lane regeneration), so
+//    a wave runs until its lanes' *sums* of path lengths are exhausted, not the max
+//    path per pass — the 4 material branches and the 0..B bounce lengths average out;
+//  * the bounce loop and the mixed/refraction branch's inner traversal are folded into
+//    ONE traversal site per loop iteration (a 2-phase state machine), so lanes doing an
+//    inner traversal and lanes doing their next bounce run the same instructions;
+//  * BVH traversal is the reference's DFS (raytracer_func.frag:734-769, right child
+//    popped first, cull test at push time) but stackless: the implicit-heap stack is
+//    encoded as a bitmask of levels holding a pending left sibling — registers only;
+//  * the scene is repacked at upload into 16-byte records (node: centre / half-width /
+//    1/half-width; prim: inverse rows, transform rows, colour, material) so every fetch
+//    is a dwordx4; scenes up to kLdsSceneBytes are staged once per workgroup into LDS;
+//  * each lane adds its passes into its own accumulator in pass order and writes once
+//    per launch (bit-identical to the reference's per-pass blend order).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "mcpt_math.h"
+#include "mcpt_internal.h"
+
+namespace mcpt {
+
+struct Hit { f3 pl, pg; float dist; int index, shape, dir; };
+
+enum { CODE_MESH = 0, CODE_SPHERE = 1, CODE_CUBE = 2, CODE_CYLINDER = 3, CODE_CONE = 4, CODE_QUAD = 5 };
+
+// ------------------------------------------------------------------------------------
+// scene views: global memory or LDS-staged copy (same record layout)
+// ------------------------------------------------------------------------------------
+struct SceneRef {
+  const float4* __restrict__ nodes;   // 3 per node: (c, 0) (w, 0) (1/w, 0)
+  const int* __restrict__ leaves;
+  const int* __restrict__ ptype;
+  const float4* __restrict__ prims;   // 8 per prim: inv r0..r2, trf r0..r2, colour, material
+  int depth;
+};
+
+struct Counters {
+  uint32_t v[EV_COUNT];
+  __device__ __forceinline__ void inc(int e) { v[e]++; }
+};
+
+template <bool COUNT>
+struct Ev {
+  Counters c;
+  __device__ __forceinline__ void init() { if (COUNT) for (int i = 0; i < EV_COUNT; ++i) c.v[i] = 0; }
+  __device__ __forceinline__ void inc(int e) { if (COUNT) c.v[e]++; }
+};
+
+// intersect_bv raytracer_func.frag:314-352; divisions as hoisted reciprocals (contract)
+__device__ __forceinline__ bool box_test(const float4* nd, f3 O, f3 D, f3 invD, float cdist) {
+  float4 a0 = nd[0], a1 = nd[1], a2 = nd[2];
+  f3 c = mk(a0.x, a0.y, a0.z), w = mk(a1.x, a1.y, a1.z), iw = mk(a2.x, a2.y, a2.z);
+  f3 Oi = mulv(sub(O, c), iw);
+  f3 Di = mulv(D, iw);
+  if (__builtin_fabsf(Oi.x) < 1.0f && __builtin_fabsf(Oi.y) < 1.0f && __builtin_fabsf(Oi.z) < 1.0f) return true;
+  f3 rD = mulv(invD, w);
+  float al = kFLTMAX;
+  // faces in reference order: (x,-1) (x,+1) (y,-1) (y,+1) (z,-1) (z,+1)
+#define MCPT_FACE(CD, OA, DA, RA, OB, DB, OC, DC)                                              \
+  if (__builtin_fabsf(DA) > kEPS) {                                                            \
+    float a = ((CD) - (OA)) * (RA);                                                            \
+    if ((a > kEPS) && (__builtin_fabsf(OB + a * DB) <= 1.0f) && (__builtin_fabsf(OC + a * DC) <= 1.0f)) \
+      if (a < al) al = a;                                                                      \
+  }
+  MCPT_FACE(-1.0f, Oi.x, Di.x, rD.x, Oi.y, Di.y, Oi.z, Di.z)
+  MCPT_FACE(1.0f, Oi.x, Di.x, rD.x, Oi.y, Di.y, Oi.z, Di.z)
+  MCPT_FACE(-1.0f, Oi.y, Di.y, rD.y, Oi.z, Di.z, Oi.x, Di.x)
+  MCPT_FACE(1.0f, Oi.y, Di.y, rD.y, Oi.z, Di.z, Oi.x, Di.x)
+  MCPT_FACE(-1.0f, Oi.z, Di.z, rD.z, Oi.x, Di.x, Oi.y, Di.y)
+  MCPT_FACE(1.0f, Oi.z, Di.z, rD.z, Oi.x, Di.x, Oi.y, Di.y)
+#undef MCPT_FACE
+  if (al < kFLTMAX) {
+    f3 Pg = add(mulv(add(muls(Di, al), Oi), w), c);
+    return length3(sub(O, Pg)) <= cdist;
+  }
+  return false;
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void accept_cand(const SceneRef& s, int index, int shape, int dir, f3 Pl, f3 Ol,
+                                            Hit& h, Ev<COUNT>& ev) {
+  ev.inc(EV_CAND);
+  const float4* pr = s.prims + (size_t)index * 8;
+  f3 Pg = xpoint(pr[3], pr[4], pr[5], Pl);
+  float dist = length3(sub(Ol, Pg));
+  if (dist < h.dist) { h.dist = dist; h.pl = Pl; h.pg = Pg; h.index = index; h.shape = shape; h.dir = dir; }
+}
+
+// intersect_prim raytracer_func.frag:681-705 + Sphere/Cube/Cylinder/Cone/OrientedQuad :398-640
+template <bool COUNT>
+__device__ __noinline__ void prim_test(const SceneRef& s, int i, f3 Ow, f3 Dw, Hit& h, Ev<COUNT>& ev) {
+  ev.inc(EV_PRIM);
+  int t = s.ptype[i];
+  if (t < 0) return;
+  const float4* pr = s.prims + (size_t)i * 8;
+  float4 r0 = pr[0], r1 = pr[1], r2 = pr[2];
+  f3 O = xpoint(r0, r1, r2, Ow);
+  f3 D = normalize3(xdir(r0, r1, r2, Dw));
+  if (t == CODE_SPHERE) {
+    float OO = dot3(O, O), OD = dot3(O, D), D2 = dot3(D, D);
+    float delta4 = OD * OD - D2 * (OO - 1.0f);
+    if (delta4 > 0.0f) {
+      float sq = __builtin_sqrtf(delta4);
+      float a = -(OD + sq) / D2;
+      if (a > kEPS) accept_cand(s, i, CODE_SPHERE, 0, add(O, muls(D, a)), Ow, h, ev);
+      a = -(OD - sq) / D2;
+      if (a > kEPS) accept_cand(s, i, CODE_SPHERE, 0, add(O, muls(D, a)), Ow, h, ev);
+    }
+  } else if (t == CODE_QUAD) {
+    if (D.z > -kEPS) return;
+    float a = -O.z / D.z;
+    f3 Pl = add(O, muls(D, a));
+    if (__builtin_fabsf(Pl.x) > 1.0f || __builtin_fabsf(Pl.y) > 1.0f) return;
+    accept_cand(s, i, CODE_QUAD, 0, Pl, Ow, h, ev);
+  } else if (t == CODE_CUBE) {
+    float al = kFLTMAX; int cl = 0;
+    float o[3] = {O.x, O.y, O.z}, d[3] = {D.x, D.y, D.z};
+#pragma unroll
+    for (int f = 0; f < 6; ++f) {
+      const int c0 = f / 2, c1 = (c0 + 1) % 3, c2 = (c0 + 2) % 3;
+      if (__builtin_fabsf(d[c0]) > kEPS) {
+        const float cd = (f % 2) ? 1.0f : -1.0f;
+        float a = (cd - o[c0]) / d[c0];
+        if ((a > kEPS) && (__builtin_fabsf(o[c1] + a * d[c1]) <= 1.0f) && (__builtin_fabsf(o[c2] + a * d[c2]) <= 1.0f))
+          if (a < al) { al = a; cl = f; }
+      }
+    }
+    if (al < kFLTMAX) accept_cand(s, i, CODE_CUBE, cl, add(O, muls(D, al)), Ow, h, ev);
+  } else if (t == CODE_CYLINDER) {
+    int cl = -1; float al = kFLTMAX;
+    if (__builtin_fabsf(D.z) > kEPS) {
+      float a = (-1.0f - O.z) / D.z;
+      if (a > kEPS) {
+        float rx = O.x + a * D.x, ry = O.y + a * D.y;
+        if ((__builtin_fmaf(ry, ry, rx * rx) < 1.0f) && (a < al)) { cl = 0; al = a; }
+      }
+      a = (1.0f - O.z) / D.z;
+      if (a > kEPS) {
+        float rx = O.x + a * D.x, ry = O.y + a * D.y;
+        if ((__builtin_fmaf(ry, ry, rx * rx) < 1.0f) && (a < al)) { cl = 1; al = a; }
+      }
+    }
+    float O2 = __builtin_fmaf(O.y, O.y, O.x * O.x);
+    float OD = __builtin_fmaf(O.y, D.y, O.x * D.x);
+    float D2 = __builtin_fmaf(D.y, D.y, D.x * D.x);
+    float delta4 = OD * OD - D2 * (O2 - 1.0f);
+    if (delta4 > 0.0f) {
+      float a = -(OD + __builtin_sqrtf(delta4)) / D2;
+      if ((a > kEPS) && (a < al)) {
+        float z = O.z + a * D.z;
+        if (__builtin_fabsf(z) < 1.0f) { cl = 2; al = a; }
+      }
+    }
+    if (al < kFLTMAX) accept_cand(s, i, CODE_CYLINDER, cl, add(O, muls(D, al)), Ow, h, ev);
+  } else if (t == CODE_CONE) {
+    int cl = -1; float tl = kFLTMAX;
+    if (__builtin_fabsf(D.z) > kEPS) {
+      float t0 = (-1.0f - O.z) / D.z;
+      if (t0 > kEPS) {
+        float rx = O.x + t0 * D.x, ry = O.y + t0 * D.y;
+        if ((__builtin_fmaf(ry, ry, rx * rx) < 1.0f) && (t0 < tl)) { cl = 0; tl = t0; }
+      }
+    }
+    f3 co = O; co.z -= 1.0f;
+    float a = D.z * D.z - 0.8f;
+    float b = 2.0f * (D.z * co.z - dot3(D, co) * 0.8f);
+    float cc = co.z * co.z - dot3(co, co) * 0.8f;
+    float det = b * b - (4.0f * a) * cc;
+    if (det > 0.0f) {
+      det = __builtin_sqrtf(det);
+      float t1 = (-b - det) / (2.0f * a);
+      if (__builtin_fabsf(O.z + t1 * D.z) > 1.0f) t1 = kFLTMAX;
+      float t2 = (-b + det) / (2.0f * a);
+      if (__builtin_fabsf(O.z + t2 * D.z) > 1.0f) t2 = kFLTMAX;
+      float tt = gmin(t1, t2);
+      if (tt < tl) { cl = 2; tl = tt; }
+    }
+    if (tl < kFLTMAX) accept_cand(s, i, CODE_CONE, cl, add(O, muls(D, tl)), Ow, h, ev);
+  }
+  // CODE_MESH: no mesh instance in any reference scene: no hit
+}
+
+// intersect_bvh raytracer_func.frag:734-769, stackless.  pending bit L = "a left sibling
+// at level L waits on the reference's stack"; popping the deepest pending bit is exactly
+// the reference's LIFO order (right child first, cull decided at push time).
+template <bool COUNT>
+__device__ __forceinline__ void traverse(const SceneRef& s, f3 O, f3 D, Hit& h, Ev<COUNT>& ev) {
+  ev.inc(EV_TRAV);
+  h.index = -1; h.dist = kFLTMAX; h.shape = -1; h.dir = -1;
+  const f3 invD = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);
+  const int leaf0 = (1 << s.depth) - 1;
+  int node = 0, level = 0;
+  uint32_t pending = 0;
+  for (;;) {
+    bool pop;
+    if (node >= leaf0) {
+      ev.inc(EV_LEAF);
+      int p = s.leaves[node - leaf0];
+      if (p >= 0) prim_test<COUNT>(s, p, O, D, h, ev);
+      pop = true;
+    } else {
+      ev.inc(EV_NODE);
+      int j = 2 * node + 1;
+      bool hl = box_test(s.nodes + (size_t)j * 3, O, D, invD, h.dist);
+      bool hr = box_test(s.nodes + (size_t)(j + 1) * 3, O, D, invD, h.dist);
+      pop = !(hl || hr);
+      if (hr) {
+        if (hl) pending |= 1u << (level + 1);
+        node = j + 1; level++;
+      } else if (hl) {
+        node = j; level++;
+      }
+    }
+    if (pop) {
+      if (pending == 0) break;
+      int L = 31 - __builtin_clz(pending);
+      pending &= ~(1u << L);
+      node = ((node + 1) >> (level - L)) - 2;
+      level = L;
+    }
+  }
+}
+
+// intersection_info raytracer_func.frag:812-897 (hit only; misses leave N,P untouched)
+template <bool COUNT>
+__device__ __forceinline__ void geom_info(const SceneRef& s, const Hit& h, f3& N, f3& P, Ev<COUNT>& ev) {
+  ev.inc(EV_GEOM);
+  const float4* pr = s.prims + (size_t)h.index * 8;
+  float4 t0 = pr[3], t1 = pr[4], t2 = pr[5];
+  P = h.pg;
+  f3 q;
+  if (h.shape == CODE_SPHERE) {
+    q = muls(h.pl, 2.0f);
+  } else if (h.shape == CODE_CUBE) {
+    float sg = (h.dir % 2 != 0) ? 1.0f : -1.0f;
+    int ax = h.dir / 2;
+    q = add(h.pl, mk(ax == 0 ? sg : 0.0f, ax == 1 ? sg : 0.0f, ax == 2 ? sg : 0.0f));
+  } else if (h.shape == CODE_CYLINDER) {
+    f3 No = (h.dir < 2) ? mk(0.0f, 0.0f, (h.dir % 2 != 0) ? 1.0f : -1.0f) : mk(h.pl.x, h.pl.y, 0.0f);
+    q = add(h.pl, No);
+  } else if (h.shape == CODE_CONE) {
+    if (h.dir == 1) { N = mk(0.0f, 0.0f, 0.0f); return; }
+    if (h.dir == 0) q = mk(h.pl.x, h.pl.y, h.pl.z - 1.0f);
+    else {
+      float lxy = __builtin_sqrtf(__builtin_fmaf(h.pl.y, h.pl.y, h.pl.x * h.pl.x));
+      q = add(h.pl, mk(h.pl.x, h.pl.y, lxy / 2.0f));
+    }
+  } else {   // CODE_QUAD
+    q = add(h.pl, mk(0.0f, 0.0f, 1.0f));
+  }
+  N = normalize3(sub(xpoint(t0, t1, t2, q), P));
+}
+
+// sample_hemisphere + random_ray tp/montecarlo.frag:49-89
+__device__ __forceinline__ f3 random_ray(Rng& rng, f3 D, float roughness) {
+  f3 W = normalize3(mk(D.x, D.y + 5.0f, D.z + 3.0f));
+  f3 U = normalize3(cross3(D, W));
+  f3 V = normalize3(cross3(D, U));
+  float alpha = roughness * roughness;
+  float beta = (2.0f * kPI) * rnd(rng);
+  float tanTheta2 = ((-alpha) * alpha) * mc_log(1.0f - rnd(rng));
+  float cosTheta = 1.0f / __builtin_sqrtf(1.0f + tanTheta2);
+  float sinTheta = __builtin_sqrtf(gmax(0.0f, 1.0f - cosTheta * cosTheta));
+  float sb, cb;
+  mc_sincos(beta, sb, cb);
+  f3 sm = normalize3(mk(cb * sinTheta, sb * sinTheta, cosTheta));
+  f3 m = mk(__builtin_fmaf(D.x, sm.z, __builtin_fmaf(V.x, sm.y, U.x * sm.x)),
+            __builtin_fmaf(D.y, sm.z, __builtin_fmaf(V.y, sm.y, U.y * sm.x)),
+            __builtin_fmaf(D.z, sm.z, __builtin_fmaf(V.z, sm.y, U.z * sm.x)));
+  return normalize3(m);
+}
+
+__device__ __forceinline__ float schlick(float ior, f3 I, f3 N) {   // :91-98
+  float r0 = (ior - 1.0f) / (ior + 1.0f);
+  r0 *= r0;
+  float x = 1.0f - dot3(N, I);
+  return gclamp(r0 + ((((1.0f - r0) * x) * x * x) * x) * x, 0.0f, 1.0f);
+}
+
+// ------------------------------------------------------------------------------------
+// the kernel
+// ------------------------------------------------------------------------------------
+template <bool COUNT>
+__global__ __launch_bounds__(256) void render_kernel(RenderParams p) {
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+  const int lr = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+  if (x >= p.W || lr >= p.n_local_rows) return;
+  const int y = ((lr / p.band_rows) * p.world + p.rank) * p.band_rows + (lr % p.band_rows);
+
+  SceneRef s{p.nodes, p.leaves, p.ptype, p.prims, p.depth};
+  Ev<COUNT> ev;
+  ev.init();
+
+  // raytracer.vert:9-22 corner rays, interpolated over the strip (v0,v1,v2) / (v1,v3,v2)
+  const float u = ((float)x + 0.5f) / (float)p.W;
+  const float v = ((float)y + 0.5f) / (float)p.H;
+  f3 dir;
+  {
+    const f3 d0 = mk(p.cd[0], p.cd[1], p.cd[2]), d1 = mk(p.cd[3], p.cd[4], p.cd[5]);
+    const f3 d2 = mk(p.cd[6], p.cd[7], p.cd[8]), d3 = mk(p.cd[9], p.cd[10], p.cd[11]);
+    if (u + v <= 1.0f) {
+      float w0 = (1.0f - u) - v;
+      dir = add(add(muls(d0, w0), muls(d1, u)), muls(d2, v));
+    } else {
+      float w1 = 1.0f - v, w3 = (u + v) - 1.0f, w2 = 1.0f - u;
+      dir = add(add(muls(d1, w1), muls(d3, w3)), muls(d2, w2));
+    }
+  }
+  const f3 Dcam = normalize3(dir);
+  const f3 Ocam = mk(p.ox, p.oy, p.oz);
+
+  float* accp = p.accum + ((size_t)lr * p.W + x) * 3;
+  float acc0 = accp[0], acc1 = accp[1], acc2 = accp[2];
+
+  const float ior = p.ior;
+  const int B = p.bounces;
+  int pass = 0;
+  // path state
+  Rng rng = seed_for(u, v, p.first_pass, p.date);
+  f3 O = Ocam, D = Dcam, att = mk(0.8f, 0.8f, 0.8f), total = mk(0.0f, 0.0f, 0.0f);
+  f3 N = mk(0.0f, 0.0f, 0.0f), P = mk(0.0f, 0.0f, 0.0f), natt = att;
+  int bounce = 0, phase = 0;
+  Hit h;
+  h.pl = mk(0.0f, 0.0f, 0.0f); h.pg = h.pl; h.dist = kFLTMAX; h.index = -1; h.shape = -1; h.dir = -1;
+
+  while (pass < p.n_passes) {
+    bool done = false;
+    f3 res = mk(0.0f, 0.0f, 0.0f);
+    if (p.variant == 0 && B <= 0) {
+      done = true;   // for(i=0; i<NB_BOUNCES ...) never runs: black
+    } else {
+      traverse<COUNT>(s, O, D, h, ev);
+      if (p.variant != 0) {
+        // tp/montecarlo_mat.frag:5-20 / montecarlo_mat_tr.frag:5-20
+        if (h.shape < 0) {
+          res = mk(0.0f, 0.0f, 0.2f);
+        } else {
+          geom_info<COUNT>(s, h, N, P, ev);
+          ev.inc(EV_COLMAT);
+          if (p.variant == 1) {
+            float rx = rnd(rng), ry = rnd(rng), rz = rnd(rng);
+            res = mk(__builtin_fabsf(N.x) * rx, __builtin_fabsf(N.y) * ry, __builtin_fabsf(N.z) * rz);
+          } else {
+            float4 col = s.prims[(size_t)h.index * 8 + 6];
+            float r = rnd(rng);
+            res = mk(col.x * r, col.y * r, col.z * r);
+          }
+        }
+        done = true;
+      } else if (phase == 0) {
+        // tp/montecarlo.frag:100-179, one bounce
+        if (h.shape < 0) {
+          float a = gmax(0.0f, D.z);
+          res = add(total, mulv(att, gmix3(mk(0.5f, 0.5f, 0.9f), mk(1.0f, 1.0f, 0.8f), a)));
+          done = true;
+        } else {
+          geom_info<COUNT>(s, h, N, P, ev);
+          ev.inc(EV_COLMAT);
+          const float4 c4 = s.prims[(size_t)h.index * 8 + 6];
+          const float4 m4 = s.prims[(size_t)h.index * 8 + 7];
+          const f3 col = mk(c4.x, c4.y, c4.z);
+          const float alpha = c4.w;
+          f3 ray = random_ray(rng, N, 1.0f - m4.y);
+          float rs = schlick(ior, D, N);
+          f3 R = greflect(neg(ray), N);
+          f3 E = normalize3(sub(O, P));
+          float se = gmix(100.0f, 2.0f, m4.y);
+          float spec = mc_pow(gmax(0.0f, dot3(E, R)), se);
+          total = add(total, add(muls(col, 0.1f), muls(muls(muls(att, m4.z), 1.0f - m4.x), alpha)));
+          if (m4.z <= 0.5f) {
+            const f3 mx = gmix3(att, col, m4.x);
+            const f3 base = mulv(col, att);
+            bool reflect_push = false, inner = false;
+            if (m4.x > 0.0f && alpha == 1.0f) {
+              reflect_push = true;
+            } else if (alpha < 1.0f && m4.x == 0.0f) {
+              inner = true;
+              natt = add(base, mulv(muls(muls(muls(att, 1.0f - alpha), 1.0f - rs), spec), mx));
+              O = sub(P, muls(N, kBIAS));
+              D = grefract(D, N, ior);
+            } else if (alpha < 1.0f && m4.x > 0.0f) {
+              float r = rnd(rng);
+              if (r > 0.5f) {
+                reflect_push = true;
+              } else {
+                inner = true;
+                natt = add(base, mulv(muls(muls(muls(att, 1.0f - alpha), 1.0f - rs), spec), mx));
+                O = sub(P, muls(N, kBIAS));
+              }
+            } else {   // diffuse
+              att = add(base, mulv(muls(att, spec), mx));
+              O = add(P, muls(N, kBIAS));
+              D = ray;
+              bounce++;
+            }
+            if (reflect_push) {
+              f3 na = add(base, mulv(muls(muls(muls(att, alpha), rs), spec), mx));
+              f3 rd = random_ray(rng, greflect(D, N), 1.0f - m4.x * m4.y);
+              att = na;
+              O = add(P, muls(N, kBIAS));
+              D = rd;
+              bounce++;
+            }
+            if (inner) phase = 1;
+            else if (bounce >= B) done = true;   // budget exhausted: black (res = 0)
+          } else {
+            res = total;                          // emissive: end of path
+            done = true;
+          }
+        }
+      } else {
+        // inner traversal of the refraction branches (montecarlo.frag:148-152 / 162-165)
+        if (h.shape >= 0) geom_info<COUNT>(s, h, N, P, ev);
+        O = add(P, muls(N, kBIAS));
+        D = grefract(D, neg(N), 1.0f / ior);
+        att = natt;
+        phase = 0;
+        bounce++;
+        if (bounce >= B) done = true;
+      }
+    }
+    if (done) {
+      acc0 = acc0 + res.x; acc1 = acc1 + res.y; acc2 = acc2 + res.z;
+      ev.inc(EV_SAMPLE);
+      pass++;
+      rng = seed_for(u, v, p.first_pass + pass, p.date);
+      O = Ocam; D = Dcam; att = mk(0.8f, 0.8f, 0.8f); total = mk(0.0f, 0.0f, 0.0f);
+      bounce = 0; phase = 0;
+    }
+  }
+  accp[0] = acc0; accp[1] = acc1; accp[2] = acc2;
+
+  if (COUNT) {
+#pragma unroll
+    for (int e = 0; e < EV_COUNT; ++e) {
+      unsigned long long vsum = ev.c.v[e];
+      for (int off = 32; off > 0; off >>= 1) vsum += __shfl_xor(vsum, off);
+      if (lane == 0) atomicAdd(p.events + e, vsum);
+    }
+  }
+}
+
+}  // namespace mcpt
+
+// ------------------------------------------------------------------------------------
+// launch wrapper (host)
+// ------------------------------------------------------------------------------------
+hipError_t mcpt_launch_render(const mcpt::RenderParams& p, bool count, hipStream_t stream) {
+  dim3 block(256);
+  dim3 grid((p.W + 15) / 16, (p.n_local_rows + 15) / 16);
+  if (grid.x == 0 || grid.y == 0) return hipSuccess;
+  if (count) hipLaunchKernelGGL(mcpt::render_kernel<true>, grid, block, 0, stream, p);
+  else hipLaunchKernelGGL(mcpt::render_kernel<false>, grid, block, 0, stream, p);
+  return hipGetLastError();
+}

@@ -1,0 +1,168 @@
+// mcpt_math.h — binary32 arithmetic contract of the path tracer.
+//
+// Everything the integrator computes goes through these helpers so that the
+// HIP kernel reproduces, bit for bit, the CPU restatement in oracle/ (which
+// implements the same contract independently).  Rules:
+//   * IEEE-754 binary32, round-to-nearest, built with -ffp-contract=off;
+//   * dot products and matrix·vector products are explicit fmaf chains in
+//     component order (x, then y, then z, then the translation column);
+//   * sqrt and '/' are the correctly-rounded HIP defaults;
+//   * normalize(v) = v * (1/sqrt(dot(v,v)));
+//   * sin/cos/log/exp2/pow are the fixed polynomial algorithms below (GLSL leaves
+//     their precision to the driver; ours are ≤ a few ulp and reproducible);
+//   * GLSL min/max/clamp keep the GLSL definitions (max(x,y) = x<y ? y : x).
+// Reference semantics: shaders/raytracer_func.frag, tp/montecarlo.frag (GLSL 4.30).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mcpt {
+
+struct f3 { float x, y, z; };
+__device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
+__device__ __forceinline__ f3 add(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ f3 sub(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ f3 mulv(f3 a, f3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ f3 muls(f3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ f3 neg(f3 a) { return mk(-a.x, -a.y, -a.z); }
+
+__device__ __forceinline__ float dot3(f3 a, f3 b) { return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x)); }
+__device__ __forceinline__ f3 normalize3(f3 a) { float r = 1.0f / __builtin_sqrtf(dot3(a, a)); return muls(a, r); }
+__device__ __forceinline__ float length3(f3 a) { return __builtin_sqrtf(dot3(a, a)); }
+__device__ __forceinline__ f3 cross3(f3 a, f3 b) {
+  return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ float gmax(float x, float y) { return (x < y) ? y : x; }
+__device__ __forceinline__ float gmin(float x, float y) { return (y < x) ? y : x; }
+__device__ __forceinline__ float gclamp(float x, float a, float b) { return gmin(gmax(x, a), b); }
+__device__ __forceinline__ float gmix(float x, float y, float a) { return x * (1.0f - a) + y * a; }
+__device__ __forceinline__ f3 gmix3(f3 x, f3 y, float a) { return mk(gmix(x.x, y.x, a), gmix(x.y, y.y, a), gmix(x.z, y.z, a)); }
+__device__ __forceinline__ f3 greflect(f3 I, f3 N) { return sub(I, muls(N, 2.0f * dot3(N, I))); }
+__device__ __forceinline__ f3 grefract(f3 I, f3 N, float eta) {
+  float d = dot3(N, I);
+  float k = 1.0f - (eta * eta) * (1.0f - d * d);
+  if (k < 0.0f) return mk(0.0f, 0.0f, 0.0f);
+  return sub(muls(I, eta), muls(N, eta * d + __builtin_sqrtf(k)));
+}
+
+// 3x4 affine rows (row r = (m[r], m[4+r], m[8+r], m[12+r]) of a column-major mat4)
+__device__ __forceinline__ f3 xpoint(float4 r0, float4 r1, float4 r2, f3 p) {
+  return mk(__builtin_fmaf(r0.z, p.z, __builtin_fmaf(r0.y, p.y, r0.x * p.x)) + r0.w,
+            __builtin_fmaf(r1.z, p.z, __builtin_fmaf(r1.y, p.y, r1.x * p.x)) + r1.w,
+            __builtin_fmaf(r2.z, p.z, __builtin_fmaf(r2.y, p.y, r2.x * p.x)) + r2.w);
+}
+__device__ __forceinline__ f3 xdir(float4 r0, float4 r1, float4 r2, f3 d) {
+  return mk(__builtin_fmaf(r0.z, d.z, __builtin_fmaf(r0.y, d.y, r0.x * d.x)),
+            __builtin_fmaf(r1.z, d.z, __builtin_fmaf(r1.y, d.y, r1.x * d.x)),
+            __builtin_fmaf(r2.z, d.z, __builtin_fmaf(r2.y, d.y, r2.x * d.x)));
+}
+
+__device__ __forceinline__ uint32_t fbits(float f) { return __float_as_uint(f); }
+__device__ __forceinline__ float bitsf(uint32_t u) { return __uint_as_float(u); }
+
+constexpr float kPI = 3.14159274101257324f;   // 2*acos(0) in binary32 (raytracer_func.frag:9)
+constexpr float kEPS = 1e-10f;                // EPSILON raytracer_func.frag:13
+constexpr float kBIAS = 1e-2f;                // BIAS raytracer_func.frag:14
+constexpr float kFLTMAX = 3.402823e38f;       // FLT_MAX raytracer_func.frag:8
+
+// sin/cos: Cody-Waite reduction by pi/2, minimax polynomials on [-pi/4, pi/4]
+__device__ __forceinline__ void mc_sincos(float x, float& s_out, float& c_out) {
+  float t = x * 0.636619746685028076f;
+  float qf = __builtin_floorf(t + 0.5f);
+  int q = (int)qf;
+  float r = __builtin_fmaf(-qf, 1.57079637050628662f, x);
+  r = __builtin_fmaf(-qf, -4.37113900018624283e-8f, r);
+  r = __builtin_fmaf(-qf, -1.71512451e-15f, r);
+  float s = r * r;
+  float sp = __builtin_fmaf(__builtin_fmaf(-1.9515295891e-4f, s, 8.3321608736e-3f), s, -1.6666654611e-1f);
+  float sn = __builtin_fmaf(r * s, sp, r);
+  float cp = __builtin_fmaf(__builtin_fmaf(2.443315711809948e-5f, s, -1.388731625493765e-3f), s, 4.166664568298827e-2f);
+  float cs = __builtin_fmaf(s * s, cp, __builtin_fmaf(-0.5f, s, 1.0f));
+  int qq = q & 3;
+  float a = (qq & 1) ? cs : sn;      // sin candidate
+  float b = (qq & 1) ? sn : cs;      // cos candidate
+  s_out = (qq & 2) ? -a : a;
+  c_out = ((qq + 1) & 2) ? -b : b;
+}
+
+// natural log (x > 0 finite expected; 0 -> -inf, <0/NaN -> NaN)
+__device__ __forceinline__ float mc_log(float x) {
+  if (!(x > 0.0f)) return (x == 0.0f) ? -__builtin_inff() : __builtin_nanf("");
+  if (x == __builtin_inff()) return x;
+  uint32_t b = fbits(x);
+  int e = 0;
+  if (b < 0x00800000u) { x = x * 8388608.0f; b = fbits(x); e = -23; }
+  e += (int)(b >> 23) - 127;
+  float m = bitsf((b & 0x007FFFFFu) | 0x3F800000u);
+  if (m > 1.41421353816986084f) { m = m * 0.5f; e += 1; }
+  float f = m - 1.0f;
+  float z = f * f;
+  float p = 7.0376836292e-2f;
+  p = __builtin_fmaf(p, f, -1.1514610310e-1f);
+  p = __builtin_fmaf(p, f, 1.1676998740e-1f);
+  p = __builtin_fmaf(p, f, -1.2420140846e-1f);
+  p = __builtin_fmaf(p, f, 1.4249322787e-1f);
+  p = __builtin_fmaf(p, f, -1.6668057665e-1f);
+  p = __builtin_fmaf(p, f, 2.0000714765e-1f);
+  p = __builtin_fmaf(p, f, -2.4999993993e-1f);
+  p = __builtin_fmaf(p, f, 3.3333331174e-1f);
+  float ef = (float)e;
+  float y = (f * z) * p;
+  y = __builtin_fmaf(ef, -2.12194440e-4f, y);
+  y = __builtin_fmaf(-0.5f, z, y);
+  float r = f + y;
+  return __builtin_fmaf(ef, 0.693359375f, r);
+}
+
+__device__ __forceinline__ float mc_exp2(float x) {
+  if (x != x) return x;
+  if (x >= 128.0f) return __builtin_inff();
+  if (x < -150.0f) return 0.0f;
+  float kf = __builtin_floorf(x + 0.5f);
+  float f = x - kf;
+  float p = 1.535336188319500e-4f;
+  p = __builtin_fmaf(p, f, 1.339887440266574e-3f);
+  p = __builtin_fmaf(p, f, 9.618437357674640e-3f);
+  p = __builtin_fmaf(p, f, 5.550332471162809e-2f);
+  p = __builtin_fmaf(p, f, 2.402264791363012e-1f);
+  p = __builtin_fmaf(p, f, 6.931472028550421e-1f);
+  float r = __builtin_fmaf(p, f, 1.0f);
+  int k = (int)kf;
+  if (k >= -126) return r * bitsf((uint32_t)(k + 127) << 23);
+  return (r * bitsf((uint32_t)(k + 127 + 64) << 23)) * 5.42101086242752217e-20f;
+}
+
+__device__ __forceinline__ float mc_pow(float x, float y) {
+  return mc_exp2(y * (mc_log(x) * 1.44269502162933350f));
+}
+
+// xxhash32 RNG — raytracer_func.frag:90-124
+__device__ __forceinline__ uint32_t xxhash32(uint32_t px, uint32_t py, uint32_t pz) {
+  uint32_t h = pz + 374761393u + px * 3266489917u;
+  h = 668265263u * ((h << 17) | (h >> 15));
+  h += py * 3266489917u;
+  h = 668265263u * ((h << 17) | (h >> 15));
+  h = 2246822519u * (h ^ (h >> 15));
+  h = 3266489917u * (h ^ (h >> 13));
+  return h ^ (h >> 16);
+}
+
+struct Rng { uint32_t x, y, z; };
+__device__ __forceinline__ float rnd(Rng& s) {
+  uint32_t m = xxhash32(s.x, s.y, s.z);
+  float f = bitsf((m & 0x007FFFFFu) | 0x3F800000u);
+  s.x += 11u; s.y += 43u; s.z += 67u;
+  return f - 1.0f;
+}
+// srand raytracer_func.frag:105-110
+__device__ __forceinline__ Rng seed_for(float tcx, float tcy, int np, float date) {
+  float f = (float)(1 + np);
+  float mid = (float)np * 3.14f + date;
+  Rng r;
+  r.x = fbits((tcx * f) * 1.125f);
+  r.y = fbits((mid * f) * 1.125f);
+  r.z = fbits((tcy * f) * 1.125f);
+  return r;
+}
+
+}  // namespace mcpt

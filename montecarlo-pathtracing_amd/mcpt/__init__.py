@@ -1,0 +1,337 @@
+"""mcpt — host-side mirror of the reference's render-path API over the libmcpt C ABI.
+
+The product is ``libmcpt.so`` (HIP kernels for gfx950 + C ABI + C++ scene producer,
+``../csrc``).  This module is a thin ctypes binding that mirrors the reference's
+host interface for the hot path so a user of ``MontecarloGPU/montecarlo.cpp`` finds
+the same objects:
+
+* :class:`Scene`     — ``ScenePrimitives`` + ``BVH_GPU_Scene`` (add_*/finalize/depth/
+  nb_prim/nb_emissives; bvh_gpu/gpu_bvh_scene.h:35-121) and the 8 reference scenes
+  (montecarlo.cpp:629-795);
+* :class:`Renderer`  — the GL program + RGB32F accumulation FBO of ``RTViewer``
+  (montecarlo.cpp:384-386, 408-477): upload, passes, read-back, average;
+* :func:`camera_canonical` — the default camera (camera.cpp:53-95, montecarlo.cpp:405).
+
+There is no CPU fallback: if ``libmcpt.so`` is missing or the GPU is absent, the
+calls raise :class:`MCPTError`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+
+__all__ = [
+    "MCPTError", "lib", "lib_path", "Scene", "Renderer", "camera_canonical",
+    "MONTECARLO", "MAT", "MAT_TR", "EVENT_NAMES", "SCENE_KEYS",
+]
+
+MONTECARLO, MAT, MAT_TR = 0, 1, 2
+EVENT_NAMES = ("node", "leaf", "prim", "cand", "geom", "colmat", "sample", "trav")
+# key bindings of montecarlo.cpp:251-290: scene id -> key
+SCENE_KEYS = {1: "Q", 2: "W", 3: "E", 4: "R", 5: "T", 6: "Y", 7: "U", 8: "I"}
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+class MCPTError(RuntimeError):
+    pass
+
+
+def lib_path() -> str:
+    return os.environ.get("MCPT_LIB", os.path.join(_HERE, "libmcpt.so"))
+
+
+_lib: Optional[ctypes.CDLL] = None
+_c_float_p = ctypes.POINTER(ctypes.c_float)
+_c_int_p = ctypes.POINTER(ctypes.c_int)
+_c_u64_p = ctypes.POINTER(ctypes.c_ulonglong)
+_vp = ctypes.c_void_p
+
+
+def _declare(L: ctypes.CDLL) -> None:
+    i, f, fp, ip = ctypes.c_int, ctypes.c_float, _c_float_p, _c_int_p
+    sig = {
+        "mcpt_error_string": (ctypes.c_char_p, [i]),
+        "mcpt_version": (i, []),
+        "mcpt_create": (i, [i, ctypes.POINTER(_vp)]),
+        "mcpt_destroy": (i, [_vp]),
+        "mcpt_upload_scene": (i, [_vp, fp, i, fp, ip, i, i]),
+        "mcpt_set_target": (i, [_vp, i, i, i, i, i]),
+        "mcpt_local_rows": (i, [_vp, ip]),
+        "mcpt_render": (i, [_vp, fp, fp, i, i, f, i, f, i]),
+        "mcpt_render_counted": (i, [_vp, fp, fp, i, i, f, i, f, i, _c_u64_p]),
+        "mcpt_event_bytes": (i, [i]),
+        "mcpt_read_accum": (i, [_vp, fp, ip]),
+        "mcpt_clear_accum": (i, [_vp]),
+        "mcpt_accum_device_ptr": (i, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(ctypes.c_size_t)]),
+        "mcpt_set_stream": (i, [_vp, _vp]),
+        "mcpt_synchronize": (i, [_vp]),
+        "mcpt_last_render_ms": (i, [_vp, fp]),
+        "mcpt_scene_create": (i, [ctypes.POINTER(_vp)]),
+        "mcpt_scene_destroy": (i, [_vp]),
+        "mcpt_scene_clear": (i, [_vp]),
+        "mcpt_scene_add_sphere": (i, [_vp, fp, fp]),
+        "mcpt_scene_add_cube": (i, [_vp, fp, fp]),
+        "mcpt_scene_add_cylinder": (i, [_vp, fp, fp]),
+        "mcpt_scene_add_cone": (i, [_vp, fp, fp]),
+        "mcpt_scene_add_oriented_quad": (i, [_vp, fp, fp]),
+        "mcpt_scene_finalize": (i, [_vp]),
+        "mcpt_scene_nb_prim": (i, [_vp, ip]),
+        "mcpt_scene_depth": (i, [_vp, ip]),
+        "mcpt_scene_nb_emissives": (i, [_vp, ip]),
+        "mcpt_scene_get_buffers": (i, [_vp, fp, fp, ip]),
+        "mcpt_scene_set_material": (i, [_vp, i, fp]),
+        "mcpt_scene_build_reference": (i, [_vp, i, f]),
+        "mcpt_camera_canonical": (i, [i, i, fp, fp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+
+
+def lib() -> ctypes.CDLL:
+    """Load libmcpt.so (fails loudly: there is no fallback implementation)."""
+    global _lib
+    if _lib is None:
+        path = lib_path()
+        if not os.path.exists(path):
+            raise MCPTError(f"libmcpt.so not found at {path}: build it with "
+                            "`python -c 'import __graft_entry__ as g; g.build()'` or `make -C "
+                            "montecarlo-pathtracing_amd/csrc`")
+        L = ctypes.CDLL(path)
+        _declare(L)
+        _lib = L
+    return _lib
+
+
+def _check(status: int, what: str) -> None:
+    if status != 0:
+        msg = lib().mcpt_error_string(status).decode()
+        raise MCPTError(f"{what} failed ({status}): {msg}")
+
+
+def _fp(a: np.ndarray):
+    return a.ctypes.data_as(_c_float_p)
+
+
+def _ip(a: np.ndarray):
+    return a.ctypes.data_as(_c_int_p)
+
+
+def _f32(a, n: int) -> np.ndarray:
+    arr = np.ascontiguousarray(np.asarray(a, dtype=np.float32).reshape(-1))
+    if arr.size != n:
+        raise ValueError(f"expected {n} floats, got {arr.size}")
+    return arr
+
+
+def material(rgba: Sequence[float], shininess: float = 0.0, roughness: float = 0.0,
+             emissivity: float = 0.0) -> np.ndarray:
+    """Material (bvh_gpu/scene.h:30-49) packed as the 7 floats the C ABI takes."""
+    return np.array(list(rgba) + [shininess, roughness, emissivity], dtype=np.float32)
+
+
+def light(rgba: Sequence[float], emissivity: float) -> np.ndarray:
+    """Material::light (scene.h:48)."""
+    return material(rgba, 0.0, 0.0, emissivity)
+
+
+class Scene:
+    """ScenePrimitives + BVH_GPU_Scene (host side, C++ in libmcpt)."""
+
+    def __init__(self) -> None:
+        h = _vp()
+        _check(lib().mcpt_scene_create(ctypes.byref(h)), "mcpt_scene_create")
+        self._h = h
+
+    def __del__(self) -> None:
+        h = getattr(self, "_h", None)
+        if h and _lib is not None:
+            _lib.mcpt_scene_destroy(h)
+            self._h = None
+
+    @classmethod
+    def reference(cls, scene_id: int, light_intensity: float = 1.2) -> "Scene":
+        """Build one of the 8 scenes of montecarlo.cpp (keys Q..I → 1..8), finalized."""
+        s = cls()
+        _check(lib().mcpt_scene_build_reference(s._h, int(scene_id), float(light_intensity)),
+               f"mcpt_scene_build_reference({scene_id})")
+        return s
+
+    def clear(self) -> None:
+        _check(lib().mcpt_scene_clear(self._h), "mcpt_scene_clear")
+
+    def _add(self, fn: str, trf, mat) -> None:
+        t = _f32(trf, 16)
+        m = _f32(mat, 7)
+        _check(getattr(lib(), fn)(self._h, _fp(t), _fp(m)), fn)
+
+    # transforms are 4x4 column-major (GL / Eigen storage); a (4,4) numpy array in
+    # row-major math convention is accepted and transposed to column-major storage.
+    @staticmethod
+    def _colmajor(trf) -> np.ndarray:
+        a = np.asarray(trf, dtype=np.float32)
+        return a.T.reshape(-1) if a.shape == (4, 4) else a.reshape(-1)
+
+    def add_sphere(self, trf, mat) -> None:
+        self._add("mcpt_scene_add_sphere", self._colmajor(trf), mat)
+
+    def add_cube(self, trf, mat) -> None:
+        self._add("mcpt_scene_add_cube", self._colmajor(trf), mat)
+
+    def add_cylinder(self, trf, mat) -> None:
+        self._add("mcpt_scene_add_cylinder", self._colmajor(trf), mat)
+
+    def add_cone(self, trf, mat) -> None:
+        self._add("mcpt_scene_add_cone", self._colmajor(trf), mat)
+
+    def add_oriented_quad(self, trf, mat) -> None:
+        self._add("mcpt_scene_add_oriented_quad", self._colmajor(trf), mat)
+
+    add_orientedQuad = add_oriented_quad   # reference spelling (gpu_bvh_scene.h:103)
+
+    def finalize(self) -> None:
+        _check(lib().mcpt_scene_finalize(self._h), "mcpt_scene_finalize")
+
+    def nb_prim(self) -> int:
+        n = ctypes.c_int()
+        _check(lib().mcpt_scene_nb_prim(self._h, ctypes.byref(n)), "mcpt_scene_nb_prim")
+        return n.value
+
+    def depth(self, i: int = 0) -> int:
+        d = ctypes.c_int()
+        _check(lib().mcpt_scene_depth(self._h, ctypes.byref(d)), "mcpt_scene_depth")
+        return d.value
+
+    def nb_emissives(self) -> int:
+        n = ctypes.c_int()
+        _check(lib().mcpt_scene_nb_emissives(self._h, ctypes.byref(n)), "mcpt_scene_nb_emissives")
+        return n.value
+
+    def buffers(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """(prims n×64 f32, nodes (2^(d+1)-1)×6 f32, leaves 2^d i32) — texture layouts."""
+        n, d = self.nb_prim(), self.depth()
+        prims = np.zeros((n, 64), np.float32)
+        nodes = np.zeros((2 ** (d + 1) - 1, 6), np.float32)
+        leaves = np.zeros(2 ** d, np.int32)
+        _check(lib().mcpt_scene_get_buffers(self._h, _fp(prims), _fp(nodes), _ip(leaves)),
+               "mcpt_scene_get_buffers")
+        return prims, nodes, leaves
+
+    def set_material(self, prim: int, mat) -> None:
+        m = _f32(mat, 7)
+        _check(lib().mcpt_scene_set_material(self._h, int(prim), _fp(m)), "mcpt_scene_set_material")
+
+
+def camera_canonical(W: int, H: int) -> Tuple[np.ndarray, np.ndarray]:
+    """(invPV, invV) of the default camera at aspect W/H, 16 f32 column-major each."""
+    ipv = np.zeros(16, np.float32)
+    iv = np.zeros(16, np.float32)
+    _check(lib().mcpt_camera_canonical(int(W), int(H), _fp(ipv), _fp(iv)), "mcpt_camera_canonical")
+    return ipv, iv
+
+
+class Renderer:
+    """Device context: scene on the GPU, row-band framebuffer, pass accumulation."""
+
+    def __init__(self, device: int = 0) -> None:
+        h = _vp()
+        _check(lib().mcpt_create(int(device), ctypes.byref(h)), "mcpt_create")
+        self._h = h
+        self.W = self.H = 0
+        self.band_rows, self.world, self.rank = 1, 1, 0
+        self.n_local_rows = 0
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().mcpt_destroy(self._h)
+            self._h = None
+
+    def __del__(self) -> None:
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def upload_scene(self, scene: Optional[Scene] = None, prims=None, nodes=None, leaves=None,
+                     depth: Optional[int] = None, nb_emissives: int = 0) -> None:
+        if scene is not None:
+            prims, nodes, leaves = scene.buffers()
+            depth = scene.depth()
+            nb_emissives = scene.nb_emissives()
+        prims = np.ascontiguousarray(prims, dtype=np.float32)
+        nodes = np.ascontiguousarray(nodes, dtype=np.float32)
+        leaves = np.ascontiguousarray(leaves, dtype=np.int32)
+        n = prims.size // 64
+        _check(lib().mcpt_upload_scene(self._h, _fp(prims), int(n), _fp(nodes), _ip(leaves),
+                                       int(depth), int(nb_emissives)), "mcpt_upload_scene")
+
+    def set_target(self, W: int, H: int, band_rows: int = 8, world: int = 1, rank: int = 0) -> None:
+        _check(lib().mcpt_set_target(self._h, int(W), int(H), int(band_rows), int(world), int(rank)),
+               "mcpt_set_target")
+        self.W, self.H = int(W), int(H)
+        self.band_rows, self.world, self.rank = int(band_rows), int(world), int(rank)
+        n = ctypes.c_int()
+        _check(lib().mcpt_local_rows(self._h, ctypes.byref(n)), "mcpt_local_rows")
+        self.n_local_rows = n.value
+
+    def local_row_ids(self) -> np.ndarray:
+        y = np.arange(self.H)
+        return y[(y // self.band_rows) % self.world == self.rank]
+
+    def render(self, invPV, invV, first_pass: int, n_passes: int, date: float = 0.0,
+               bounces: int = 3, refract_ind: float = 1.0, variant: int = MONTECARLO) -> None:
+        a, b = _f32(invPV, 16), _f32(invV, 16)
+        _check(lib().mcpt_render(self._h, _fp(a), _fp(b), int(first_pass), int(n_passes), float(date),
+                                 int(bounces), float(refract_ind), int(variant)), "mcpt_render")
+
+    def render_counted(self, invPV, invV, first_pass: int, n_passes: int, date: float = 0.0,
+                       bounces: int = 3, refract_ind: float = 1.0, variant: int = MONTECARLO) -> np.ndarray:
+        a, b = _f32(invPV, 16), _f32(invV, 16)
+        ev = np.zeros(len(EVENT_NAMES), np.uint64)
+        _check(lib().mcpt_render_counted(self._h, _fp(a), _fp(b), int(first_pass), int(n_passes),
+                                         float(date), int(bounces), float(refract_ind), int(variant),
+                                         ev.ctypes.data_as(_c_u64_p)), "mcpt_render_counted")
+        return ev
+
+    @staticmethod
+    def event_bytes() -> np.ndarray:
+        return np.array([lib().mcpt_event_bytes(e) for e in range(len(EVENT_NAMES))], np.int64)
+
+    def read_accum(self) -> Tuple[np.ndarray, int]:
+        """(local rows × W × 3 f32 sums, pass count)."""
+        out = np.zeros((self.n_local_rows, self.W, 3), np.float32)
+        pc = ctypes.c_int()
+        _check(lib().mcpt_read_accum(self._h, _fp(out), ctypes.byref(pc)), "mcpt_read_accum")
+        return out, pc.value
+
+    def read_image(self) -> np.ndarray:
+        """Averaged image (fs_frag: accum / nb, montecarlo.cpp:59-70); single-shard only."""
+        acc, n = self.read_accum()
+        if self.world != 1:
+            raise MCPTError("read_image needs the full frame; gather shards with mcpt.dist")
+        return acc / max(n, 1)
+
+    def clear_accum(self) -> None:
+        _check(lib().mcpt_clear_accum(self._h), "mcpt_clear_accum")
+
+    def accum_device_ptr(self) -> Tuple[int, int]:
+        p = _vp()
+        n = ctypes.c_size_t()
+        _check(lib().mcpt_accum_device_ptr(self._h, ctypes.byref(p), ctypes.byref(n)), "mcpt_accum_device_ptr")
+        return int(p.value or 0), int(n.value)
+
+    def set_stream(self, hip_stream_ptr: int) -> None:
+        _check(lib().mcpt_set_stream(self._h, _vp(hip_stream_ptr)), "mcpt_set_stream")
+
+    def synchronize(self) -> None:
+        _check(lib().mcpt_synchronize(self._h), "mcpt_synchronize")
+
+    def last_render_ms(self) -> float:
+        ms = ctypes.c_float()
+        _check(lib().mcpt_last_render_ms(self._h, ctypes.byref(ms)), "mcpt_last_render_ms")
+        return ms.value

@@ -1,0 +1,163 @@
+"""ctypes binding of the CPU oracle (oracle/oracle.cpp).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() (as the checker)
+and bench.py's cpu_baseline leg (as the timed CPU baseline).  Never the product path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from typing import Tuple
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
+EV_NAMES = ("node", "leaf", "prim", "cand", "geom", "colmat", "sample", "trav")
+# bytes per event: node 48, leaf 4, prim 16+64, cand 64, geom 64, col+mat 32, sample 24
+EV_BYTES = np.array([48, 4, 80, 64, 64, 32, 24, 0], np.int64)
+
+_fp = ctypes.POINTER(ctypes.c_float)
+_ip = ctypes.POINTER(ctypes.c_int)
+_up = ctypes.POINTER(ctypes.c_uint)
+_u64p = ctypes.POINTER(ctypes.c_ulonglong)
+_vp = ctypes.c_void_p
+_L = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return LIB_PATH
+
+
+def lib() -> ctypes.CDLL:
+    global _L
+    if _L is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        i, f = ctypes.c_int, ctypes.c_float
+        sigs = {
+            "orc_scene_build": (_vp, [i, f]),
+            "orc_scene_free": (None, [_vp]),
+            "orc_scene_n_prims": (i, [_vp]),
+            "orc_scene_depth": (i, [_vp]),
+            "orc_scene_n_emissive": (i, [_vp]),
+            "orc_scene_export": (i, [_vp, _fp, _fp, _ip]),
+            "orc_camera": (None, [i, i, _fp, _fp]),
+            "orc_render": (i, [_fp, i, _fp, _ip, i, _fp, _fp, i, i, i, i, f, i, f, i, i, i, i, _fp, _u64p]),
+            "orc_xxhash32": (ctypes.c_uint, [ctypes.c_uint, ctypes.c_uint, ctypes.c_uint]),
+            "orc_srand": (None, [f, f, i, f, _up]),
+            "orc_random_floats": (None, [_up, i, _fp]),
+            "orc_sincos": (None, [f, _fp, _fp]),
+            "orc_log": (f, [f]),
+            "orc_exp2": (f, [f]),
+            "orc_pow": (f, [f, f]),
+            "orc_random_ray": (None, [_up, _fp, f, _fp, _up]),
+            "orc_intersect_prim": (i, [_fp, _fp, _fp, _fp, _ip, _fp, _fp]),
+            "orc_corner_rays": (None, [_fp, _fp, _fp]),
+        }
+        for name, (res, args) in sigs.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _L = L
+    return _L
+
+
+def P(a: np.ndarray, t=_fp):
+    return a.ctypes.data_as(t)
+
+
+def scene(scene_id: int, light_intensity: float = 1.2) -> Tuple[np.ndarray, np.ndarray, np.ndarray, int, int]:
+    """(prims n×64, nodes, leaves, depth, nb_emissive) built by the oracle's restatement."""
+    L = lib()
+    h = L.orc_scene_build(int(scene_id), float(light_intensity))
+    if not h:
+        raise ValueError(f"unknown scene {scene_id}")
+    try:
+        n, d, ne = L.orc_scene_n_prims(h), L.orc_scene_depth(h), L.orc_scene_n_emissive(h)
+        prims = np.zeros((n, 64), np.float32)
+        nodes = np.zeros((2 ** (d + 1) - 1, 6), np.float32)
+        leaves = np.zeros(2 ** d, np.int32)
+        L.orc_scene_export(h, P(prims), P(nodes), P(leaves, _ip))
+    finally:
+        L.orc_scene_free(h)
+    return prims, nodes, leaves, d, ne
+
+
+def camera(W: int, H: int) -> Tuple[np.ndarray, np.ndarray]:
+    ipv = np.zeros(16, np.float32)
+    iv = np.zeros(16, np.float32)
+    lib().orc_camera(int(W), int(H), P(ipv), P(iv))
+    return ipv, iv
+
+
+def render(prims, nodes, leaves, depth, invPV, invV, W, H, first_pass=1, n_passes=1, date=0.0,
+           bounces=3, ior=1.0, variant=0, row_step=1, row_offset=0, n_threads=0, accum=None):
+    """Accumulate passes into accum (H×W×3 f32, row 0 = bottom); returns (accum, events[8])."""
+    prims = np.ascontiguousarray(prims, np.float32)
+    nodes = np.ascontiguousarray(nodes, np.float32)
+    leaves = np.ascontiguousarray(leaves, np.int32)
+    invPV = np.ascontiguousarray(invPV, np.float32)
+    invV = np.ascontiguousarray(invV, np.float32)
+    if accum is None:
+        accum = np.zeros((H, W, 3), np.float32)
+    ev = np.zeros(8, np.uint64)
+    r = lib().orc_render(P(prims), prims.size // 64, P(nodes), P(leaves, _ip), int(depth), P(invPV), P(invV),
+                         int(W), int(H), int(first_pass), int(n_passes), float(date), int(bounces), float(ior),
+                         int(variant), int(row_step), int(row_offset), int(n_threads), P(accum), P(ev, _u64p))
+    if r != 0:
+        raise RuntimeError(f"orc_render failed ({r})")
+    return accum, ev
+
+
+def xxhash32(x: int, y: int, z: int) -> int:
+    return int(lib().orc_xxhash32(x, y, z))
+
+
+def srand(tcx: float, tcy: float, np_: int, date: float = 0.0) -> np.ndarray:
+    s = np.zeros(3, np.uint32)
+    lib().orc_srand(float(tcx), float(tcy), int(np_), float(date), P(s, _up))
+    return s
+
+
+def random_floats(seed3, n: int) -> np.ndarray:
+    s = np.ascontiguousarray(seed3, np.uint32)
+    out = np.zeros(n, np.float32)
+    lib().orc_random_floats(P(s, _up), int(n), P(out))
+    return out
+
+
+def sincos(x: float) -> Tuple[float, float]:
+    s, c = ctypes.c_float(), ctypes.c_float()
+    lib().orc_sincos(float(x), ctypes.byref(s), ctypes.byref(c))
+    return s.value, c.value
+
+
+def random_ray(seed3, D, roughness: float):
+    s = np.ascontiguousarray(seed3, np.uint32)
+    d = np.ascontiguousarray(D, np.float32)
+    out = np.zeros(3, np.float32)
+    so = np.zeros(3, np.uint32)
+    lib().orc_random_ray(P(s, _up), P(d), float(roughness), P(out), P(so, _up))
+    return out, so
+
+
+def intersect_prim(rec64, O, D):
+    rec = np.ascontiguousarray(rec64, np.float32)
+    o = np.ascontiguousarray(O, np.float32)
+    d = np.ascontiguousarray(D, np.float32)
+    dist = ctypes.c_float()
+    dr = ctypes.c_int()
+    pl = np.zeros(3, np.float32)
+    pg = np.zeros(3, np.float32)
+    shape = lib().orc_intersect_prim(P(rec), P(o), P(d), ctypes.byref(dist), ctypes.byref(dr), P(pl), P(pg))
+    return shape, dist.value, dr.value, pl, pg
+
+
+def corner_rays(invPV, invV) -> np.ndarray:
+    out = np.zeros(15, np.float32)
+    lib().orc_corner_rays(P(np.ascontiguousarray(invPV, np.float32)), P(np.ascontiguousarray(invV, np.float32)), P(out))
+    return out
