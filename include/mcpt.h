@@ -82,7 +82,11 @@ int mcpt_set_target(mcpt_ctx* ctx, int W, int H, int band_rows, int world, int r
 int mcpt_local_rows(mcpt_ctx* ctx, int* n_local_rows);
 
 /* Accumulate passes first_pass .. first_pass+n_passes-1 into the accumulator (the
- * glDrawArrays loop of montecarlo.cpp:454-466 with blend ONE/ONE).  Uniform ABI:
+ * glDrawArrays loop of montecarlo.cpp:454-466 with blend ONE/ONE).  Summation order
+ * (DESIGN.md §3.3): per pixel, passes are summed from 0 within each chunk of 32
+ * consecutive absolute pass numbers ((pass-1)/32), and chunk sums are added to the
+ * accumulator in chunk order — results are identical for any GPU count and for any
+ * split of a pass range into calls at multiples of 32.  Uniform ABI:
  * invPV(10), invV(6), numero_pass(4) = pass index, date(5), NB_BOUNCES(21),
  * refract_ind(24); variant = tp/ shader.  Asynchronous on the context's stream. */
 int mcpt_render(mcpt_ctx* ctx, const float* invPV, const float* invV, int first_pass,
@@ -103,6 +107,9 @@ int mcpt_clear_accum(mcpt_ctx* ctx);
 
 /* Device pointer of the local accumulator (for an RCCL gather by the caller). */
 int mcpt_accum_device_ptr(mcpt_ctx* ctx, void** dev_ptr, size_t* bytes);
+/* Device-to-device copy of the local accumulator into a caller buffer of >= bytes
+ * (e.g. a torch tensor that feeds the RCCL gather), ordered on the context's stream. */
+int mcpt_copy_accum_device(mcpt_ctx* ctx, void* dst_dev_ptr, size_t bytes);
 
 /* Use an external hipStream_t (e.g. torch's current stream); NULL = library stream. */
 int mcpt_set_stream(mcpt_ctx* ctx, void* hip_stream);
@@ -111,6 +118,9 @@ int mcpt_synchronize(mcpt_ctx* ctx);
 /* Device time (ms) of the kernel(s) of the last mcpt_render, from HIP events recorded
  * on the launch stream around the launch.  Synchronizes on the end event. */
 int mcpt_last_render_ms(mcpt_ctx* ctx, float* ms);
+/* The same interval split into the path-tracing kernel and the chunk-combine kernel
+ * (launches spanning more than one 32-pass accumulation chunk). */
+int mcpt_last_kernel_ms(mcpt_ctx* ctx, float* trace_ms, float* combine_ms);
 
 /* ---------------------------------------------------------------------------------
  * 2. host scene producer (BVH_GPU_Scene-compatible)

@@ -50,7 +50,9 @@ struct mcpt_ctx {
   int pass_count = 0;
   bool has_target = false;
   unsigned long long* d_events = nullptr;
-  hipEvent_t ev_start = nullptr, ev_stop = nullptr;
+  float* d_partial = nullptr;       // pass-segment sums (launches spanning > 1 chunk)
+  size_t partial_bytes = 0;
+  hipEvent_t ev_start = nullptr, ev_mid = nullptr, ev_stop = nullptr;
   bool timed = false;
 };
 
@@ -83,6 +85,7 @@ int mcpt_create(int device_ordinal, mcpt_ctx** out) {
   c->device = device_ordinal;
   hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&c->ev_start);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev_mid);
   if (e == hipSuccess) e = hipEventCreate(&c->ev_stop);
   if (e == hipSuccess) e = hipMalloc(&c->d_events, sizeof(unsigned long long) * mcpt::EV_COUNT);
   if (e != hipSuccess) { mcpt_destroy(c); return set_err(MCPT_ERR_HIP, "mcpt_create", e); }
@@ -104,7 +107,9 @@ int mcpt_destroy(mcpt_ctx* c) {
   free_scene(c);
   (void)hipFree(c->d_accum);
   (void)hipFree(c->d_events);
+  (void)hipFree(c->d_partial);
   if (c->ev_start) (void)hipEventDestroy(c->ev_start);
+  if (c->ev_mid) (void)hipEventDestroy(c->ev_mid);
   if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
@@ -241,9 +246,32 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   p.n_local_rows = c->n_local_rows; p.depth = c->depth;
   p.first_pass = first_pass; p.n_passes = n_passes; p.bounces = bounces; p.variant = variant;
   p.date = date; p.ior = refract_ind;
+  p.n_local_px = (long long)c->n_local_rows * c->W;
+  p.n_tiles = ((c->W + 15) / 16) * ((c->n_local_rows + 15) / 16);
+  p.n_segments = 0;
+  if (n_passes > 0) {
+    auto fdiv = [](int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); };
+    int c_first = fdiv(first_pass - 1, mcpt::kPassChunk);
+    int c_last = fdiv(first_pass + n_passes - 2, mcpt::kPassChunk);
+    p.n_segments = c_last - c_first + 1;
+  }
+  if (p.n_segments > 1) {
+    size_t need = (size_t)p.n_segments * (size_t)p.n_local_px * 3 * sizeof(float);
+    if (need > c->partial_bytes) {
+      HIP_OR_RETURN(hipStreamSynchronize(c->stream));
+      (void)hipFree(c->d_partial);
+      c->d_partial = nullptr;
+      c->partial_bytes = 0;
+      HIP_OR_RETURN(hipMalloc(&c->d_partial, need));
+      c->partial_bytes = need;
+    }
+  }
+  p.partial = c->d_partial;
   if (count) HIP_OR_RETURN(hipMemsetAsync(c->d_events, 0, sizeof(unsigned long long) * mcpt::EV_COUNT, c->stream));
   HIP_OR_RETURN(hipEventRecord(c->ev_start, c->stream));
   HIP_OR_RETURN(mcpt_launch_render(p, count, c->stream));
+  HIP_OR_RETURN(hipEventRecord(c->ev_mid, c->stream));
+  HIP_OR_RETURN(mcpt_launch_combine(p, c->stream));
   HIP_OR_RETURN(hipEventRecord(c->ev_stop, c->stream));
   c->timed = true;
   c->pass_count += n_passes;
@@ -291,6 +319,16 @@ int mcpt_accum_device_ptr(mcpt_ctx* c, void** dev_ptr, size_t* bytes) {
   return MCPT_OK;
 }
 
+int mcpt_copy_accum_device(mcpt_ctx* c, void* dst, size_t bytes) {
+  if (!c || (!dst && bytes)) return MCPT_ERR_INVALID_ARG;
+  if (!c->has_target) return MCPT_ERR_NO_TARGET;
+  if (bytes < c->accum_bytes) return set_err(MCPT_ERR_INVALID_ARG, "destination smaller than the accumulator");
+  HIP_OR_RETURN(hipSetDevice(c->device));
+  if (c->accum_bytes)
+    HIP_OR_RETURN(hipMemcpyAsync(dst, c->d_accum, c->accum_bytes, hipMemcpyDeviceToDevice, c->stream));
+  return MCPT_OK;
+}
+
 int mcpt_set_stream(mcpt_ctx* c, void* s) {
   if (!c) return MCPT_ERR_INVALID_ARG;
   HIP_OR_RETURN(hipSetDevice(c->device));
@@ -312,6 +350,16 @@ int mcpt_last_render_ms(mcpt_ctx* c, float* ms) {
   HIP_OR_RETURN(hipSetDevice(c->device));
   HIP_OR_RETURN(hipEventSynchronize(c->ev_stop));
   HIP_OR_RETURN(hipEventElapsedTime(ms, c->ev_start, c->ev_stop));
+  return MCPT_OK;
+}
+
+int mcpt_last_kernel_ms(mcpt_ctx* c, float* trace_ms, float* combine_ms) {
+  if (!c || !trace_ms || !combine_ms) return MCPT_ERR_INVALID_ARG;
+  if (!c->timed) return set_err(MCPT_ERR_INVALID_ARG, "no render timed yet");
+  HIP_OR_RETURN(hipSetDevice(c->device));
+  HIP_OR_RETURN(hipEventSynchronize(c->ev_stop));
+  HIP_OR_RETURN(hipEventElapsedTime(trace_ms, c->ev_start, c->ev_mid));
+  HIP_OR_RETURN(hipEventElapsedTime(combine_ms, c->ev_mid, c->ev_stop));
   return MCPT_OK;
 }
 

@@ -24,6 +24,10 @@ constexpr int kEventBytes[EV_COUNT] = {
 //   node  : 3 × float4  (centre.xyz,0) (halfwidth.xyz,0) (1/halfwidth.xyz,0)
 //   prim  : 8 × float4  inverse rows 0..2, transform rows 0..2, colour, material
 constexpr int kNodeF4 = 3;
+// accumulation chunk of the arithmetic contract: passes are summed from 0
+// inside each chunk of kPassChunk consecutive absolute pass numbers, chunk sums added to
+// the accumulator in chunk order
+constexpr int kPassChunk = 32;
 constexpr int kPrimF4 = 8;
 
 struct RenderParams {
@@ -32,11 +36,14 @@ struct RenderParams {
   const int* ptype;
   const float4* prims;
   float* accum;                 // n_local_rows × W × 3 (local rows of this shard)
+  float* partial;               // n_segments × n_local_px × 3 (segment sums; n_segments > 1)
   unsigned long long* events;   // EV_COUNT counters (counting build only)
   float ox, oy, oz;             // camera origin (invV · (0,0,0,1))
   float cd[12];                 // 4 normalized corner directions (raytracer.vert:19)
   int W, H;
   int band_rows, world, rank, n_local_rows;
+  long long n_local_px;         // n_local_rows × W
+  int n_tiles, n_segments;      // 16x16 tiles of the local rows; pass segments of this launch
   int depth;
   int first_pass, n_passes, bounces, variant;
   float date, ior;
@@ -45,3 +52,4 @@ struct RenderParams {
 }  // namespace mcpt
 
 hipError_t mcpt_launch_render(const mcpt::RenderParams& p, bool count, hipStream_t stream);
+hipError_t mcpt_launch_combine(const mcpt::RenderParams& p, hipStream_t stream);

@@ -5,10 +5,12 @@
 // and its additive ONE/ONE blend into the RGB32F FBO (montecarlo.cpp:450-466).
 //
 // Design:
-//  * one lane = one pixel for ALL passes of a launch; a lane whose path terminates
-//    immediately regenerates the next pass's path (persistent-lane regeneration), so
-//    a wave runs until its lanes' *sums* of path lengths are exhausted, not the max
-//    path per pass — the 4 material branches and the 0..B bounce lengths average out;
+//  * one lane = one pixel for a segment of up to 32 passes (one accumulation chunk);
+//    a lane whose path terminates immediately regenerates the next pass's path
+//    (persistent-lane regeneration), so a wave runs until its lanes' *sums* of path
+//    lengths are exhausted, not the max path per pass — the 4 material branches and
+//    the 0..B bounce lengths average out.  Work items = (16x16 tile, pass segment), so
+//    a shard has enough items to fill the chip even at 8-way row-band sharding;
 //  * the bounce loop and the mixed/refraction branch's inner traversal are folded into
 //    ONE traversal site per loop iteration (a 2-phase state machine), so lanes doing an
 //    inner traversal and lanes doing their next bounce run the same instructions;
@@ -18,8 +20,8 @@
 //  * the scene is repacked at upload into 16-byte records (node: centre / half-width /
 //    1/half-width; prim: inverse rows, transform rows, colour, material) so every fetch
 //    is a dwordx4; scenes up to kLdsSceneBytes are staged once per workgroup into LDS;
-//  * each lane adds its passes into its own accumulator in pass order and writes once
-//    per launch (bit-identical to the reference's per-pass blend order).
+//  * each lane sums its segment from 0 in pass order; segment sums are added to the
+//    accumulator in chunk order (combine_kernel).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "mcpt_math.h"
@@ -288,13 +290,25 @@ __device__ __forceinline__ float schlick(float ior, f3 I, f3 N) {   // :91-98
 // ------------------------------------------------------------------------------------
 // the kernel
 // ------------------------------------------------------------------------------------
+__device__ __forceinline__ int floordiv(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
+
+// Work item = (16x16 pixel tile, pass segment).  A segment is the part of the launch's
+// pass range inside one accumulation chunk of kPassChunk absolute passes:
+// segments of one pixel are independent items (strong-scaling parallelism beyond one
+// lane per pixel); their sums are combined in chunk order by combine_kernel.
 template <bool COUNT>
 __global__ __launch_bounds__(256) void render_kernel(RenderParams p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-  const int lr = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+  const int item = blockIdx.x;
+  const int tile = item % p.n_tiles, seg = item / p.n_tiles;
+  const int tiles_x = (p.W + 15) >> 4;
+  const int x = (tile % tiles_x) * 16 + (wave & 1) * 8 + (lane & 7);
+  const int lr = (tile / tiles_x) * 16 + (wave >> 1) * 8 + (lane >> 3);
   if (x >= p.W || lr >= p.n_local_rows) return;
+  const int c0 = floordiv(p.first_pass - 1, kPassChunk) + seg;
+  const int pass_begin = max(p.first_pass, c0 * kPassChunk + 1);
+  const int pass_end = min(p.first_pass + p.n_passes, (c0 + 1) * kPassChunk + 1);
   const int y = ((lr / p.band_rows) * p.world + p.rank) * p.band_rows + (lr % p.band_rows);
 
   SceneRef s{p.nodes, p.leaves, p.ptype, p.prims, p.depth};
@@ -319,21 +333,20 @@ __global__ __launch_bounds__(256) void render_kernel(RenderParams p) {
   const f3 Dcam = normalize3(dir);
   const f3 Ocam = mk(p.ox, p.oy, p.oz);
 
-  float* accp = p.accum + ((size_t)lr * p.W + x) * 3;
-  float acc0 = accp[0], acc1 = accp[1], acc2 = accp[2];
+  float acc0 = 0.0f, acc1 = 0.0f, acc2 = 0.0f;   // this segment's sum, from 0 in pass order
 
   const float ior = p.ior;
   const int B = p.bounces;
-  int pass = 0;
+  int pass = pass_begin;
   // path state
-  Rng rng = seed_for(u, v, p.first_pass, p.date);
+  Rng rng = seed_for(u, v, pass, p.date);
   f3 O = Ocam, D = Dcam, att = mk(0.8f, 0.8f, 0.8f), total = mk(0.0f, 0.0f, 0.0f);
   f3 N = mk(0.0f, 0.0f, 0.0f), P = mk(0.0f, 0.0f, 0.0f), natt = att;
   int bounce = 0, phase = 0;
   Hit h;
   h.pl = mk(0.0f, 0.0f, 0.0f); h.pg = h.pl; h.dist = kFLTMAX; h.index = -1; h.shape = -1; h.dir = -1;
 
-  while (pass < p.n_passes) {
+  while (pass < pass_end) {
     bool done = false;
     f3 res = mk(0.0f, 0.0f, 0.0f);
     if (p.variant == 0 && B <= 0) {
@@ -433,12 +446,19 @@ __global__ __launch_bounds__(256) void render_kernel(RenderParams p) {
       acc0 = acc0 + res.x; acc1 = acc1 + res.y; acc2 = acc2 + res.z;
       ev.inc(EV_SAMPLE);
       pass++;
-      rng = seed_for(u, v, p.first_pass + pass, p.date);
+      rng = seed_for(u, v, pass, p.date);
       O = Ocam; D = Dcam; att = mk(0.8f, 0.8f, 0.8f); total = mk(0.0f, 0.0f, 0.0f);
       bounce = 0; phase = 0;
     }
   }
-  accp[0] = acc0; accp[1] = acc1; accp[2] = acc2;
+  const size_t px = (size_t)lr * p.W + x;
+  if (p.n_segments == 1) {
+    float* accp = p.accum + px * 3;
+    accp[0] = accp[0] + acc0; accp[1] = accp[1] + acc1; accp[2] = accp[2] + acc2;
+  } else {
+    float* part = p.partial + ((size_t)seg * p.n_local_px + px) * 3;
+    part[0] = acc0; part[1] = acc1; part[2] = acc2;
+  }
 
   if (COUNT) {
 #pragma unroll
@@ -450,16 +470,36 @@ __global__ __launch_bounds__(256) void render_kernel(RenderParams p) {
   }
 }
 
+// accum += seg_0 + seg_1 + ... in chunk order (one thread per pixel channel triple)
+__global__ __launch_bounds__(256) void combine_kernel(float* __restrict__ accum, const float* __restrict__ partial,
+                                                      long long n_px, int n_seg) {
+  long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n_px) return;
+  float a0 = accum[i * 3], a1 = accum[i * 3 + 1], a2 = accum[i * 3 + 2];
+  for (int s = 0; s < n_seg; ++s) {
+    const float* q = partial + ((size_t)s * n_px + i) * 3;
+    a0 = a0 + q[0]; a1 = a1 + q[1]; a2 = a2 + q[2];
+  }
+  accum[i * 3] = a0; accum[i * 3 + 1] = a1; accum[i * 3 + 2] = a2;
+}
+
 }  // namespace mcpt
 
 // ------------------------------------------------------------------------------------
 // launch wrapper (host)
 // ------------------------------------------------------------------------------------
 hipError_t mcpt_launch_render(const mcpt::RenderParams& p, bool count, hipStream_t stream) {
-  dim3 block(256);
-  dim3 grid((p.W + 15) / 16, (p.n_local_rows + 15) / 16);
-  if (grid.x == 0 || grid.y == 0) return hipSuccess;
+  const long long items = (long long)p.n_tiles * p.n_segments;
+  if (items <= 0) return hipSuccess;
+  dim3 block(256), grid((unsigned)items);
   if (count) hipLaunchKernelGGL(mcpt::render_kernel<true>, grid, block, 0, stream, p);
   else hipLaunchKernelGGL(mcpt::render_kernel<false>, grid, block, 0, stream, p);
+  return hipGetLastError();
+}
+
+hipError_t mcpt_launch_combine(const mcpt::RenderParams& p, hipStream_t stream) {
+  if (p.n_segments <= 1 || p.n_local_px <= 0) return hipSuccess;
+  dim3 block(256), grid((unsigned)((p.n_local_px + 255) / 256));
+  hipLaunchKernelGGL(mcpt::combine_kernel, grid, block, 0, stream, p.accum, p.partial, p.n_local_px, p.n_segments);
   return hipGetLastError();
 }

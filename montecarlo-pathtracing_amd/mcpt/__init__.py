@@ -67,9 +67,11 @@ def _declare(L: ctypes.CDLL) -> None:
         "mcpt_read_accum": (i, [_vp, fp, ip]),
         "mcpt_clear_accum": (i, [_vp]),
         "mcpt_accum_device_ptr": (i, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(ctypes.c_size_t)]),
+        "mcpt_copy_accum_device": (i, [_vp, _vp, ctypes.c_size_t]),
         "mcpt_set_stream": (i, [_vp, _vp]),
         "mcpt_synchronize": (i, [_vp]),
         "mcpt_last_render_ms": (i, [_vp, fp]),
+        "mcpt_last_kernel_ms": (i, [_vp, fp, fp]),
         "mcpt_scene_create": (i, [ctypes.POINTER(_vp)]),
         "mcpt_scene_destroy": (i, [_vp]),
         "mcpt_scene_clear": (i, [_vp]),
@@ -325,6 +327,11 @@ class Renderer:
         _check(lib().mcpt_accum_device_ptr(self._h, ctypes.byref(p), ctypes.byref(n)), "mcpt_accum_device_ptr")
         return int(p.value or 0), int(n.value)
 
+    def copy_accum_device(self, dst_ptr: int, nbytes: int) -> None:
+        """D2D copy of the local accumulator into a device buffer (ordered on our stream)."""
+        _check(lib().mcpt_copy_accum_device(self._h, _vp(dst_ptr), ctypes.c_size_t(nbytes)),
+               "mcpt_copy_accum_device")
+
     def set_stream(self, hip_stream_ptr: int) -> None:
         _check(lib().mcpt_set_stream(self._h, _vp(hip_stream_ptr)), "mcpt_set_stream")
 
@@ -335,3 +342,9 @@ class Renderer:
         ms = ctypes.c_float()
         _check(lib().mcpt_last_render_ms(self._h, ctypes.byref(ms)), "mcpt_last_render_ms")
         return ms.value
+
+    def last_kernel_ms(self) -> Tuple[float, float]:
+        """(path-tracing kernel ms, chunk-combine kernel ms) of the last render."""
+        a, b = ctypes.c_float(), ctypes.c_float()
+        _check(lib().mcpt_last_kernel_ms(self._h, ctypes.byref(a), ctypes.byref(b)), "mcpt_last_kernel_ms")
+        return a.value, b.value

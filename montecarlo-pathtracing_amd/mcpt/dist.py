@@ -1,0 +1,110 @@
+"""Multi-GPU rendering: interleaved row-band shards + one gather to rank 0.
+
+One process per GPU (torch.distributed; backend "nccl" = RCCL over xGMI on ROCm).  Every
+pixel×pass is independent and the RNG seed is a pure function of (screen_tc, pass, date),
+so splitting the frame by rows is bit-identical to one GPU: each rank renders the rows
+``y`` with ``(y // band_rows) % world == rank`` for ALL passes, into a compact local
+accumulator, and rank 0 gathers the shards (one RCCL gather of fp32 RGB rows, padded to
+the largest shard) and scatters them back into frame order.  No collective runs on the
+data path of the render itself; the gather is the frame's only exchange step.
+
+The gather/reassembly here is device-agnostic torch code so the N>1 path is covered by
+world_size-2 ``gloo`` tests on CPU (tests/test_dist_gloo.py).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def local_rows(H: int, band_rows: int, world: int, rank: int) -> np.ndarray:
+    """Global row ids (increasing) owned by `rank` — matches mcpt_set_target."""
+    y = np.arange(H)
+    return y[(y // band_rows) % world == rank]
+
+
+def max_local_rows(H: int, band_rows: int, world: int) -> int:
+    return max(len(local_rows(H, band_rows, world, r)) for r in range(world))
+
+
+def frame_row_index(H: int, band_rows: int, world: int) -> np.ndarray:
+    """For the padded gather buffer [world, max_rows, ...]: flat source index of each frame row."""
+    m = max_local_rows(H, band_rows, world)
+    src = np.empty(H, np.int64)
+    for r in range(world):
+        rows = local_rows(H, band_rows, world, r)
+        src[rows] = r * m + np.arange(len(rows))
+    return src
+
+
+class FrameGather:
+    """Pre-allocated buffers + index for gathering row-band shards into a frame on `dst`.
+
+    ``gather(local)``: local is [n_local_rows, W, 3] on this rank's device; returns the
+    assembled [H, W, 3] frame on `dst` (None on other ranks).
+    """
+
+    def __init__(self, H: int, W: int, band_rows: int, world: int, rank: int, device: torch.device,
+                 dst: int = 0, group=None, use_gather: bool = True):
+        self.H, self.W, self.band_rows, self.world, self.rank = H, W, band_rows, world, rank
+        self.dst, self.group, self.device = dst, group, device
+        self.m = max_local_rows(H, band_rows, world)
+        self.n_local = len(local_rows(H, band_rows, world, rank))
+        self.send = torch.zeros((self.m, W, 3), dtype=torch.float32, device=device)
+        self.use_gather = use_gather
+        if rank == dst or not use_gather:
+            self.recv = torch.empty((world * self.m, W, 3), dtype=torch.float32, device=device)
+            self.recv_list = list(self.recv.view(world, self.m, W, 3).unbind(0))
+        else:
+            self.recv, self.recv_list = None, None
+        self.index = torch.as_tensor(frame_row_index(H, band_rows, world), device=device)
+        self.frame = (torch.empty((H, W, 3), dtype=torch.float32, device=device)
+                      if rank == dst and world > 1 else None)
+
+    def gather(self, local: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
+        if local is not None:
+            self.send[: self.n_local].copy_(local)
+        if self.world == 1:
+            return self.send
+        if self.use_gather:
+            dist.gather(self.send, self.recv_list if self.rank == self.dst else None, dst=self.dst, group=self.group)
+        else:
+            dist.all_gather_into_tensor(self.recv, self.send, group=self.group)
+        if self.rank != self.dst:
+            return None
+        torch.index_select(self.recv, 0, self.index, out=self.frame)
+        return self.frame
+
+
+class ShardedRenderer:
+    """mcpt.Renderer for this rank's row bands + the RCCL gather (GPU path)."""
+
+    def __init__(self, W: int, H: int, band_rows: int = 8, world: int = 1, rank: int = 0,
+                 local_rank: int = 0, group=None):
+        import mcpt
+        self.device = torch.device("cuda", local_rank)
+        self.r = mcpt.Renderer(local_rank)
+        # kernels, D2D copy and the collective all run on torch's current stream of this device
+        with torch.cuda.device(self.device):
+            self.r.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
+        self.r.set_target(W, H, band_rows, world, rank)
+        self.W, self.H, self.band_rows, self.world, self.rank = W, H, band_rows, world, rank
+        self.g = FrameGather(H, W, band_rows, world, rank, self.device, group=group)
+
+    def upload_scene(self, scene) -> None:
+        self.r.upload_scene(scene)
+
+    def render(self, invPV, invV, first_pass, n_passes, date=0.0, bounces=3, refract_ind=1.0, variant=0):
+        self.r.render(invPV, invV, first_pass, n_passes, date, bounces, refract_ind, variant)
+
+    def gather(self) -> Optional[torch.Tensor]:
+        n = self.g.n_local
+        if n:
+            self.r.copy_accum_device(self.g.send.data_ptr(), n * self.W * 3 * 4)
+        return self.g.gather(None)
+
+    def close(self) -> None:
+        self.r.close()

@@ -101,9 +101,18 @@ def test_zero_bounces_is_black(mcpt_mod, renderer):
 
 
 def test_multi_launch_equals_single(mcpt_mod, renderer):
-    one = _gpu(mcpt_mod, renderer, 2, 40, 30, 1, 6, 8)
-    split = _gpu(mcpt_mod, renderer, 2, 40, 30, 1, 6, 8, split=[2, 1, 3])
+    """Calls split at multiples of the 32-pass accumulation chunk give identical sums."""
+    one = _gpu(mcpt_mod, renderer, 2, 24, 16, 1, 70, 4)
+    split = _gpu(mcpt_mod, renderer, 2, 24, 16, 1, 70, 4, split=[32, 32, 6])
     assert np.array_equal(one.view(np.uint32), split.view(np.uint32))
+
+
+@pytest.mark.parametrize("first,S", [(20, 50), (1, 64), (33, 1), (7, 100)])
+def test_pass_segments_vs_oracle(mcpt_mod, oracle_mod, renderer, first, S):
+    """Launches spanning several accumulation chunks (segment sums + combine kernel)."""
+    gpu = _gpu(mcpt_mod, renderer, 6, 16, 12, first, S, 4)
+    ref, _ = _oracle(oracle_mod, 6, 16, 12, first, S, 4)
+    _compare(gpu, ref, f"passes {first}..{first + S - 1}")
 
 
 @pytest.mark.parametrize("world,band_rows", [(2, 8), (3, 4), (8, 8)])
