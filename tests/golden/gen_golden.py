@@ -1,0 +1,411 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ (committed; rerun to regenerate).
+
+1. kat.npz — known-answer vectors from an INDEPENDENT numpy float32 restatement of the
+   pieces of the sampling loop (RNG, transcendental contract, hemisphere sampler,
+   primitive intersections), written from the GLSL text (raytracer_func.frag,
+   tp/montecarlo.frag) and DESIGN.md §3, not from oracle.cpp.  fma is emulated exactly
+   (double product + TwoSum + midpoint fix-up), so the vectors are bit-exact.
+2. img_s{scene}_v{variant}.npy — small accumulator images rendered by the C++ oracle
+   (regression pins for the oracle and direct fixtures for the GPU tests).
+
+The reference itself cannot run here (no GL 4.3 / Eigen / GLFW / assimp):
+parity with the executed GLSL is unpinned; these fixtures pin the restatement.
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+f32 = np.float32
+u32 = np.uint32
+
+
+# ----------------------------------------------------------------------------------
+# exact binary32 fma in numpy
+# ----------------------------------------------------------------------------------
+def fma32(a, b, c):
+    """round-to-nearest-even binary32 of a*b+c, exactly (no double-rounding)."""
+    a = np.asarray(a, np.float32).astype(np.float64)
+    b = np.asarray(b, np.float32).astype(np.float64)
+    c = np.asarray(c, np.float32).astype(np.float64)
+    p = a * b                            # exact: 24+24 significant bits
+    s = p + c
+    bb = s - p
+    err = (p - (s - bb)) + (c - bb)      # TwoSum: s + err == p + c exactly
+    r = s.astype(np.float32)
+    r64 = r.astype(np.float64)
+    other = np.nextafter(r, np.where(s > r64, np.float32(np.inf), np.float32(-np.inf)).astype(np.float32))
+    mid = (r64 + other.astype(np.float64)) * 0.5
+    # float32(s) is correct unless s sits exactly on a binary32 midpoint and err != 0
+    is_mid = (s != r64) & (s == mid) & (err != 0)
+    res = np.where(is_mid, np.where(err > 0, np.maximum(r, other), np.minimum(r, other)), r)
+    return res.astype(np.float32) if np.ndim(res) else np.float32(res)
+
+
+def dot3(a, b):
+    return fma32(a[2], b[2], fma32(a[1], b[1], f32(a[0] * b[0])))
+
+
+def normalize(v):
+    r = f32(f32(1.0) / np.sqrt(dot3(v, v)))
+    return [f32(v[0] * r), f32(v[1] * r), f32(v[2] * r)]
+
+
+def length(v):
+    return f32(np.sqrt(dot3(v, v)))
+
+
+def cross(a, b):
+    return [f32(a[1] * b[2] - a[2] * b[1]), f32(a[2] * b[0] - a[0] * b[2]), f32(a[0] * b[1] - a[1] * b[0])]
+
+
+def vsub(a, b):
+    return [f32(a[i] - b[i]) for i in range(3)]
+
+
+def vadd(a, b):
+    return [f32(a[i] + b[i]) for i in range(3)]
+
+
+def vmul(a, s):
+    return [f32(a[i] * s) for i in range(3)]
+
+
+def xpoint(m, p):   # column-major mat4, rows 0..2, fma chain x,y,z then + translation
+    return [f32(fma32(m[8 + r], p[2], fma32(m[4 + r], p[1], f32(m[r] * p[0]))) + m[12 + r]) for r in range(3)]
+
+
+def xdir(m, d):
+    return [fma32(m[8 + r], d[2], fma32(m[4 + r], d[1], f32(m[r] * d[0]))) for r in range(3)]
+
+
+# ----------------------------------------------------------------------------------
+# RNG (raytracer_func.frag:90-135)
+# ----------------------------------------------------------------------------------
+def xxhash32(px, py, pz):
+    with np.errstate(over="ignore"):
+        px, py, pz = u32(px), u32(py), u32(pz)
+        P2, P3, P4, P5 = u32(2246822519), u32(3266489917), u32(668265263), u32(374761393)
+        h = u32(pz + P5 + px * P3)
+        h = u32(P4 * u32((h << u32(17)) | (h >> u32(15))))
+        h = u32(h + py * P3)
+        h = u32(P4 * u32((h << u32(17)) | (h >> u32(15))))
+        h = u32(P2 * u32(h ^ (h >> u32(15))))
+        h = u32(P3 * u32(h ^ (h >> u32(13))))
+        return u32(h ^ (h >> u32(16)))
+
+
+def srand(tcx, tcy, npass, date):
+    f = f32(1 + npass)
+    mid = f32(f32(f32(npass) * f32(3.14)) + f32(date))
+    w = [f32(f32(f32(tcx) * f) * f32(1.125)), f32(f32(mid * f) * f32(1.125)), f32(f32(f32(tcy) * f) * f32(1.125))]
+    return [int(np.array(x, np.float32).view(np.uint32)) for x in w]
+
+
+def random_float(seed):
+    m = int(xxhash32(*seed))
+    v = np.array((m & 0x7FFFFF) | 0x3F800000, np.uint32).view(np.float32)
+    seed[0] = (seed[0] + 11) & 0xFFFFFFFF
+    seed[1] = (seed[1] + 43) & 0xFFFFFFFF
+    seed[2] = (seed[2] + 67) & 0xFFFFFFFF
+    return f32(v - f32(1.0))
+
+
+# ----------------------------------------------------------------------------------
+# transcendental contract
+# ----------------------------------------------------------------------------------
+def mc_sincos(x):
+    x = f32(x)
+    qf = f32(np.floor(f32(f32(x * f32(0.636619746685028076)) + f32(0.5))))
+    q = int(qf)
+    r = fma32(-qf, f32(1.57079637050628662), x)
+    r = fma32(-qf, f32(-4.37113900018624283e-8), r)
+    r = fma32(-qf, f32(-1.71512451e-15), r)
+    s = f32(r * r)
+    sp = fma32(fma32(f32(-1.9515295891e-4), s, f32(8.3321608736e-3)), s, f32(-1.6666654611e-1))
+    sn = fma32(f32(r * s), sp, r)
+    cp = fma32(fma32(f32(2.443315711809948e-5), s, f32(-1.388731625493765e-3)), s, f32(4.166664568298827e-2))
+    cs = fma32(f32(s * s), cp, fma32(f32(-0.5), s, f32(1.0)))
+    return [(sn, cs), (cs, f32(-sn)), (f32(-sn), f32(-cs)), (f32(-cs), sn)][q & 3]
+
+
+LOG_P = [7.0376836292e-2, -1.1514610310e-1, 1.1676998740e-1, -1.2420140846e-1, 1.4249322787e-1,
+         -1.6668057665e-1, 2.0000714765e-1, -2.4999993993e-1, 3.3333331174e-1]
+
+
+def mc_log(x):
+    x = f32(x)
+    if not (x > 0):
+        return f32(-np.inf) if x == 0 else f32(np.nan)
+    if np.isinf(x):
+        return x
+    b = int(np.array(x, np.float32).view(np.uint32))
+    e = 0
+    if b < 0x00800000:
+        x = f32(x * f32(8388608.0))
+        b = int(np.array(x, np.float32).view(np.uint32))
+        e = -23
+    e += (b >> 23) - 127
+    m = np.array((b & 0x7FFFFF) | 0x3F800000, np.uint32).view(np.float32)[()]
+    if m > f32(1.41421353816986084):
+        m = f32(m * f32(0.5))
+        e += 1
+    f = f32(m - f32(1.0))
+    z = f32(f * f)
+    p = f32(LOG_P[0])
+    for c in LOG_P[1:]:
+        p = fma32(p, f, f32(c))
+    ef = f32(e)
+    y = f32(f32(f * z) * p)
+    y = fma32(ef, f32(-2.12194440e-4), y)
+    y = fma32(f32(-0.5), z, y)
+    r = f32(f + y)
+    return fma32(ef, f32(0.693359375), r)
+
+
+EXP2_P = [1.535336188319500e-4, 1.339887440266574e-3, 9.618437357674640e-3, 5.550332471162809e-2,
+          2.402264791363012e-1, 6.931472028550421e-1]
+
+
+def mc_exp2(x):
+    x = f32(x)
+    if np.isnan(x):
+        return x
+    if x >= 128:
+        return f32(np.inf)
+    if x < -150:
+        return f32(0.0)
+    kf = f32(np.floor(f32(x + f32(0.5))))
+    f = f32(x - kf)
+    p = f32(EXP2_P[0])
+    for c in EXP2_P[1:]:
+        p = fma32(p, f, f32(c))
+    r = fma32(p, f, f32(1.0))
+    k = int(kf)
+    if k >= -126:
+        return f32(r * np.array((k + 127) << 23, np.uint32).view(np.float32)[()])
+    sc = np.array((k + 127 + 64) << 23, np.uint32).view(np.float32)[()]
+    return f32(f32(r * sc) * f32(5.42101086242752217e-20))
+
+
+def mc_pow(x, y):
+    return mc_exp2(f32(f32(y) * f32(mc_log(x) * f32(1.44269502162933350))))
+
+
+# ----------------------------------------------------------------------------------
+# sampler (tp/montecarlo.frag:49-89)
+# ----------------------------------------------------------------------------------
+PI = f32(3.14159274101257324)
+
+
+def random_ray(seed, D, rough):
+    D = [f32(d) for d in D]
+    W = normalize([D[0], f32(D[1] + f32(5.0)), f32(D[2] + f32(3.0))])
+    U = normalize(cross(D, W))
+    V = normalize(cross(D, U))
+    alpha = f32(f32(rough) * f32(rough))
+    beta = f32(f32(f32(2.0) * PI) * random_float(seed))
+    t2 = f32(f32(-alpha * alpha) * mc_log(f32(f32(1.0) - random_float(seed))))
+    ct = f32(f32(1.0) / np.sqrt(f32(f32(1.0) + t2)))
+    one_m = f32(f32(1.0) - f32(ct * ct))
+    st = f32(np.sqrt(one_m if (f32(0.0) < one_m) else f32(0.0)))   # GLSL max(0, x)
+    sb, cb = mc_sincos(beta)
+    sm = normalize([f32(cb * st), f32(sb * st), ct])
+    m = [fma32(D[i], sm[2], fma32(V[i], sm[1], f32(U[i] * sm[0]))) for i in range(3)]
+    return normalize(m)
+
+
+# ----------------------------------------------------------------------------------
+# primitive intersection (raytracer_func.frag:398-705), world-space distances
+# ----------------------------------------------------------------------------------
+EPS = f32(1e-10)
+FMAX = f32(3.402823e38)
+
+
+def intersect_prim(rec, Ow, Dw):
+    rec = np.asarray(rec, np.float32)
+    t = int(rec[48])
+    inv, trf = rec[16:32], rec[0:16]
+    O = xpoint(inv, Ow)
+    D = normalize(xdir(inv, Dw))
+    best = {"shape": -1, "dist": FMAX, "dir": -1, "pl": [f32(0)] * 3, "pg": [f32(0)] * 3}
+
+    def cand(a, shape, d):
+        Pl = vadd(O, vmul(D, a))
+        Pg = xpoint(trf, Pl)
+        dist = length(vsub([f32(v) for v in Ow], Pg))
+        if dist < best["dist"]:
+            best.update(shape=shape, dist=dist, dir=d, pl=Pl, pg=Pg)
+
+    if t == 1:
+        OO, OD, D2 = dot3(O, O), dot3(O, D), dot3(D, D)
+        d4 = f32(f32(OD * OD) - f32(D2 * f32(OO - f32(1.0))))
+        if d4 > 0:
+            sq = f32(np.sqrt(d4))
+            for a in (f32(-f32(OD + sq) / D2), f32(-f32(OD - sq) / D2)):
+                if a > EPS:
+                    cand(a, 1, 0)
+    elif t == 5:
+        if D[2] > -EPS:
+            return best
+        a = f32(-O[2] / D[2])
+        Pl = vadd(O, vmul(D, a))
+        if abs(Pl[0]) > 1 or abs(Pl[1]) > 1:
+            return best
+        cand(a, 5, 0)
+    elif t == 2:
+        al, cl = FMAX, 0
+        for fc in range(6):
+            c0 = fc // 2
+            if abs(D[c0]) > EPS:
+                c1, c2 = (c0 + 1) % 3, (c0 + 2) % 3
+                cd = f32(-1.0 + 2.0 * (fc % 2))
+                a = f32(f32(cd - O[c0]) / D[c0])
+                if a > EPS and abs(f32(O[c1] + f32(a * D[c1]))) <= 1 and abs(f32(O[c2] + f32(a * D[c2]))) <= 1:
+                    if a < al:
+                        al, cl = a, fc
+        if al < FMAX:
+            cand(al, 2, cl)
+    elif t == 3:
+        cl, al = -1, FMAX
+        if abs(D[2]) > EPS:
+            for cd, code in ((f32(-1.0), 0), (f32(1.0), 1)):
+                a = f32(f32(cd - O[2]) / D[2])
+                if a > EPS:
+                    rx, ry = f32(O[0] + f32(a * D[0])), f32(O[1] + f32(a * D[1]))
+                    if fma32(ry, ry, f32(rx * rx)) < 1 and a < al:
+                        cl, al = code, a
+        O2 = fma32(O[1], O[1], f32(O[0] * O[0]))
+        OD = fma32(O[1], D[1], f32(O[0] * D[0]))
+        D2 = fma32(D[1], D[1], f32(D[0] * D[0]))
+        d4 = f32(f32(OD * OD) - f32(D2 * f32(O2 - f32(1.0))))
+        if d4 > 0:
+            a = f32(-f32(OD + f32(np.sqrt(d4))) / D2)
+            if a > EPS and a < al:
+                z = f32(O[2] + f32(a * D[2]))
+                if abs(z) < 1:
+                    cl, al = 2, a
+        if al < FMAX:
+            cand(al, 3, cl)
+    return best
+
+
+# ----------------------------------------------------------------------------------
+def make_kat(rng: np.random.Generator):
+    kat = {}
+    # xxhash32 on random triples
+    xs = rng.integers(0, 2**32, size=(256, 3), dtype=np.uint64).astype(np.uint32)
+    kat["xx_in"] = xs
+    kat["xx_out"] = np.array([xxhash32(*x) for x in xs], np.uint32)
+    # srand + 16 random floats for pixels/passes
+    cases = [(0.5 / 64, 0.5 / 48, 1, 0.0), (0.9921875, 0.0104166670, 7, 0.0), (0.3, 0.7, 256, 0.0),
+             (0.00026041666, 0.99953705, 84000, 0.0), (0.5, 0.5, 1, 0.016), (0.125, 0.875, 33, 0.0)]
+    kat["srand_in"] = np.array([c[:2] for c in cases], np.float32)
+    kat["srand_pass"] = np.array([c[2] for c in cases], np.int32)
+    kat["srand_date"] = np.array([c[3] for c in cases], np.float32)
+    seeds, seqs = [], []
+    for (tx, ty, p, d) in cases:
+        s = srand(f32(tx), f32(ty), p, f32(d))
+        seeds.append(list(s))
+        seqs.append([random_float(s) for _ in range(16)])
+    kat["srand_seed"] = np.array(seeds, np.uint32)
+    kat["rf_seq"] = np.array(seqs, np.float32)
+    # transcendentals
+    xb = np.concatenate([np.linspace(0, 2 * np.pi, 257)[:-1], rng.uniform(0, 6.2831853, 256)]).astype(np.float32)
+    kat["sc_in"] = xb
+    kat["sc_out"] = np.array([mc_sincos(x) for x in xb], np.float32)
+    xl = np.concatenate([rng.uniform(1.2e-7, 1.0, 256), [1.0, 0.5, 2 ** -23, 0.70710677, 1.4142135, 3.0, 1e-30,
+                                                          1e-40]]).astype(np.float32)
+    kat["log_in"] = xl
+    kat["log_out"] = np.array([mc_log(x) for x in xl], np.float32)
+    xe = np.concatenate([rng.uniform(-140, 20, 256), [0.0, -0.5, 0.5, -126.5, -149.0, -10.25]]).astype(np.float32)
+    kat["exp2_in"] = xe
+    kat["exp2_out"] = np.array([mc_exp2(x) for x in xe], np.float32)
+    px = np.concatenate([rng.uniform(0, 1, 128), [0.0, 1.0, 0.999]]).astype(np.float32)
+    py = np.concatenate([rng.uniform(2, 100, 128), [50.0, 2.0, 100.0]]).astype(np.float32)
+    kat["pow_in"] = np.stack([px, py], 1)
+    kat["pow_out"] = np.array([mc_pow(a, b) for a, b in zip(px, py)], np.float32)
+    # sampler
+    rr_in, rr_seed, rr_rough, rr_out = [], [], [], []
+    for k in range(128):
+        d = rng.normal(size=3)
+        d = (d / np.linalg.norm(d)).astype(np.float32)
+        rough = f32([0.0, 0.01, 0.2, 0.5, 0.8, 1.0, rng.uniform()][k % 7])
+        s = [int(v) for v in rng.integers(0, 2**32, 3, dtype=np.uint64)]
+        rr_in.append(d)
+        rr_seed.append(list(s))
+        rr_rough.append(rough)
+        rr_out.append(random_ray(list(s), d, rough))
+    kat["rr_dir"] = np.array(rr_in, np.float32)
+    kat["rr_seed"] = np.array(rr_seed, np.uint32)
+    kat["rr_rough"] = np.array(rr_rough, np.float32)
+    kat["rr_out"] = np.array(rr_out, np.float32)
+    return kat
+
+
+def make_prim_kat(rng, prims_by_scene):
+    recs, O, D, shape, dist, dr, pl, pg = [], [], [], [], [], [], [], []
+    for recs_scene in prims_by_scene:
+        for rec in recs_scene:
+            if int(rec[48]) not in (1, 2, 3, 5):
+                continue
+            c = rec[12:15].astype(np.float64)
+            size = float(np.linalg.norm(rec[0:3])) + float(np.linalg.norm(rec[4:7])) + float(np.linalg.norm(rec[8:11]))
+            for _ in range(6):
+                o = (c + rng.normal(scale=300, size=3)).astype(np.float32)
+                tgt = c + rng.normal(scale=0.25 * min(size, 300.0), size=3)
+                d = (tgt - o)
+                d = (d / np.linalg.norm(d)).astype(np.float32)
+                b = intersect_prim(rec, list(o), list(d))
+                recs.append(rec)
+                O.append(o)
+                D.append(d)
+                shape.append(b["shape"])
+                dist.append(b["dist"])
+                dr.append(b["dir"])
+                pl.append(b["pl"])
+                pg.append(b["pg"])
+    return {"ip_rec": np.array(recs, np.float32), "ip_O": np.array(O, np.float32), "ip_D": np.array(D, np.float32),
+            "ip_shape": np.array(shape, np.int32), "ip_dist": np.array(dist, np.float32),
+            "ip_dir": np.array(dr, np.int32), "ip_pl": np.array(pl, np.float32), "ip_pg": np.array(pg, np.float32)}
+
+
+IMAGES = [  # (scene, variant, W, H, first_pass, spp, bounces, ior, light)
+    (1, 0, 32, 24, 1, 4, 3, 1.0, 1.2), (2, 0, 32, 24, 1, 2, 8, 1.0, 1.2), (3, 0, 32, 24, 1, 2, 8, 1.0, 1.2),
+    (4, 0, 32, 24, 1, 2, 8, 1.0, 1.2), (5, 0, 32, 24, 1, 2, 8, 1.0, 1.2), (6, 0, 32, 24, 1, 4, 8, 1.0, 1.2),
+    (6, 0, 32, 24, 1, 4, 8, 1.5, 0.443), (7, 0, 32, 24, 1, 2, 8, 1.0, 1.2), (8, 0, 32, 24, 1, 2, 12, 1.0, 1.2),
+    (1, 1, 32, 24, 1, 2, 3, 1.0, 1.2), (6, 2, 32, 24, 1, 2, 3, 1.0, 1.2), (6, 0, 16, 12, 20, 50, 4, 1.0, 1.2),
+]
+
+
+def image_name(c):
+    s, v, W, H, p, n, B, ior, li = c
+    return f"img_s{s}_v{v}_{W}x{H}_p{p}_n{n}_B{B}_ior{ior}_li{li}.npy"
+
+
+def main():
+    from oracle import oracle as orc
+    rng = np.random.default_rng(20241008)
+    kat = make_kat(rng)
+    prims = [orc.scene(s)[0] for s in (1, 2, 3, 6, 8)]
+    prims = [p[: 24] for p in prims]
+    kat.update(make_prim_kat(rng, prims))
+    np.savez_compressed(os.path.join(HERE, "kat.npz"), **kat)
+    for c in IMAGES:
+        s, v, W, H, p, n, B, ior, li = c
+        pr, nodes, leaves, d, _ = orc.scene(s, li)
+        ipv, iv = orc.camera(W, H)
+        acc, _ = orc.render(pr, nodes, leaves, d, ipv, iv, W, H, p, n, 0.0, B, ior, v)
+        np.save(os.path.join(HERE, image_name(c)), acc)
+    print("wrote kat.npz and", len(IMAGES), "images")
+
+
+if __name__ == "__main__":
+    main()

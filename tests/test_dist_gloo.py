@@ -1,0 +1,71 @@
+"""N>1 path on CPU: row-band partition + gather + reassembly over gloo (world 2 and 3).
+
+Each rank's local accumulator is produced by the CPU oracle for its own rows (the GPU
+renderer's stand-in: same rows, same bits — test_gpu_parity.py::test_row_band_shards_bit_equal
+checks the GPU side of that claim); mcpt.dist.FrameGather must reassemble a frame that is
+bit-identical to the single-rank render.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, W, H, band_rows, use_gather, q):
+    import sys
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "montecarlo-pathtracing_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mcpt.dist import FrameGather, local_rows
+        from oracle import oracle as orc
+        prims, nodes, leaves, d, _ = orc.scene(6)
+        ipv, iv = orc.camera(W, H)
+        full, _ = orc.render(prims, nodes, leaves, d, ipv, iv, W, H, 1, 2, 0.0, 4, 1.0, 0, n_threads=2)
+        rows = local_rows(H, band_rows, world, rank)
+        g = FrameGather(H, W, band_rows, world, rank, torch.device("cpu"), use_gather=use_gather)
+        frame = g.gather(torch.from_numpy(np.ascontiguousarray(full[rows])))
+        if rank == 0:
+            q.put(bool(np.array_equal(frame.numpy().view(np.uint32), full.view(np.uint32))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,band_rows,use_gather", [(2, 8, True), (2, 3, False), (3, 4, True)])
+def test_row_band_gather_bit_equal(world, band_rows, use_gather):
+    W, H = 20, 29
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    mp.start_processes(_worker, args=(world, _free_port(), W, H, band_rows, use_gather, q), nprocs=world,
+                       join=True, start_method="spawn")
+    assert q.get(timeout=60) is True
+
+
+def test_partition_covers_frame():
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "montecarlo-pathtracing_amd"))
+    from mcpt.dist import frame_row_index, local_rows, max_local_rows
+    for H, b, w in [(1080, 8, 8), (1080, 8, 3), (53, 4, 3), (7, 8, 2)]:
+        allrows = np.concatenate([local_rows(H, b, w, r) for r in range(w)])
+        assert sorted(allrows.tolist()) == list(range(H))
+        m = max_local_rows(H, b, w)
+        idx = frame_row_index(H, b, w)
+        assert len(set(idx.tolist())) == H and idx.max() < w * m
+    # 1080p over 8 ranks: 17 or 16 bands of 8 rows each
+    sizes = [len(local_rows(1080, 8, 8, r)) for r in range(8)]
+    assert max(sizes) - min(sizes) <= 8
