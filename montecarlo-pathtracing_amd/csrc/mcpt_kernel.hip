@@ -98,7 +98,7 @@ __device__ __forceinline__ void accept_cand(const SceneRef& s, int index, int sh
 
 // intersect_prim raytracer_func.frag:681-705 + Sphere/Cube/Cylinder/Cone/OrientedQuad :398-640
 template <bool COUNT>
-__device__ __noinline__ void prim_test(const SceneRef& s, int i, f3 Ow, f3 Dw, Hit& h, Ev<COUNT>& ev) {
+__device__ __forceinline__ void prim_test(const SceneRef& s, int i, f3 Ow, f3 Dw, Hit& h, Ev<COUNT>& ev) {
   ev.inc(EV_PRIM);
   int t = s.ptype[i];
   if (t < 0) return;
