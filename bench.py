@@ -93,11 +93,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("MCPT_DIST_BACKEND") == "gloo":
+        local_rank = local_rank % max(torch.cuda.device_count(), 1)   # ranks may share a GPU
     if world != args.gpus and not (world == 1 and args.gpus == 1):
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     torch.cuda.set_device(local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        backend = os.environ.get("MCPT_DIST_BACKEND", "nccl")   # "gloo": N>1 rehearsal on one GPU
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
 
     W, H, S, B = args.width, args.height, args.spp, args.bounces
     scene = mcpt.Scene.reference(args.scene, args.light)
@@ -124,7 +130,8 @@ def main():
         trace_ms.append(sr.r.last_kernel_ms())   # HIP events of this launch (waits for its stop event)
     barrier()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=sr.device)
+    stat_dev = sr.device if os.environ.get("MCPT_DIST_BACKEND", "nccl") == "nccl" else torch.device("cpu")
+    t = torch.tensor([elapsed], dtype=torch.float64, device=stat_dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
@@ -137,7 +144,7 @@ def main():
     avg_trace_ms = float(np.mean([a for a, _ in trace_ms]))
     avg_combine_ms = float(np.mean([b for _, b in trace_ms]))
     stats = torch.tensor([bytes_local, avg_trace_ms, avg_combine_ms, float(ev_local[6])], dtype=torch.float64,
-                         device=sr.device)
+                         device=stat_dev)
     if world > 1:
         allstats = [torch.zeros_like(stats) for _ in range(world)]
         dist.all_gather(allstats, stats)

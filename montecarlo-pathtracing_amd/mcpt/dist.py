@@ -69,12 +69,20 @@ class FrameGather:
             self.send[: self.n_local].copy_(local)
         if self.world == 1:
             return self.send
-        if self.use_gather:
-            dist.gather(self.send, self.recv_list if self.rank == self.dst else None, dst=self.dst, group=self.group)
+        staged = self.device.type != "cpu" and dist.get_backend(self.group) == "gloo"
+        if staged:   # rehearsal of the N>1 path on one GPU (gloo collectives need host tensors)
+            send, recv = self.send.cpu(), (self.recv.cpu() if self.recv is not None else None)
+            recv_list = list(recv.view(self.world, self.m, self.W, 3).unbind(0)) if recv is not None else None
         else:
-            dist.all_gather_into_tensor(self.recv, self.send, group=self.group)
+            send, recv, recv_list = self.send, self.recv, self.recv_list
+        if self.use_gather:
+            dist.gather(send, recv_list if self.rank == self.dst else None, dst=self.dst, group=self.group)
+        else:
+            dist.all_gather_into_tensor(recv, send, group=self.group)
         if self.rank != self.dst:
             return None
+        if staged:
+            self.recv.copy_(recv)
         torch.index_select(self.recv, 0, self.index, out=self.frame)
         return self.frame
 
