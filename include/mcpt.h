@@ -43,6 +43,13 @@ enum mcpt_variant {
   MCPT_MAT_TR = 2,           /* tp/montecarlo_mat_tr.frag */
 };
 
+/* BVH traversal strategy of the kernel (same results, different speed) */
+enum mcpt_traversal {
+  MCPT_TRAVERSAL_AUTO = 0,   /* wave-coherent for shallow BVHs, per lane otherwise */
+  MCPT_TRAVERSAL_LANE = 1,   /* each lane walks its own DFS (divergent, vector loads) */
+  MCPT_TRAVERSAL_WAVE = 2,   /* the wave walks the union of its lanes' DFS orders (scalar loads) */
+};
+
 /* algorithmic-byte event counters, index order */
 enum mcpt_event {
   MCPT_EV_NODE = 0, MCPT_EV_LEAF, MCPT_EV_PRIM, MCPT_EV_CAND, MCPT_EV_GEOM, MCPT_EV_COLMAT,
@@ -99,6 +106,11 @@ int mcpt_render_counted(mcpt_ctx* ctx, const float* invPV, const float* invV, in
                         unsigned long long* events);
 int mcpt_event_bytes(int event);
 
+/* Diagnostics: read (and optionally zero) the context's MCPT_EV_COUNT device counter slots.
+ * Only the counting launches and diagnostic builds (-DMCPT_STAMPS: wave-cycle section
+ * totals) write them.  Synchronizes the context's stream. */
+int mcpt_debug_counters(mcpt_ctx* ctx, unsigned long long* out, int reset);
+
 /* Copy the local accumulator (n_local_rows × W × 3 f32) to the host and report the
  * number of passes accumulated (the caller divides: fs_frag, montecarlo.cpp:59-70).
  * Synchronizes the context's stream. */
@@ -110,6 +122,11 @@ int mcpt_accum_device_ptr(mcpt_ctx* ctx, void** dev_ptr, size_t* bytes);
 /* Device-to-device copy of the local accumulator into a caller buffer of >= bytes
  * (e.g. a torch tensor that feeds the RCCL gather), ordered on the context's stream. */
 int mcpt_copy_accum_device(mcpt_ctx* ctx, void* dst_dev_ptr, size_t bytes);
+
+/* Select the traversal strategy (mcpt_traversal) for later renders; default AUTO.
+ * mcpt_get_traversal reports the strategy AUTO resolves to for the uploaded scene. */
+int mcpt_set_traversal(mcpt_ctx* ctx, int mode);
+int mcpt_get_traversal(mcpt_ctx* ctx, int* resolved_mode);
 
 /* Use an external hipStream_t (e.g. torch's current stream); NULL = library stream. */
 int mcpt_set_stream(mcpt_ctx* ctx, void* hip_stream);

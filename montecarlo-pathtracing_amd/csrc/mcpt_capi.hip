@@ -54,7 +54,13 @@ struct mcpt_ctx {
   size_t partial_bytes = 0;
   hipEvent_t ev_start = nullptr, ev_mid = nullptr, ev_stop = nullptr;
   bool timed = false;
+  int traversal = MCPT_TRAVERSAL_AUTO;
 };
+
+static int resolve_traversal(const mcpt_ctx* c) {
+  if (c->traversal != MCPT_TRAVERSAL_AUTO) return c->traversal;
+  return (c->depth <= mcpt::kWaveMaxDepth) ? MCPT_TRAVERSAL_WAVE : MCPT_TRAVERSAL_LANE;
+}
 
 extern "C" {
 
@@ -123,13 +129,19 @@ int mcpt_upload_scene(mcpt_ctx* c, const float* prims, int n_prims, const float*
   const int n_leaf = 1 << depth, n_node = 2 * n_leaf - 1;
   for (int i = 0; i < n_leaf; ++i)
     if (leaves[i] < -1 || leaves[i] >= n_prims) return set_err(MCPT_ERR_BAD_SCENE, "leaf id out of range");
-  // nodes → (centre, half-width, 1/half-width): raytracer_func.frag:319-320 hoisted to upload
+  // subtree-holds-a-primitive flags (bottom-up over the implicit heap): empty subtrees
+  // are never visited by the kernel (they cannot change the closest hit)
+  std::vector<char> has(n_node, 0);
+  for (int i = n_node - 1; i >= 0; --i)
+    has[i] = (i >= n_leaf - 1) ? (leaves[i - (n_leaf - 1)] >= 0) : (has[2 * i + 1] || has[2 * i + 2]);
+  // nodes → (centre, has-prim flag) (half-width, 0) (1/half-width, 0): raytracer_func.frag:319-320
+  // hoisted to upload
   std::vector<float4> hn((size_t)n_node * mcpt::kNodeF4);
   for (int i = 0; i < n_node; ++i) {
     const float* b = nodes + (size_t)i * 6;
     float cx = (b[0] + b[3]) / 2.0f, cy = (b[1] + b[4]) / 2.0f, cz = (b[2] + b[5]) / 2.0f;
     float wx = 0.5f * (b[3] - b[0]), wy = 0.5f * (b[4] - b[1]), wz = 0.5f * (b[5] - b[2]);
-    hn[(size_t)i * 3 + 0] = make_float4(cx, cy, cz, 0.0f);
+    hn[(size_t)i * 3 + 0] = make_float4(cx, cy, cz, has[i] ? 1.0f : 0.0f);
     hn[(size_t)i * 3 + 1] = make_float4(wx, wy, wz, 0.0f);
     hn[(size_t)i * 3 + 2] = make_float4(1.0f / wx, 1.0f / wy, 1.0f / wz, 0.0f);
   }
@@ -244,6 +256,7 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   corner_rays(invPV, invV, p);
   p.W = c->W; p.H = c->H; p.band_rows = c->band_rows; p.world = c->world; p.rank = c->rank;
   p.n_local_rows = c->n_local_rows; p.depth = c->depth;
+  p.wave_traversal = (resolve_traversal(c) == MCPT_TRAVERSAL_WAVE) ? 1 : 0;
   p.first_pass = first_pass; p.n_passes = n_passes; p.bounces = bounces; p.variant = variant;
   p.date = date; p.ior = refract_ind;
   p.n_local_px = (long long)c->n_local_rows * c->W;
@@ -295,6 +308,16 @@ int mcpt_render_counted(mcpt_ctx* c, const float* invPV, const float* invV, int 
   return launch(c, invPV, invV, first_pass, n_passes, date, bounces, refract_ind, variant, true, events);
 }
 
+int mcpt_debug_counters(mcpt_ctx* c, unsigned long long* out, int reset) {
+  if (!c || !out) return MCPT_ERR_INVALID_ARG;
+  HIP_OR_RETURN(hipSetDevice(c->device));
+  HIP_OR_RETURN(hipMemcpyAsync(out, c->d_events, sizeof(unsigned long long) * mcpt::EV_COUNT,
+                               hipMemcpyDeviceToHost, c->stream));
+  if (reset) HIP_OR_RETURN(hipMemsetAsync(c->d_events, 0, sizeof(unsigned long long) * mcpt::EV_COUNT, c->stream));
+  HIP_OR_RETURN(hipStreamSynchronize(c->stream));
+  return MCPT_OK;
+}
+
 int mcpt_event_bytes(int e) {
   if (e < 0 || e >= mcpt::EV_COUNT) return MCPT_ERR_INVALID_ARG;
   return mcpt::kEventBytes[e];
@@ -326,6 +349,19 @@ int mcpt_copy_accum_device(mcpt_ctx* c, void* dst, size_t bytes) {
   HIP_OR_RETURN(hipSetDevice(c->device));
   if (c->accum_bytes)
     HIP_OR_RETURN(hipMemcpyAsync(dst, c->d_accum, c->accum_bytes, hipMemcpyDeviceToDevice, c->stream));
+  return MCPT_OK;
+}
+
+int mcpt_set_traversal(mcpt_ctx* c, int mode) {
+  if (!c || mode < MCPT_TRAVERSAL_AUTO || mode > MCPT_TRAVERSAL_WAVE)
+    return set_err(MCPT_ERR_INVALID_ARG, "mcpt_set_traversal: bad mode");
+  c->traversal = mode;
+  return MCPT_OK;
+}
+
+int mcpt_get_traversal(mcpt_ctx* c, int* resolved) {
+  if (!c || !resolved) return MCPT_ERR_INVALID_ARG;
+  *resolved = resolve_traversal(c);
   return MCPT_OK;
 }
 

@@ -29,6 +29,8 @@ constexpr int kNodeF4 = 3;
 // the accumulator in chunk order
 constexpr int kPassChunk = 32;
 constexpr int kPrimF4 = 8;
+// MCPT_TRAVERSAL_AUTO picks the wave-coherent walk for BVHs up to this depth
+constexpr int kWaveMaxDepth = 4;
 
 struct RenderParams {
   const float4* nodes;
@@ -45,6 +47,7 @@ struct RenderParams {
   long long n_local_px;         // n_local_rows × W
   int n_tiles, n_segments;      // 16x16 tiles of the local rows; pass segments of this launch
   int depth;
+  int wave_traversal;           // 1: wave-coherent BVH walk (traverse_wave), 0: per lane
   int first_pass, n_passes, bounces, variant;
   float date, ior;
 };

@@ -27,9 +27,31 @@
 #include "mcpt_math.h"
 #include "mcpt_internal.h"
 
+// minimum waves per SIMD the register allocator must allow (occupancy vs spills)
+#ifndef MCPT_MIN_WAVES
+#define MCPT_MIN_WAVES 6
+#endif
+
 namespace mcpt {
 
-struct Hit { f3 pl, pg; float dist; int index, shape, dir; };
+struct Hit {
+  f3 pl, pg;
+  float dist;
+  int index, shape, dir;
+  double cull2;   // (midpoint between dist and the next float above)^2, exact in binary64
+};
+
+// The BVH cull `length(O - Pg) <= dist` (raytracer_func.frag:351) without the sqrt: for
+// binary32 d2 >= 0 and c >= 0, RN(sqrt(d2)) <= c  <=>  sqrt(d2) < m, m = the midpoint
+// between c and the next float (sqrt of a binary32 is never exactly such a 25-bit
+// midpoint), <=> d2 < m*m, and m*m (<= 52 significant bits) is exact in binary64.
+// NaN and +inf d2 compare false on both sides.  Bit-identical decisions, 2 VALU ops
+// instead of the ~16-op correctly rounded sqrt.
+__device__ __forceinline__ double cull_bound_sq(float c) {
+  const float nx = __uint_as_float(__float_as_uint(c) + 1u);
+  const double m = ((double)c + (double)nx) * 0.5;
+  return m * m;
+}
 
 enum { CODE_MESH = 0, CODE_SPHERE = 1, CODE_CUBE = 2, CODE_CYLINDER = 3, CODE_CONE = 4, CODE_QUAD = 5 };
 
@@ -37,12 +59,32 @@ enum { CODE_MESH = 0, CODE_SPHERE = 1, CODE_CUBE = 2, CODE_CYLINDER = 3, CODE_CO
 // scene views: global memory or LDS-staged copy (same record layout)
 // ------------------------------------------------------------------------------------
 struct SceneRef {
-  const float4* __restrict__ nodes;   // 3 per node: (c, 0) (w, 0) (1/w, 0)
+  const float4* __restrict__ nodes;   // 3 per node: (c, has-prim) (w, 0) (1/w, 0)
   const int* __restrict__ leaves;
   const int* __restrict__ ptype;
   const float4* __restrict__ prims;   // 8 per prim: inv r0..r2, trf r0..r2, colour, material
   int depth;
 };
+
+// Wave-uniform records are read through the constant address space so the compiler emits
+// scalar loads (s_load_dwordx4/x8 into SGPRs, scalar cache) instead of per-lane gathers.
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(4))) v4f* cv4p;
+typedef const __attribute__((address_space(4))) int* cip;
+
+template <bool UNIFORM>
+__device__ __forceinline__ float4 ld4(const float4* p, size_t i) {
+  if (UNIFORM) {
+    v4f v = ((cv4p)(const void*)p)[i];
+    return make_float4(v.x, v.y, v.z, v.w);
+  }
+  return p[i];
+}
+template <bool UNIFORM>
+__device__ __forceinline__ int ld1(const int* p, size_t i) {
+  if (UNIFORM) return ((cip)(const void*)p)[i];
+  return p[i];
+}
 
 struct Counters {
   uint32_t v[EV_COUNT];
@@ -56,13 +98,17 @@ struct Ev {
   __device__ __forceinline__ void inc(int e) { if (COUNT) c.v[e]++; }
 };
 
-// intersect_bv raytracer_func.frag:314-352; divisions as hoisted reciprocals (contract)
-__device__ __forceinline__ bool box_test(const float4* nd, f3 O, f3 D, f3 invD, float cdist) {
-  float4 a0 = nd[0], a1 = nd[1], a2 = nd[2];
+// intersect_bv raytracer_func.frag:314-352; divisions as hoisted reciprocals (contract).
+// WAVE: the all-lanes-inside early out is taken wave-uniformly (big boxes such as the
+// ground's contain every ray origin).
+template <bool WAVE>
+__device__ __forceinline__ bool box_test(float4 a0, float4 a1, float4 a2, f3 O, f3 D, f3 invD, double cull2) {
   f3 c = mk(a0.x, a0.y, a0.z), w = mk(a1.x, a1.y, a1.z), iw = mk(a2.x, a2.y, a2.z);
   f3 Oi = mulv(sub(O, c), iw);
   f3 Di = mulv(D, iw);
-  if (__builtin_fabsf(Oi.x) < 1.0f && __builtin_fabsf(Oi.y) < 1.0f && __builtin_fabsf(Oi.z) < 1.0f) return true;
+  const bool inside = __builtin_fabsf(Oi.x) < 1.0f && __builtin_fabsf(Oi.y) < 1.0f && __builtin_fabsf(Oi.z) < 1.0f;
+  if (WAVE && __ballot(!inside) == 0) return true;
+  if (inside) return true;
   f3 rD = mulv(invD, w);
   float al = kFLTMAX;
   // faces in reference order: (x,-1) (x,+1) (y,-1) (y,+1) (z,-1) (z,+1)
@@ -81,29 +127,33 @@ __device__ __forceinline__ bool box_test(const float4* nd, f3 O, f3 D, f3 invD, 
 #undef MCPT_FACE
   if (al < kFLTMAX) {
     f3 Pg = add(mulv(add(muls(Di, al), Oi), w), c);
-    return length3(sub(O, Pg)) <= cdist;
+    f3 v = sub(O, Pg);
+    return (double)dot3(v, v) < cull2;
   }
   return false;
 }
 
-template <bool COUNT>
+template <bool COUNT, bool UNI>
 __device__ __forceinline__ void accept_cand(const SceneRef& s, int index, int shape, int dir, f3 Pl, f3 Ol,
                                             Hit& h, Ev<COUNT>& ev) {
   ev.inc(EV_CAND);
-  const float4* pr = s.prims + (size_t)index * 8;
-  f3 Pg = xpoint(pr[3], pr[4], pr[5], Pl);
+  const size_t b = (size_t)index * 8;
+  f3 Pg = xpoint(ld4<UNI>(s.prims, b + 3), ld4<UNI>(s.prims, b + 4), ld4<UNI>(s.prims, b + 5), Pl);
   float dist = length3(sub(Ol, Pg));
-  if (dist < h.dist) { h.dist = dist; h.pl = Pl; h.pg = Pg; h.index = index; h.shape = shape; h.dir = dir; }
+  if (dist < h.dist) {
+    h.dist = dist; h.pl = Pl; h.pg = Pg; h.index = index; h.shape = shape; h.dir = dir;
+    h.cull2 = cull_bound_sq(dist);
+  }
 }
 
 // intersect_prim raytracer_func.frag:681-705 + Sphere/Cube/Cylinder/Cone/OrientedQuad :398-640
-template <bool COUNT>
+template <bool COUNT, bool UNI>
 __device__ __forceinline__ void prim_test(const SceneRef& s, int i, f3 Ow, f3 Dw, Hit& h, Ev<COUNT>& ev) {
   ev.inc(EV_PRIM);
-  int t = s.ptype[i];
+  int t = ld1<UNI>(s.ptype, i);
   if (t < 0) return;
-  const float4* pr = s.prims + (size_t)i * 8;
-  float4 r0 = pr[0], r1 = pr[1], r2 = pr[2];
+  const size_t b = (size_t)i * 8;
+  float4 r0 = ld4<UNI>(s.prims, b), r1 = ld4<UNI>(s.prims, b + 1), r2 = ld4<UNI>(s.prims, b + 2);
   f3 O = xpoint(r0, r1, r2, Ow);
   f3 D = normalize3(xdir(r0, r1, r2, Dw));
   if (t == CODE_SPHERE) {
@@ -112,16 +162,16 @@ __device__ __forceinline__ void prim_test(const SceneRef& s, int i, f3 Ow, f3 Dw
     if (delta4 > 0.0f) {
       float sq = __builtin_sqrtf(delta4);
       float a = -(OD + sq) / D2;
-      if (a > kEPS) accept_cand(s, i, CODE_SPHERE, 0, add(O, muls(D, a)), Ow, h, ev);
+      if (a > kEPS) accept_cand<COUNT, UNI>(s, i, CODE_SPHERE, 0, add(O, muls(D, a)), Ow, h, ev);
       a = -(OD - sq) / D2;
-      if (a > kEPS) accept_cand(s, i, CODE_SPHERE, 0, add(O, muls(D, a)), Ow, h, ev);
+      if (a > kEPS) accept_cand<COUNT, UNI>(s, i, CODE_SPHERE, 0, add(O, muls(D, a)), Ow, h, ev);
     }
   } else if (t == CODE_QUAD) {
     if (D.z > -kEPS) return;
     float a = -O.z / D.z;
     f3 Pl = add(O, muls(D, a));
     if (__builtin_fabsf(Pl.x) > 1.0f || __builtin_fabsf(Pl.y) > 1.0f) return;
-    accept_cand(s, i, CODE_QUAD, 0, Pl, Ow, h, ev);
+    accept_cand<COUNT, UNI>(s, i, CODE_QUAD, 0, Pl, Ow, h, ev);
   } else if (t == CODE_CUBE) {
     float al = kFLTMAX; int cl = 0;
     float o[3] = {O.x, O.y, O.z}, d[3] = {D.x, D.y, D.z};
@@ -135,7 +185,7 @@ __device__ __forceinline__ void prim_test(const SceneRef& s, int i, f3 Ow, f3 Dw
           if (a < al) { al = a; cl = f; }
       }
     }
-    if (al < kFLTMAX) accept_cand(s, i, CODE_CUBE, cl, add(O, muls(D, al)), Ow, h, ev);
+    if (al < kFLTMAX) accept_cand<COUNT, UNI>(s, i, CODE_CUBE, cl, add(O, muls(D, al)), Ow, h, ev);
   } else if (t == CODE_CYLINDER) {
     int cl = -1; float al = kFLTMAX;
     if (__builtin_fabsf(D.z) > kEPS) {
@@ -161,7 +211,7 @@ __device__ __forceinline__ void prim_test(const SceneRef& s, int i, f3 Ow, f3 Dw
         if (__builtin_fabsf(z) < 1.0f) { cl = 2; al = a; }
       }
     }
-    if (al < kFLTMAX) accept_cand(s, i, CODE_CYLINDER, cl, add(O, muls(D, al)), Ow, h, ev);
+    if (al < kFLTMAX) accept_cand<COUNT, UNI>(s, i, CODE_CYLINDER, cl, add(O, muls(D, al)), Ow, h, ev);
   } else if (t == CODE_CONE) {
     int cl = -1; float tl = kFLTMAX;
     if (__builtin_fabsf(D.z) > kEPS) {
@@ -185,18 +235,18 @@ __device__ __forceinline__ void prim_test(const SceneRef& s, int i, f3 Ow, f3 Dw
       float tt = gmin(t1, t2);
       if (tt < tl) { cl = 2; tl = tt; }
     }
-    if (tl < kFLTMAX) accept_cand(s, i, CODE_CONE, cl, add(O, muls(D, tl)), Ow, h, ev);
+    if (tl < kFLTMAX) accept_cand<COUNT, UNI>(s, i, CODE_CONE, cl, add(O, muls(D, tl)), Ow, h, ev);
   }
   // CODE_MESH: no mesh instance in any reference scene: no hit
 }
 
-// intersect_bvh raytracer_func.frag:734-769, stackless.  pending bit L = "a left sibling
-// at level L waits on the reference's stack"; popping the deepest pending bit is exactly
-// the reference's LIFO order (right child first, cull decided at push time).
+// intersect_bvh raytracer_func.frag:734-769, per lane, stackless.  pending bit L = "a left
+// sibling at level L waits on the reference's stack"; popping the deepest pending bit is
+// exactly the reference's LIFO order (right child first, cull decided at push time).
 template <bool COUNT>
-__device__ __forceinline__ void traverse(const SceneRef& s, f3 O, f3 D, Hit& h, Ev<COUNT>& ev) {
+__device__ __forceinline__ void traverse_lane(const SceneRef& s, f3 O, f3 D, Hit& h, Ev<COUNT>& ev) {
   ev.inc(EV_TRAV);
-  h.index = -1; h.dist = kFLTMAX; h.shape = -1; h.dir = -1;
+  h.index = -1; h.dist = kFLTMAX; h.shape = -1; h.dir = -1; h.cull2 = cull_bound_sq(kFLTMAX);
   const f3 invD = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);
   const int leaf0 = (1 << s.depth) - 1;
   int node = 0, level = 0;
@@ -206,19 +256,22 @@ __device__ __forceinline__ void traverse(const SceneRef& s, f3 O, f3 D, Hit& h, 
     if (node >= leaf0) {
       ev.inc(EV_LEAF);
       int p = s.leaves[node - leaf0];
-      if (p >= 0) prim_test<COUNT>(s, p, O, D, h, ev);
+      if (p >= 0) prim_test<COUNT, false>(s, p, O, D, h, ev);
       pop = true;
     } else {
       ev.inc(EV_NODE);
-      int j = 2 * node + 1;
-      bool hl = box_test(s.nodes + (size_t)j * 3, O, D, invD, h.dist);
-      bool hr = box_test(s.nodes + (size_t)(j + 1) * 3, O, D, invD, h.dist);
+      const size_t j = 2 * (size_t)node + 1;
+      const float4 l0 = s.nodes[j * 3], r0 = s.nodes[j * 3 + 3];
+      // a child whose subtree holds no primitive (c.w == 0) cannot change the hit: never
+      // visited (the counting build keeps the reference's visits for its event model)
+      bool hl = (COUNT || l0.w != 0.0f) && box_test<false>(l0, s.nodes[j * 3 + 1], s.nodes[j * 3 + 2], O, D, invD, h.cull2);
+      bool hr = (COUNT || r0.w != 0.0f) && box_test<false>(r0, s.nodes[j * 3 + 4], s.nodes[j * 3 + 5], O, D, invD, h.cull2);
       pop = !(hl || hr);
       if (hr) {
         if (hl) pending |= 1u << (level + 1);
-        node = j + 1; level++;
+        node = (int)j + 1; level++;
       } else if (hl) {
-        node = j; level++;
+        node = (int)j; level++;
       }
     }
     if (pop) {
@@ -229,6 +282,72 @@ __device__ __forceinline__ void traverse(const SceneRef& s, f3 O, f3 D, Hit& h, 
       level = L;
     }
   }
+}
+
+// intersect_bvh, wave-coherent.  Every lane's DFS visits a subsequence of ONE fixed order:
+// the right-child-first pre-order of the implicit heap, with the subtrees its push-time
+// box tests culled.  The wave walks that order once with a wave-uniform cursor (node,
+// level) and skips a subtree only when NO lane pushed it (ballot); a lane works at a
+// node only if it pushed it ("act").  Per lane this is the reference's visit sequence, so
+// every box test sees the same h.dist and every prim test happens in the same order.
+// Gains: node records, leaf ids and prim records are wave-uniform (scalar loads into
+// SGPRs), the primitive-type switch is a uniform branch, and leaf and internal-node
+// work never diverge inside a wave.  Per lane: 1 bit per level for a pushed left child.
+template <bool COUNT>
+__device__ __forceinline__ void traverse_wave(const SceneRef& s, f3 O, f3 D, Hit& h, Ev<COUNT>& ev) {
+  ev.inc(EV_TRAV);
+  h.index = -1; h.dist = kFLTMAX; h.shape = -1; h.dir = -1; h.cull2 = cull_bound_sq(kFLTMAX);
+  const f3 invD = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);
+  const int leaf0 = (1 << s.depth) - 1;
+  uint32_t lpend = 0;    // bit L: this lane pushed the left child at level L of the cursor path
+  bool act = true;       // this lane visits the cursor node
+  int node = 0, level = 0;   // wave-uniform cursor
+  for (;;) {
+    bool descend = false;
+    if (node >= leaf0) {
+      if (act) {
+        ev.inc(EV_LEAF);
+        int p = ld1<true>(s.leaves, node - leaf0);
+        if (p >= 0) prim_test<COUNT, true>(s, p, O, D, h, ev);
+      }
+    } else {
+      const size_t j = 2 * (size_t)node + 1;
+      bool hl = false, hr = false;
+      if (act) {
+        ev.inc(EV_NODE);
+        const float4 l0 = ld4<true>(s.nodes, j * 3), r0 = ld4<true>(s.nodes, j * 3 + 3);
+        // empty subtrees (c.w == 0) are never visited (wave-uniform skip; see traverse_lane)
+        if (COUNT || l0.w != 0.0f)
+          hl = box_test<true>(l0, ld4<true>(s.nodes, j * 3 + 1), ld4<true>(s.nodes, j * 3 + 2), O, D, invD, h.cull2);
+        if (COUNT || r0.w != 0.0f)
+          hr = box_test<true>(r0, ld4<true>(s.nodes, j * 3 + 4), ld4<true>(s.nodes, j * 3 + 5), O, D, invD, h.cull2);
+      }
+      const uint32_t bit = 1u << (level + 1);
+      lpend = hl ? (lpend | bit) : (lpend & ~bit);
+      if (__ballot(hr)) {
+        node = (int)j + 1; level++; act = hr; descend = true;
+      } else if (__ballot(hl)) {
+        node = (int)j; level++; act = hl; descend = true;
+      }
+    }
+    if (descend) continue;
+    // subtree(node) done: next pushed node in right-first pre-order, climbing
+    bool found = false;
+    while (level > 0) {
+      if ((node & 1) == 0) {                       // a right child: its left sibling next
+        const bool a = (lpend >> level) & 1u;
+        if (__ballot(a)) { node = node - 1; act = a; found = true; break; }
+      }
+      node = (node - 1) >> 1; level--;
+    }
+    if (!found) break;
+  }
+}
+
+template <bool COUNT, bool WAVE>
+__device__ __forceinline__ void traverse(const SceneRef& s, f3 O, f3 D, Hit& h, Ev<COUNT>& ev) {
+  if (WAVE) traverse_wave<COUNT>(s, O, D, h, ev);
+  else traverse_lane<COUNT>(s, O, D, h, ev);
 }
 
 // intersection_info raytracer_func.frag:812-897 (hit only; misses leave N,P untouched)
@@ -296,8 +415,8 @@ __device__ __forceinline__ int floordiv(int a, int b) { return (a >= 0) ? a / b 
 // pass range inside one accumulation chunk of kPassChunk absolute passes:
 // segments of one pixel are independent items (strong-scaling parallelism beyond one
 // lane per pixel); their sums are combined in chunk order by combine_kernel.
-template <bool COUNT>
-__global__ __launch_bounds__(256) void render_kernel(RenderParams p) {
+template <bool COUNT, bool WAVE>
+__global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParams p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int item = blockIdx.x;
@@ -345,20 +464,55 @@ __global__ __launch_bounds__(256) void render_kernel(RenderParams p) {
   int bounce = 0, phase = 0;
   Hit h;
   h.pl = mk(0.0f, 0.0f, 0.0f); h.pg = h.pl; h.dist = kFLTMAX; h.index = -1; h.shape = -1; h.dir = -1;
+  h.cull2 = 0.0;
 
+  // Primary-ray cache.  The camera ray of a pixel is the same in every pass (fixed
+  // interpolated direction, fixed origin: raytracer.vert has no jitter) and the
+  // traversal, the hit record and intersection_info consume no RNG, so the first
+  // traversal of every pass has one result per pixel: compute it once per segment.
+  // Exact (same values); the counting build keeps the reference's per-pass traversal so
+  // its events stay the reference's algorithmic model.
+  int shape0 = -1, idx0 = -1;
+  f3 N0 = N, P0 = P;
+  const bool run = !(p.variant == 0 && B <= 0);
+#ifdef MCPT_STAMPS
+  // diagnostic build only (never timed): wave-cycle shares of the kernel's sections
+  unsigned long long st_k0 = __builtin_amdgcn_s_memtime(), st_t = 0, st_s = 0, st_it = 0;
+#endif
+  if (!COUNT && run) {
+    traverse<COUNT, WAVE>(s, Ocam, Dcam, h, ev);
+    shape0 = h.shape; idx0 = h.index;
+    if (shape0 >= 0) geom_info<COUNT>(s, h, N0, P0, ev);
+  }
+
+#ifdef MCPT_STAMPS
+  const unsigned long long st_p = __builtin_amdgcn_s_memtime() - st_k0;
+#endif
   while (pass < pass_end) {
+#ifdef MCPT_STAMPS
+    const unsigned long long st_a = __builtin_amdgcn_s_memtime();
+    st_it++;
+#endif
     bool done = false;
     f3 res = mk(0.0f, 0.0f, 0.0f);
-    if (p.variant == 0 && B <= 0) {
+    const bool first = !COUNT && bounce == 0 && phase == 0;   // camera ray of this pass
+    if (!run) {
       done = true;   // for(i=0; i<NB_BOUNCES ...) never runs: black
     } else {
-      traverse<COUNT>(s, O, D, h, ev);
+      if (first) { h.shape = shape0; h.index = idx0; }
+      else traverse<COUNT, WAVE>(s, O, D, h, ev);
+#ifdef MCPT_STAMPS
+      const unsigned long long st_b = __builtin_amdgcn_s_memtime();
+      st_t += st_b - st_a;
+      st_s -= st_b;
+#endif
       if (p.variant != 0) {
         // tp/montecarlo_mat.frag:5-20 / montecarlo_mat_tr.frag:5-20
         if (h.shape < 0) {
           res = mk(0.0f, 0.0f, 0.2f);
         } else {
-          geom_info<COUNT>(s, h, N, P, ev);
+          if (first) { N = N0; P = P0; }
+          else geom_info<COUNT>(s, h, N, P, ev);
           ev.inc(EV_COLMAT);
           if (p.variant == 1) {
             float rx = rnd(rng), ry = rnd(rng), rz = rnd(rng);
@@ -377,7 +531,8 @@ __global__ __launch_bounds__(256) void render_kernel(RenderParams p) {
           res = add(total, mulv(att, gmix3(mk(0.5f, 0.5f, 0.9f), mk(1.0f, 1.0f, 0.8f), a)));
           done = true;
         } else {
-          geom_info<COUNT>(s, h, N, P, ev);
+          if (first) { N = N0; P = P0; }
+          else geom_info<COUNT>(s, h, N, P, ev);
           ev.inc(EV_COLMAT);
           const float4 c4 = s.prims[(size_t)h.index * 8 + 6];
           const float4 m4 = s.prims[(size_t)h.index * 8 + 7];
@@ -450,7 +605,26 @@ __global__ __launch_bounds__(256) void render_kernel(RenderParams p) {
       O = Ocam; D = Dcam; att = mk(0.8f, 0.8f, 0.8f); total = mk(0.0f, 0.0f, 0.0f);
       bounce = 0; phase = 0;
     }
+#ifdef MCPT_STAMPS
+    if (run) st_s += __builtin_amdgcn_s_memtime();
+#endif
   }
+#ifdef MCPT_STAMPS
+  {
+    // wave totals = the last-finishing lane's sums (max over lanes); lane-iterations summed
+    unsigned long long vals[5] = {__builtin_amdgcn_s_memtime() - st_k0, st_p, st_t, st_s, st_it};
+    unsigned long long it_sum = st_it;
+    for (int off = 32; off > 0; off >>= 1) {
+      for (int k = 0; k < 5; ++k) { unsigned long long o = __shfl_xor(vals[k], off); vals[k] = vals[k] > o ? vals[k] : o; }
+      it_sum += __shfl_xor(it_sum, off);
+    }
+    if (lane == 0 && p.events) {
+      for (int k = 0; k < 5; ++k) atomicAdd(p.events + k, vals[k]);
+      atomicAdd(p.events + 5, it_sum);
+      atomicAdd(p.events + 6, 1ull);
+    }
+  }
+#endif
   const size_t px = (size_t)lr * p.W + x;
   if (p.n_segments == 1) {
     float* accp = p.accum + px * 3;
@@ -492,8 +666,14 @@ hipError_t mcpt_launch_render(const mcpt::RenderParams& p, bool count, hipStream
   const long long items = (long long)p.n_tiles * p.n_segments;
   if (items <= 0) return hipSuccess;
   dim3 block(256), grid((unsigned)items);
-  if (count) hipLaunchKernelGGL(mcpt::render_kernel<true>, grid, block, 0, stream, p);
-  else hipLaunchKernelGGL(mcpt::render_kernel<false>, grid, block, 0, stream, p);
+  const bool wave = p.wave_traversal != 0;
+  if (count) {
+    if (wave) hipLaunchKernelGGL((mcpt::render_kernel<true, true>), grid, block, 0, stream, p);
+    else hipLaunchKernelGGL((mcpt::render_kernel<true, false>), grid, block, 0, stream, p);
+  } else {
+    if (wave) hipLaunchKernelGGL((mcpt::render_kernel<false, true>), grid, block, 0, stream, p);
+    else hipLaunchKernelGGL((mcpt::render_kernel<false, false>), grid, block, 0, stream, p);
+  }
   return hipGetLastError();
 }
 

@@ -26,9 +26,11 @@ import numpy as np
 __all__ = [
     "MCPTError", "lib", "lib_path", "Scene", "Renderer", "camera_canonical",
     "MONTECARLO", "MAT", "MAT_TR", "EVENT_NAMES", "SCENE_KEYS",
+    "TRAVERSAL_AUTO", "TRAVERSAL_LANE", "TRAVERSAL_WAVE",
 ]
 
 MONTECARLO, MAT, MAT_TR = 0, 1, 2
+TRAVERSAL_AUTO, TRAVERSAL_LANE, TRAVERSAL_WAVE = 0, 1, 2
 EVENT_NAMES = ("node", "leaf", "prim", "cand", "geom", "colmat", "sample", "trav")
 # key bindings of montecarlo.cpp:251-290: scene id -> key
 SCENE_KEYS = {1: "Q", 2: "W", 3: "E", 4: "R", 5: "T", 6: "Y", 7: "U", 8: "I"}
@@ -64,10 +66,13 @@ def _declare(L: ctypes.CDLL) -> None:
         "mcpt_render": (i, [_vp, fp, fp, i, i, f, i, f, i]),
         "mcpt_render_counted": (i, [_vp, fp, fp, i, i, f, i, f, i, _c_u64_p]),
         "mcpt_event_bytes": (i, [i]),
+        "mcpt_debug_counters": (i, [_vp, _c_u64_p, i]),
         "mcpt_read_accum": (i, [_vp, fp, ip]),
         "mcpt_clear_accum": (i, [_vp]),
         "mcpt_accum_device_ptr": (i, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(ctypes.c_size_t)]),
         "mcpt_copy_accum_device": (i, [_vp, _vp, ctypes.c_size_t]),
+        "mcpt_set_traversal": (i, [_vp, i]),
+        "mcpt_get_traversal": (i, [_vp, ip]),
         "mcpt_set_stream": (i, [_vp, _vp]),
         "mcpt_synchronize": (i, [_vp]),
         "mcpt_last_render_ms": (i, [_vp, fp]),
@@ -300,6 +305,13 @@ class Renderer:
                                          ev.ctypes.data_as(_c_u64_p)), "mcpt_render_counted")
         return ev
 
+    def debug_counters(self, reset: bool = True) -> np.ndarray:
+        """The context's device counter slots (diagnostic builds write section cycles there)."""
+        out = np.zeros(len(EVENT_NAMES), np.uint64)
+        _check(lib().mcpt_debug_counters(self._h, out.ctypes.data_as(_c_u64_p), int(reset)),
+               "mcpt_debug_counters")
+        return out
+
     @staticmethod
     def event_bytes() -> np.ndarray:
         return np.array([lib().mcpt_event_bytes(e) for e in range(len(EVENT_NAMES))], np.int64)
@@ -331,6 +343,16 @@ class Renderer:
         """D2D copy of the local accumulator into a device buffer (ordered on our stream)."""
         _check(lib().mcpt_copy_accum_device(self._h, _vp(dst_ptr), ctypes.c_size_t(nbytes)),
                "mcpt_copy_accum_device")
+
+    def set_traversal(self, mode: int) -> None:
+        """BVH traversal strategy: TRAVERSAL_AUTO / _LANE / _WAVE (same results)."""
+        _check(lib().mcpt_set_traversal(self._h, int(mode)), "mcpt_set_traversal")
+
+    def traversal(self) -> int:
+        """The strategy AUTO resolves to for the uploaded scene."""
+        m = ctypes.c_int()
+        _check(lib().mcpt_get_traversal(self._h, ctypes.byref(m)), "mcpt_get_traversal")
+        return m.value
 
     def set_stream(self, hip_stream_ptr: int) -> None:
         _check(lib().mcpt_set_stream(self._h, _vp(hip_stream_ptr)), "mcpt_set_stream")

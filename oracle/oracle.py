@@ -46,7 +46,7 @@ def lib() -> ctypes.CDLL:
             "orc_scene_n_emissive": (i, [_vp]),
             "orc_scene_export": (i, [_vp, _fp, _fp, _ip]),
             "orc_camera": (None, [i, i, _fp, _fp]),
-            "orc_render": (i, [_fp, i, _fp, _ip, i, _fp, _fp, i, i, i, i, f, i, f, i, i, i, i, _fp, _u64p]),
+            "orc_render": (i, [_fp, i, _fp, _ip, i, _fp, _fp, i, i, i, i, f, i, f, i, i, i, i, _fp, _u64p, _up]),
             "orc_xxhash32": (ctypes.c_uint, [ctypes.c_uint, ctypes.c_uint, ctypes.c_uint]),
             "orc_srand": (None, [f, f, i, f, _up]),
             "orc_random_floats": (None, [_up, i, _fp]),
@@ -95,8 +95,9 @@ def camera(W: int, H: int) -> Tuple[np.ndarray, np.ndarray]:
 
 
 def render(prims, nodes, leaves, depth, invPV, invV, W, H, first_pass=1, n_passes=1, date=0.0,
-           bounces=3, ior=1.0, variant=0, row_step=1, row_offset=0, n_threads=0, accum=None):
-    """Accumulate passes into accum (H×W×3 f32, row 0 = bottom); returns (accum, events[8])."""
+           bounces=3, ior=1.0, variant=0, row_step=1, row_offset=0, n_threads=0, accum=None, trav_px=None):
+    """Accumulate passes into accum (H×W×3 f32, row 0 = bottom); returns (accum, events[8]).
+    trav_px: optional H×W uint32 array receiving each pixel's traversal count (analysis)."""
     prims = np.ascontiguousarray(prims, np.float32)
     nodes = np.ascontiguousarray(nodes, np.float32)
     leaves = np.ascontiguousarray(leaves, np.int32)
@@ -107,7 +108,8 @@ def render(prims, nodes, leaves, depth, invPV, invV, W, H, first_pass=1, n_passe
     ev = np.zeros(8, np.uint64)
     r = lib().orc_render(P(prims), prims.size // 64, P(nodes), P(leaves, _ip), int(depth), P(invPV), P(invV),
                          int(W), int(H), int(first_pass), int(n_passes), float(date), int(bounces), float(ior),
-                         int(variant), int(row_step), int(row_offset), int(n_threads), P(accum), P(ev, _u64p))
+                         int(variant), int(row_step), int(row_offset), int(n_threads), P(accum), P(ev, _u64p),
+                         P(trav_px, _up) if trav_px is not None else None)
     if r != 0:
         raise RuntimeError(f"orc_render failed ({r})")
     return accum, ev

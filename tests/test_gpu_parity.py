@@ -21,8 +21,9 @@ def renderer(mcpt_mod):
 
 
 def _gpu(mcpt_mod, r, scene_id, W, H, first, S, B, ior=1.0, variant=0, li=1.2, band_rows=8, world=1, rank=0,
-         scene=None, split=None):
+         scene=None, split=None, traversal=0):
     sc = scene if scene is not None else mcpt_mod.Scene.reference(scene_id, li)
+    r.set_traversal(traversal)
     r.upload_scene(sc)
     r.set_target(W, H, band_rows, world, rank)
     ipv, iv = mcpt_mod.camera_canonical(W, H)
@@ -55,25 +56,42 @@ def _compare(gpu, ref, what):
     assert diff.max() <= TOL
 
 
+TRAVERSALS = [1, 2]   # MCPT_TRAVERSAL_LANE, MCPT_TRAVERSAL_WAVE: same bits required from both
+
+
+@pytest.mark.parametrize("traversal", TRAVERSALS)
 @pytest.mark.parametrize("scene_id,B", [(1, 3), (2, 8), (3, 8), (4, 8), (5, 8), (6, 8), (7, 8), (8, 12)])
-def test_scene_parity(mcpt_mod, oracle_mod, renderer, scene_id, B):
+def test_scene_parity(mcpt_mod, oracle_mod, renderer, scene_id, B, traversal):
     W, H, S = 64, 48, 3
-    gpu = _gpu(mcpt_mod, renderer, scene_id, W, H, 1, S, B)
+    gpu = _gpu(mcpt_mod, renderer, scene_id, W, H, 1, S, B, traversal=traversal)
     ref, _ = _oracle(oracle_mod, scene_id, W, H, 1, S, B)
-    _compare(gpu, ref, f"scene {scene_id}")
+    _compare(gpu, ref, f"scene {scene_id} traversal {traversal}")
 
 
+@pytest.mark.parametrize("traversal", TRAVERSALS)
 @pytest.mark.parametrize("variant", [1, 2])
 @pytest.mark.parametrize("scene_id", [1, 6, 8])
-def test_variant_parity(mcpt_mod, oracle_mod, renderer, scene_id, variant):
+def test_variant_parity(mcpt_mod, oracle_mod, renderer, scene_id, variant, traversal):
     W, H, S = 48, 40, 2
-    gpu = _gpu(mcpt_mod, renderer, scene_id, W, H, 1, S, 3, variant=variant)
+    gpu = _gpu(mcpt_mod, renderer, scene_id, W, H, 1, S, 3, variant=variant, traversal=traversal)
     ref, _ = _oracle(oracle_mod, scene_id, W, H, 1, S, 3, variant=variant)
-    _compare(gpu, ref, f"scene {scene_id} variant {variant}")
+    _compare(gpu, ref, f"scene {scene_id} variant {variant} traversal {traversal}")
 
 
-def test_ior_and_light(mcpt_mod, oracle_mod, renderer):
-    gpu = _gpu(mcpt_mod, renderer, 6, 64, 36, 5, 3, 8, ior=1.5, li=0.443)
+def test_auto_traversal_resolution(mcpt_mod, renderer):
+    """AUTO resolves per scene depth (kWaveMaxDepth) and can be overridden."""
+    renderer.set_traversal(0)
+    for sid in (6, 8):
+        renderer.upload_scene(mcpt_mod.Scene.reference(sid))
+        assert renderer.traversal() in (1, 2)
+    renderer.set_traversal(1)
+    assert renderer.traversal() == 1
+    renderer.set_traversal(0)
+
+
+@pytest.mark.parametrize("traversal", TRAVERSALS)
+def test_ior_and_light(mcpt_mod, oracle_mod, renderer, traversal):
+    gpu = _gpu(mcpt_mod, renderer, 6, 64, 36, 5, 3, 8, ior=1.5, li=0.443, traversal=traversal)
     ref, _ = _oracle(oracle_mod, 6, 64, 36, 5, 3, 8, ior=1.5, li=0.443)
     _compare(gpu, ref, "scene 6 ior 1.5 light 0.443")
 
@@ -126,22 +144,26 @@ def test_row_band_shards_bit_equal(mcpt_mod, renderer, world, band_rows):
         assert np.array_equal(part.view(np.uint32), full[rows].view(np.uint32))
 
 
-@pytest.mark.parametrize("scene_id,B", [(6, 8), (8, 12), (7, 8)])
-def test_event_counters_match_oracle(mcpt_mod, oracle_mod, renderer, scene_id, B):
+@pytest.mark.parametrize("traversal", TRAVERSALS)
+@pytest.mark.parametrize("scene_id,B", [(6, 8), (8, 12), (7, 8), (1, 3)])
+def test_event_counters_match_oracle(mcpt_mod, oracle_mod, renderer, scene_id, B, traversal):
     W, H, S = 40, 30, 2
     sc = mcpt_mod.Scene.reference(scene_id)
+    renderer.set_traversal(traversal)
     renderer.upload_scene(sc)
     renderer.set_target(W, H, 8, 1, 0)
     ipv, iv = mcpt_mod.camera_canonical(W, H)
     ev = renderer.render_counted(ipv, iv, 1, S, 0.0, B, 1.0, 0)
     _, ref_ev = _oracle(oracle_mod, scene_id, W, H, 1, S, B)
+    renderer.set_traversal(0)
     assert np.array_equal(ev, ref_ev), (ev, ref_ev)
 
 
-def test_full_hd_rows_subset(mcpt_mod, oracle_mod, renderer):
+@pytest.mark.parametrize("traversal", TRAVERSALS)
+def test_full_hd_rows_subset(mcpt_mod, oracle_mod, renderer, traversal):
     """C2 geometry at full size: 1920x1080, B=8; oracle checks every 45th row."""
     W, H, S, B = 1920, 1080, 2, 8
-    gpu = _gpu(mcpt_mod, renderer, 6, W, H, 1, S, B)
+    gpu = _gpu(mcpt_mod, renderer, 6, W, H, 1, S, B, traversal=traversal)
     assert np.isfinite(gpu).all() and (gpu >= 0).all()
     ref, _ = _oracle(oracle_mod, 6, W, H, 1, S, B, row_step=45, row_offset=7)
     rows = np.arange(7, H, 45)

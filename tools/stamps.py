@@ -1,0 +1,35 @@
+#!/usr/bin/env python3
+"""Section shares from the diagnostic stamp build (MCPT_LIB=.../libmcpt_stamps.so).
+
+Per scene/traversal mode: wave-cycles in the primary-ray prelude, the loop's traversal
+site and the rest of the loop (shading + bookkeeping), and the lane utilisation of the
+loop (lane-iterations / (64 x wave-iterations)).  Shares only: stamps perturb timing.
+"""
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "montecarlo-pathtracing_amd"))
+import torch  # noqa: E402,F401
+import mcpt  # noqa: E402
+
+W, H, S = 1920, 1080, 32
+r = mcpt.Renderer(0)
+r.set_target(W, H)
+ipv, iv = mcpt.camera_canonical(W, H)
+for sid, B in [(6, 8), (1, 3), (8, 12)]:
+    r.upload_scene(mcpt.Scene.reference(sid))
+    for mode in (1, 2):
+        r.set_traversal(mode)
+        r.debug_counters(reset=True)
+        r.render(ipv, iv, 1, S, 0.0, B, 1.0, 0)
+        c = r.debug_counters(reset=True).astype(float)
+        tot, pre, trav, rest, it, lane_it, waves = c[:7]
+        print(json.dumps({"scene": sid, "mode": mode, "waves": int(waves),
+                          "share_prelude": round(pre / tot, 3), "share_traverse": round(trav / tot, 3),
+                          "share_shade": round(rest / tot, 3),
+                          "wave_iters_per_wave": round(it / waves, 1),
+                          "lane_util": round(lane_it / (64 * it), 3),
+                          "cycles_per_wave_iter": round((trav + rest) / it, 1)}), flush=True)
+r.close()
