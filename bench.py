@@ -10,8 +10,11 @@ Scene buffers and the framebuffer are resident in HBM before the timed region.
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
-Multi-GPU: strong scaling — the same C2 frame split into interleaved 8-row bands across
-ranks, one gather of the fp32 RGB shards to rank 0 inside the timed region.
+Multi-GPU: weak scaling — per-GPU work fixed at one C2 frame's worth of samples: at N GPUs
+a step accumulates 256·N passes of the 1080p frame (progressive accumulation, as configs
+C4/C5 do), the frame split into interleaved 8-row bands across ranks (each rank: H/N rows
+× 256·N passes = one C2 frame of samples), then one RCCL gather of the fp32 RGB shards to
+rank 0 inside the timed region.  Bit-identical to rendering the same passes on one GPU.
 
 Prints ONE JSON line (rank 0) with `roofline` (dominant kernel = the path-tracing
 kernel; achieved = algorithmic bytes per launch, counted exactly by the counting build
@@ -39,6 +42,7 @@ import mcpt  # noqa: E402
 from mcpt.dist import ShardedRenderer  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+VALU_PEAK_T = 78.64     # 256 CUs x 4 SIMD x 32 lanes/clk x 2.4 GHz (wave64 VALU = 2 clk/SIMD)
 METRIC = "Msamples/s (W×H×spp/s) + achieved HBM GB/s, 1080p scene6, 1/2/4/8 GPU"
 
 
@@ -63,15 +67,15 @@ def parse():
 
 def cpu_baseline(args, seconds: float):
     """Oracle (C++ restatement, same arithmetic) on a bounded sample of the C2 workload:
-    every 8th row of the frame, 1-pass launches of increasing pass number until the
-    budget is spent.  Threads = the host share of one GPU on the box (OMP_NUM_THREADS,
+    every 2nd row of the frame, 1-pass launches of increasing pass number (1..256) until
+    the budget is spent (≈10 s on the box's 16 host threads).  Threads = the host share of one GPU on the box (OMP_NUM_THREADS,
     16 there), else nproc."""
     from oracle import oracle as orc
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     threads = max(1, min(threads, os.cpu_count() or threads))
     prims, nodes, leaves, depth, _ = orc.scene(args.scene, args.light)
     ipv, iv = orc.camera(args.width, args.height)
-    W, H, row_step = args.width, args.height, 8
+    W, H, row_step = args.width, args.height, 2
     rows = len(range(0, H, row_step))
     acc = np.zeros((H, W, 3), np.float32)
     samples, t0, p = 0, time.perf_counter(), 1
@@ -105,7 +109,8 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    W, H, S, B = args.width, args.height, args.spp, args.bounces
+    W, H, B = args.width, args.height, args.bounces
+    S = args.spp * world          # passes per step: per-GPU work = one C2 frame of samples
     scene = mcpt.Scene.reference(args.scene, args.light)
     sr = ShardedRenderer(W, H, args.band_rows, world, rank, local_rank)
     sr.upload_scene(scene)
@@ -158,16 +163,24 @@ def main():
         # dominant kernel = path-tracing kernel, rank 0's launches (the others are alike)
         achieved = allstats[0, 0] / (allstats[0, 1] / 1e3) / 1e9 if allstats[0, 1] > 0 else 0.0
         bytes_per_sample = allstats[:, 0].sum() / max(allstats[:, 3].sum(), 1.0)
-        traffic = None
+        traffic, valu = None, None
         pmc = os.path.join(REPO, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc):
+        if os.path.exists(pmc) and world == 1:
             try:
                 with open(pmc) as f:
                     rec = json.load(f)
-                if rec.get("workload") == f"scene{args.scene}_{W}x{H}_{S}spp_B{B}" and world == 1:
+                if rec.get("workload") == f"scene{args.scene}_{W}x{H}_{S}spp_B{B}":
                     traffic = rec.get("hbm_bytes_per_launch")
+                    n_valu = rec.get("counters_per_launch", {}).get("SQ_INSTS_VALU")
+                    if n_valu and avg_trace_ms > 0:
+                        # VALU issue roofline: wave64 instructions x 64 lanes over this run's
+                        # kernel time; peak = 256 CUs x 4 SIMD x 32 lanes/clk x 2.4 GHz
+                        ach = n_valu * 64 / (avg_trace_ms / 1e3) / 1e12
+                        valu = {"achieved": round(ach, 2), "peak": VALU_PEAK_T, "unit": "T lane-instr/s",
+                                "frac": round(ach / VALU_PEAK_T, 4), "instructions_per_launch": n_valu,
+                                "source": rec.get("source")}
             except Exception:
-                traffic = None
+                traffic, valu = None, None
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -177,13 +190,14 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (reference scene 6 built by the C++ scene producer; deterministic RNG seeds)",
             "config": {
                 "workload": f"scene{args.scene}_{W}x{H}_{S}spp_B{B}",
-                "scene": args.scene, "width": W, "height": H, "spp_per_step": S, "bounces": B,
+                "scene": args.scene, "width": W, "height": H, "spp_per_step": S,
+                "spp_per_gpu_step": args.spp, "bounces": B,
                 "ior": args.ior, "light_intensity": args.light, "variant": "montecarlo.frag",
                 "parallelism": f"row-bands({args.band_rows} rows) x{world} + RCCL gather" if world > 1
                                else "single GPU",
@@ -198,6 +212,10 @@ def main():
                 "traffic": traffic,
                 "algorithmic_bytes_per_launch": allstats[0, 0],
                 "algorithmic_bytes_per_sample": round(float(bytes_per_sample), 2),
+                "note": ("achieved = the reference's texel-fetch bytes (SURVEY §8d model) / kernel time; "
+                         "scene records live in SGPRs/L1/L2 and primary hits are cached per pixel, so "
+                         "actual HBM bytes are `traffic` and the kernel is VALU-issue bound: see `valu`"),
+                "valu": valu,
             },
         }
         if not args.no_cpu_baseline and world == 1:

@@ -30,7 +30,7 @@ constexpr int kNodeF4 = 3;
 constexpr int kPassChunk = 32;
 constexpr int kPrimF4 = 8;
 // MCPT_TRAVERSAL_AUTO picks the wave-coherent walk for BVHs up to this depth
-constexpr int kWaveMaxDepth = 4;
+constexpr int kWaveMaxDepth = 3;
 
 struct RenderParams {
   const float4* nodes;

@@ -110,20 +110,25 @@ __device__ __forceinline__ bool box_test(float4 a0, float4 a1, float4 a2, f3 O, 
   if (WAVE && __ballot(!inside) == 0) return true;
   if (inside) return true;
   f3 rD = mulv(invD, w);
+  // faces in reference order: (x,-1) (x,+1) (y,-1) (y,+1) (z,-1) (z,+1).  Branch-free:
+  // every face is evaluated and the valid minimum kept with a select (`if (a < al) al = a`
+  // == min(al, valid ? a : FLT_MAX) for the non-NaN a a valid face has); bitwise & keeps
+  // the compares in SGPR masks instead of exec-mask branches (+5 % Msamples/s, r01_ab4).
+  const bool dx = __builtin_fabsf(Di.x) > kEPS, dy = __builtin_fabsf(Di.y) > kEPS, dz = __builtin_fabsf(Di.z) > kEPS;
   float al = kFLTMAX;
-  // faces in reference order: (x,-1) (x,+1) (y,-1) (y,+1) (z,-1) (z,+1)
-#define MCPT_FACE(CD, OA, DA, RA, OB, DB, OC, DC)                                              \
-  if (__builtin_fabsf(DA) > kEPS) {                                                            \
-    float a = ((CD) - (OA)) * (RA);                                                            \
-    if ((a > kEPS) && (__builtin_fabsf(OB + a * DB) <= 1.0f) && (__builtin_fabsf(OC + a * DC) <= 1.0f)) \
-      if (a < al) al = a;                                                                      \
+#define MCPT_FACE(CD, OA, DV, RA, OB, DB, OC, DC)                                              \
+  {                                                                                            \
+    const float a = ((CD) - (OA)) * (RA);                                                      \
+    const bool ok = (DV) & (a > kEPS) & (__builtin_fabsf(OB + a * DB) <= 1.0f) &               \
+                    (__builtin_fabsf(OC + a * DC) <= 1.0f);                                    \
+    al = __builtin_fminf(al, ok ? a : kFLTMAX);                                                \
   }
-  MCPT_FACE(-1.0f, Oi.x, Di.x, rD.x, Oi.y, Di.y, Oi.z, Di.z)
-  MCPT_FACE(1.0f, Oi.x, Di.x, rD.x, Oi.y, Di.y, Oi.z, Di.z)
-  MCPT_FACE(-1.0f, Oi.y, Di.y, rD.y, Oi.z, Di.z, Oi.x, Di.x)
-  MCPT_FACE(1.0f, Oi.y, Di.y, rD.y, Oi.z, Di.z, Oi.x, Di.x)
-  MCPT_FACE(-1.0f, Oi.z, Di.z, rD.z, Oi.x, Di.x, Oi.y, Di.y)
-  MCPT_FACE(1.0f, Oi.z, Di.z, rD.z, Oi.x, Di.x, Oi.y, Di.y)
+  MCPT_FACE(-1.0f, Oi.x, dx, rD.x, Oi.y, Di.y, Oi.z, Di.z)
+  MCPT_FACE(1.0f, Oi.x, dx, rD.x, Oi.y, Di.y, Oi.z, Di.z)
+  MCPT_FACE(-1.0f, Oi.y, dy, rD.y, Oi.z, Di.z, Oi.x, Di.x)
+  MCPT_FACE(1.0f, Oi.y, dy, rD.y, Oi.z, Di.z, Oi.x, Di.x)
+  MCPT_FACE(-1.0f, Oi.z, dz, rD.z, Oi.x, Di.x, Oi.y, Di.y)
+  MCPT_FACE(1.0f, Oi.z, dz, rD.z, Oi.x, Di.x, Oi.y, Di.y)
 #undef MCPT_FACE
   if (al < kFLTMAX) {
     f3 Pg = add(mulv(add(muls(Di, al), Oi), w), c);

@@ -17,7 +17,7 @@ import json
 import os
 import sys
 
-KERNEL = "render_kernel<false>"
+KERNEL = "render_kernel<false"
 
 
 def load(d):
@@ -36,7 +36,7 @@ def main():
     write_b = c["WRITE_SIZE"] * 1024
     rec = {
         "workload": workload,
-        "kernel": "mcpt::render_kernel<false>",
+        "kernel": "mcpt::render_kernel<false, *>",
         "source": f"rocprofv3 --pmc passes of tools/pmc.sh ({os.path.basename(d.rstrip('/'))})",
         "hbm_bytes_per_launch": fetch_b + write_b,
         "fetch_bytes_per_launch_corrected": fetch_b,

@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
 """Section shares from the diagnostic stamp build (MCPT_LIB=.../libmcpt_stamps.so).
 
-Per scene/traversal mode: wave-cycles in the primary-ray prelude, the loop's traversal
-site and the rest of the loop (shading + bookkeeping), and the lane utilisation of the
-loop (lane-iterations / (64 x wave-iterations)).  Shares only: stamps perturb timing.
+Per scene/traversal mode: wave-cycles in the primary-ray prelude, in traversal rounds and
+in shading rounds, and the lane utilisation of the rounds (participating lanes /
+(64 x rounds)).  Shares only: stamps perturb timing.
 """
 import json
 import os
@@ -27,9 +27,9 @@ for sid, B in [(6, 8), (1, 3), (8, 12)]:
         c = r.debug_counters(reset=True).astype(float)
         tot, pre, trav, rest, it, lane_it, waves = c[:7]
         print(json.dumps({"scene": sid, "mode": mode, "waves": int(waves),
-                          "share_prelude": round(pre / tot, 3), "share_traverse": round(trav / tot, 3),
-                          "share_shade": round(rest / tot, 3),
-                          "wave_iters_per_wave": round(it / waves, 1),
+                          "share_prelude": round(pre / tot, 3), "share_traverse_rounds": round(trav / tot, 3),
+                          "share_shade_rounds": round(rest / tot, 3),
+                          "rounds_per_wave": round(it / waves, 1),
                           "lane_util": round(lane_it / (64 * it), 3),
-                          "cycles_per_wave_iter": round((trav + rest) / it, 1)}), flush=True)
+                          "cycles_per_round": round((trav + rest) / it, 1)}), flush=True)
 r.close()
