@@ -29,8 +29,11 @@ constexpr int kNodeF4 = 3;
 // the accumulator in chunk order
 constexpr int kPassChunk = 32;
 constexpr int kPrimF4 = 8;
-// MCPT_TRAVERSAL_AUTO picks the wave-coherent walk for BVHs up to this depth
-constexpr int kWaveMaxDepth = 3;
+// MCPT_TRAVERSAL_AUTO picks the wave-coherent walk for BVHs up to this depth.  Since the
+// per-pixel state moved to LDS (7 waves/SIMD), the per-lane walk is faster on every
+// reference scene (profiles/r01_ab6.jsonl: scene 6 8.07 vs 7.72, scene 1 10.4 vs 8.9,
+// scene 8 0.26 vs 0.11 Gsamples/s), so AUTO = per lane; the wave walk stays selectable.
+constexpr int kWaveMaxDepth = -1;
 
 struct RenderParams {
   const float4* nodes;

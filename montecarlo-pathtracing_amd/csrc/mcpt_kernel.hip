@@ -29,7 +29,7 @@
 
 // minimum waves per SIMD the register allocator must allow (occupancy vs spills)
 #ifndef MCPT_MIN_WAVES
-#define MCPT_MIN_WAVES 6
+#define MCPT_MIN_WAVES 7
 #endif
 
 namespace mcpt {
@@ -454,18 +454,27 @@ __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParam
       dir = add(add(muls(d1, w1), muls(d3, w3)), muls(d2, w2));
     }
   }
-  const f3 Dcam = normalize3(dir);
+  // Per-pixel constants live in LDS (SoA by thread: conflict-free), not in VGPRs: the
+  // camera direction and the cached primary hit are read once per pass, and keeping them
+  // out of the register file is what lets 6 waves/SIMD fit with fewer spills.
+  // rows: 0-2 Dcam, 3-5 N0, 6-8 P0 (primary hit), 9-11 N / 17-19 P saved across the inner
+  // traversal, 12-14 this segment's sum (from 0 in pass order), 15-16 screen_tc
+  __shared__ float s_pix[20][256];
+  __shared__ int s_hit0[2][256];     // primary hit shape, index
+  const f3 Dcam0 = normalize3(dir);
+  s_pix[0][tid] = Dcam0.x; s_pix[1][tid] = Dcam0.y; s_pix[2][tid] = Dcam0.z;
+  s_pix[12][tid] = 0.0f; s_pix[13][tid] = 0.0f; s_pix[14][tid] = 0.0f;   // this segment's sum
+  s_pix[15][tid] = u; s_pix[16][tid] = v;
   const f3 Ocam = mk(p.ox, p.oy, p.oz);
 
-  float acc0 = 0.0f, acc1 = 0.0f, acc2 = 0.0f;   // this segment's sum, from 0 in pass order
 
   const float ior = p.ior;
   const int B = p.bounces;
   int pass = pass_begin;
   // path state
   Rng rng = seed_for(u, v, pass, p.date);
-  f3 O = Ocam, D = Dcam, att = mk(0.8f, 0.8f, 0.8f), total = mk(0.0f, 0.0f, 0.0f);
-  f3 N = mk(0.0f, 0.0f, 0.0f), P = mk(0.0f, 0.0f, 0.0f), natt = att;
+  f3 O = Ocam, D = Dcam0, att = mk(0.8f, 0.8f, 0.8f), total = mk(0.0f, 0.0f, 0.0f);
+  f3 N = mk(0.0f, 0.0f, 0.0f), P = mk(0.0f, 0.0f, 0.0f);
   int bounce = 0, phase = 0;
   Hit h;
   h.pl = mk(0.0f, 0.0f, 0.0f); h.pg = h.pl; h.dist = kFLTMAX; h.index = -1; h.shape = -1; h.dir = -1;
@@ -478,17 +487,20 @@ __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParam
   // Exact (same values); the counting build keeps the reference's per-pass traversal so
   // its events stay the reference's algorithmic model.
   int shape0 = -1, idx0 = -1;
-  f3 N0 = N, P0 = P;
+  f3 N0 = N, P0 = P;   // only live until stored to LDS
   const bool run = !(p.variant == 0 && B <= 0);
 #ifdef MCPT_STAMPS
   // diagnostic build only (never timed): wave-cycle shares of the kernel's sections
   unsigned long long st_k0 = __builtin_amdgcn_s_memtime(), st_t = 0, st_s = 0, st_it = 0;
 #endif
   if (!COUNT && run) {
-    traverse<COUNT, WAVE>(s, Ocam, Dcam, h, ev);
+    traverse<COUNT, WAVE>(s, Ocam, Dcam0, h, ev);
     shape0 = h.shape; idx0 = h.index;
     if (shape0 >= 0) geom_info<COUNT>(s, h, N0, P0, ev);
   }
+  s_pix[3][tid] = N0.x; s_pix[4][tid] = N0.y; s_pix[5][tid] = N0.z;
+  s_pix[6][tid] = P0.x; s_pix[7][tid] = P0.y; s_pix[8][tid] = P0.z;
+  s_hit0[0][tid] = shape0; s_hit0[1][tid] = idx0;
 
 #ifdef MCPT_STAMPS
   const unsigned long long st_p = __builtin_amdgcn_s_memtime() - st_k0;
@@ -504,7 +516,7 @@ __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParam
     if (!run) {
       done = true;   // for(i=0; i<NB_BOUNCES ...) never runs: black
     } else {
-      if (first) { h.shape = shape0; h.index = idx0; }
+      if (first) { h.shape = s_hit0[0][tid]; h.index = s_hit0[1][tid]; }
       else traverse<COUNT, WAVE>(s, O, D, h, ev);
 #ifdef MCPT_STAMPS
       const unsigned long long st_b = __builtin_amdgcn_s_memtime();
@@ -516,7 +528,10 @@ __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParam
         if (h.shape < 0) {
           res = mk(0.0f, 0.0f, 0.2f);
         } else {
-          if (first) { N = N0; P = P0; }
+          if (first) {
+            N = mk(s_pix[3][tid], s_pix[4][tid], s_pix[5][tid]);
+            P = mk(s_pix[6][tid], s_pix[7][tid], s_pix[8][tid]);
+          }
           else geom_info<COUNT>(s, h, N, P, ev);
           ev.inc(EV_COLMAT);
           if (p.variant == 1) {
@@ -536,7 +551,10 @@ __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParam
           res = add(total, mulv(att, gmix3(mk(0.5f, 0.5f, 0.9f), mk(1.0f, 1.0f, 0.8f), a)));
           done = true;
         } else {
-          if (first) { N = N0; P = P0; }
+          if (first) {
+            N = mk(s_pix[3][tid], s_pix[4][tid], s_pix[5][tid]);
+            P = mk(s_pix[6][tid], s_pix[7][tid], s_pix[8][tid]);
+          }
           else geom_info<COUNT>(s, h, N, P, ev);
           ev.inc(EV_COLMAT);
           const float4 c4 = s.prims[(size_t)h.index * 8 + 6];
@@ -558,7 +576,8 @@ __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParam
               reflect_push = true;
             } else if (alpha < 1.0f && m4.x == 0.0f) {
               inner = true;
-              natt = add(base, mulv(muls(muls(muls(att, 1.0f - alpha), 1.0f - rs), spec), mx));
+              // new_attenu of the pushed ray (att is not read again before the push)
+              att = add(base, mulv(muls(muls(muls(att, 1.0f - alpha), 1.0f - rs), spec), mx));
               O = sub(P, muls(N, kBIAS));
               D = grefract(D, N, ior);
             } else if (alpha < 1.0f && m4.x > 0.0f) {
@@ -567,7 +586,7 @@ __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParam
                 reflect_push = true;
               } else {
                 inner = true;
-                natt = add(base, mulv(muls(muls(muls(att, 1.0f - alpha), 1.0f - rs), spec), mx));
+                att = add(base, mulv(muls(muls(muls(att, 1.0f - alpha), 1.0f - rs), spec), mx));
                 O = sub(P, muls(N, kBIAS));
               }
             } else {   // diffuse
@@ -584,7 +603,13 @@ __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParam
               D = rd;
               bounce++;
             }
-            if (inner) phase = 1;
+            if (inner) {
+              // intersection_info leaves N,P untouched on a miss: keep them for the
+              // inner hit in LDS rather than across the traversal in registers
+              phase = 1;
+              s_pix[9][tid] = N.x; s_pix[10][tid] = N.y; s_pix[11][tid] = N.z;
+              s_pix[17][tid] = P.x; s_pix[18][tid] = P.y; s_pix[19][tid] = P.z;
+            }
             else if (bounce >= B) done = true;   // budget exhausted: black (res = 0)
           } else {
             res = total;                          // emissive: end of path
@@ -593,21 +618,28 @@ __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParam
         }
       } else {
         // inner traversal of the refraction branches (montecarlo.frag:148-152 / 162-165)
-        if (h.shape >= 0) geom_info<COUNT>(s, h, N, P, ev);
+        if (h.shape >= 0) {
+          geom_info<COUNT>(s, h, N, P, ev);
+        } else {
+          N = mk(s_pix[9][tid], s_pix[10][tid], s_pix[11][tid]);
+          P = mk(s_pix[17][tid], s_pix[18][tid], s_pix[19][tid]);
+        }
         O = add(P, muls(N, kBIAS));
         D = grefract(D, neg(N), 1.0f / ior);
-        att = natt;
         phase = 0;
         bounce++;
         if (bounce >= B) done = true;
       }
     }
     if (done) {
-      acc0 = acc0 + res.x; acc1 = acc1 + res.y; acc2 = acc2 + res.z;
+      s_pix[12][tid] = s_pix[12][tid] + res.x;
+      s_pix[13][tid] = s_pix[13][tid] + res.y;
+      s_pix[14][tid] = s_pix[14][tid] + res.z;
       ev.inc(EV_SAMPLE);
       pass++;
-      rng = seed_for(u, v, pass, p.date);
-      O = Ocam; D = Dcam; att = mk(0.8f, 0.8f, 0.8f); total = mk(0.0f, 0.0f, 0.0f);
+      rng = seed_for(s_pix[15][tid], s_pix[16][tid], pass, p.date);
+      O = Ocam; D = mk(s_pix[0][tid], s_pix[1][tid], s_pix[2][tid]);
+      att = mk(0.8f, 0.8f, 0.8f); total = mk(0.0f, 0.0f, 0.0f);
       bounce = 0; phase = 0;
     }
 #ifdef MCPT_STAMPS
@@ -633,10 +665,10 @@ __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParam
   const size_t px = (size_t)lr * p.W + x;
   if (p.n_segments == 1) {
     float* accp = p.accum + px * 3;
-    accp[0] = accp[0] + acc0; accp[1] = accp[1] + acc1; accp[2] = accp[2] + acc2;
+    accp[0] = accp[0] + s_pix[12][tid]; accp[1] = accp[1] + s_pix[13][tid]; accp[2] = accp[2] + s_pix[14][tid];
   } else {
     float* part = p.partial + ((size_t)seg * p.n_local_px + px) * 3;
-    part[0] = acc0; part[1] = acc1; part[2] = acc2;
+    part[0] = s_pix[12][tid]; part[1] = s_pix[13][tid]; part[2] = s_pix[14][tid];
   }
 
   if (COUNT) {
