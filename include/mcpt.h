@@ -170,6 +170,21 @@ int mcpt_scene_build_reference(mcpt_scene* s, int scene_id, float light_intensit
  * view = modelview · rotateX(-80); outputs (P·V)^-1 and V^-1, column-major */
 int mcpt_camera_canonical(int W, int H, float* invPV16, float* invV16);
 
+/* ---------------------------------------------------------------------------------
+ * 3. host helpers: Transfo (easycppogl/gl_eigen.cpp:29-105, degrees, column-major) and
+ *    the output step
+ * --------------------------------------------------------------------------------- */
+int mcpt_transfo_translate(float x, float y, float z, float* out16);           /* Transfo::translate */
+int mcpt_transfo_scale(float x, float y, float z, float* out16);               /* Transfo::scale */
+int mcpt_transfo_rotate(int axis, float degrees, float* out16);                /* rotateX/Y/Z: axis 0/1/2 */
+int mcpt_mat4_mul(const float* a16, const float* b16, float* out16);           /* GLMat4 a * b */
+/* fs_frag (montecarlo.cpp:59-70): out = accum / pass_count, per channel */
+int mcpt_average(const float* accum, long long n_values, int pass_count, float* out);
+/* averaged image (H rows × W × RGB f32, row 0 = bottom) to a little-endian PFM */
+int mcpt_write_pfm(const char* path, const float* rgb, int W, int H);
+/* what the 8-bit default framebuffer shows: clamp to [0,1], round(255·c), no gamma; PNG RGB8 */
+int mcpt_write_png(const char* path, const float* rgb, int W, int H);
+
 #ifdef __cplusplus
 }
 #endif

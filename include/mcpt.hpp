@@ -1,0 +1,216 @@
+// mcpt.hpp — C++ host API over the libmcpt C ABI (include/mcpt.h), header-only.
+//
+// Mirrors the reference's host interface of the hot path so montecarlo.cpp-style code keeps
+// its shape (names and argument meaning of bvh_gpu/scene.h, bvh_gpu/gpu_bvh_scene.h,
+// easycppogl/gl_eigen.h):
+//
+//   GLVec4, GLMat4            Eigen column-major storage (gl_eigen.h:46-60)
+//   Transfo::translate/scale/rotateX/rotateY/rotateZ   gl_eigen.cpp:29-105 (degrees)
+//   Material (3 ctors + Material::light)               scene.h:30-49
+//   BVH_GPU_Scene: clear, add_sphere/add_cube/add_cylinder/add_cone/add_orientedQuad,
+//                  finalize, depth(i), nb_prim, nb_emissives     gpu_bvh_scene.h:35-121
+//   Renderer: the GL program + accumulation FBO of RTViewer (montecarlo.cpp:384-386, 408-477)
+//
+// Every matrix product goes through libmcpt (mcpt_mat4_mul) so transforms are bit-identical
+// to the reference scenes the library builds.  Errors throw mcpt::Error (the reference has
+// no error convention; the C ABI returns status codes).
+#ifndef MCPT_HPP_
+#define MCPT_HPP_
+
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "mcpt.h"
+
+namespace mcpt {
+
+class Error : public std::runtime_error {
+ public:
+  Error(const std::string& what, int status)
+      : std::runtime_error(what + " failed (" + std::to_string(status) + "): " + mcpt_error_string(status)),
+        status_(status) {}
+  int status() const { return status_; }
+
+ private:
+  int status_;
+};
+
+inline void check(int status, const char* what) {
+  if (status != MCPT_OK) throw Error(what, status);
+}
+
+struct GLVec4 {
+  float v[4];
+  GLVec4(float r = 0, float g = 0, float b = 0, float a = 1) : v{r, g, b, a} {}
+  float& operator[](int i) { return v[i]; }
+  float operator[](int i) const { return v[i]; }
+};
+
+// column-major 4x4 (Eigen default storage: m[col * 4 + row])
+struct GLMat4 {
+  float m[16];
+  GLMat4() { std::memset(m, 0, sizeof(m)); m[0] = m[5] = m[10] = m[15] = 1.0f; }
+  static GLMat4 Identity() { return GLMat4(); }
+  float& operator()(int r, int c) { return m[c * 4 + r]; }
+  float operator()(int r, int c) const { return m[c * 4 + r]; }
+  const float* data() const { return m; }
+  GLMat4 operator*(const GLMat4& b) const {
+    GLMat4 r;
+    check(mcpt_mat4_mul(m, b.m, r.m), "mcpt_mat4_mul");
+    return r;
+  }
+};
+
+namespace Transfo {
+inline GLMat4 translate(float x, float y, float z) {
+  GLMat4 r;
+  check(mcpt_transfo_translate(x, y, z, r.m), "mcpt_transfo_translate");
+  return r;
+}
+inline GLMat4 scale(float sx, float sy, float sz) {
+  GLMat4 r;
+  check(mcpt_transfo_scale(sx, sy, sz, r.m), "mcpt_transfo_scale");
+  return r;
+}
+inline GLMat4 scale(float s) { return scale(s, s, s); }
+inline GLMat4 rotateX(float deg) { GLMat4 r; check(mcpt_transfo_rotate(0, deg, r.m), "rotateX"); return r; }
+inline GLMat4 rotateY(float deg) { GLMat4 r; check(mcpt_transfo_rotate(1, deg, r.m), "rotateY"); return r; }
+inline GLMat4 rotateZ(float deg) { GLMat4 r; check(mcpt_transfo_rotate(2, deg, r.m), "rotateZ"); return r; }
+}  // namespace Transfo
+
+class Material {
+ public:
+  GLVec4 color_;
+  float shininess_, roughness_, emissivity_;
+  Material(const GLVec4& color, float shin, float rough, float emi)
+      : color_(color), shininess_(shin), roughness_(rough), emissivity_(emi) {}
+  Material(const GLVec4& color, float shin, float rough) : Material(color, shin, rough, 0.0f) {}
+  explicit Material(const GLVec4& color) : Material(color, 0.0f, 0.0f, 0.0f) {}
+  static Material light(const GLVec4& col, float emi) { return Material(col, 0.0f, 0.0f, emi); }
+  // the 7 floats the C ABI takes: r, g, b, a(opacity), shininess, roughness, emissivity
+  void pack(float out[7]) const {
+    for (int k = 0; k < 4; ++k) out[k] = color_[k];
+    out[4] = shininess_; out[5] = roughness_; out[6] = emissivity_;
+  }
+};
+
+// ScenePrimitives + BVH_KDtree + BVH_GPU_Scene (host side, in libmcpt)
+class BVH_GPU_Scene {
+ public:
+  BVH_GPU_Scene() { check(mcpt_scene_create(&s_), "mcpt_scene_create"); }
+  ~BVH_GPU_Scene() { mcpt_scene_destroy(s_); }
+  BVH_GPU_Scene(const BVH_GPU_Scene&) = delete;
+  BVH_GPU_Scene& operator=(const BVH_GPU_Scene&) = delete;
+
+  // one of the 8 scenes of montecarlo.cpp:629-795 (keys Q..I = 1..8), finalized
+  void build_reference(int scene_id, float light_intensity = 1.2f) {
+    check(mcpt_scene_build_reference(s_, scene_id, light_intensity), "mcpt_scene_build_reference");
+  }
+  void clear() { check(mcpt_scene_clear(s_), "mcpt_scene_clear"); }
+  void add_sphere(const GLMat4& trf, const Material& mat) { add(&mcpt_scene_add_sphere, trf, mat, "add_sphere"); }
+  void add_cube(const GLMat4& trf, const Material& mat) { add(&mcpt_scene_add_cube, trf, mat, "add_cube"); }
+  void add_cylinder(const GLMat4& trf, const Material& mat) { add(&mcpt_scene_add_cylinder, trf, mat, "add_cylinder"); }
+  void add_cone(const GLMat4& trf, const Material& mat) { add(&mcpt_scene_add_cone, trf, mat, "add_cone"); }
+  void add_orientedQuad(const GLMat4& trf, const Material& mat) {
+    add(&mcpt_scene_add_oriented_quad, trf, mat, "add_orientedQuad");
+  }
+  void finalize() { check(mcpt_scene_finalize(s_), "mcpt_scene_finalize"); }
+  int depth(int /*bvh*/ = 0) const { int d = 0; check(mcpt_scene_depth(s_, &d), "mcpt_scene_depth"); return d; }
+  int nb_prim() const { int n = 0; check(mcpt_scene_nb_prim(s_, &n), "mcpt_scene_nb_prim"); return n; }
+  int nb_emissives() const { int n = 0; check(mcpt_scene_nb_emissives(s_, &n), "mcpt_scene_nb_emissives"); return n; }
+
+  // the reference's texture layouts (tex_prim / tex_bb / tex_ind), flattened
+  void buffers(std::vector<float>& prims, std::vector<float>& nodes, std::vector<int>& leaves) const {
+    const int n = nb_prim(), d = depth();
+    prims.assign((size_t)n * 64, 0.0f);
+    nodes.assign(((size_t(2) << d) - 1) * 6, 0.0f);
+    leaves.assign(size_t(1) << d, 0);
+    check(mcpt_scene_get_buffers(s_, prims.data(), nodes.data(), leaves.data()), "mcpt_scene_get_buffers");
+  }
+  mcpt_scene* handle() const { return s_; }
+
+ private:
+  typedef int (*AddFn)(mcpt_scene*, const float*, const float*);
+  void add(AddFn fn, const GLMat4& trf, const Material& mat, const char* what) {
+    float m7[7];
+    mat.pack(m7);
+    check(fn(s_, trf.m, m7), what);
+  }
+  mcpt_scene* s_ = nullptr;
+};
+
+// canonical camera of RTViewer at aspect W/H: (P·V)^-1 and V^-1, column-major
+struct Camera {
+  GLMat4 invPV, invV;
+  static Camera canonical(int W, int H) {
+    Camera c;
+    check(mcpt_camera_canonical(W, H, c.invPV.m, c.invV.m), "mcpt_camera_canonical");
+    return c;
+  }
+};
+
+// prg_ray + the RGB32F accumulation FBO (montecarlo.cpp:384-386, 408-477), one GPU
+class Renderer {
+ public:
+  explicit Renderer(int device = 0) { check(mcpt_create(device, &c_), "mcpt_create"); }
+  ~Renderer() { mcpt_destroy(c_); }
+  Renderer(const Renderer&) = delete;
+  Renderer& operator=(const Renderer&) = delete;
+
+  void upload(const BVH_GPU_Scene& sc) {
+    std::vector<float> p, n;
+    std::vector<int> l;
+    sc.buffers(p, n, l);
+    check(mcpt_upload_scene(c_, p.data(), sc.nb_prim(), n.data(), l.data(), sc.depth(), sc.nb_emissives()),
+          "mcpt_upload_scene");
+  }
+  void set_target(int W, int H, int band_rows = 8, int world = 1, int rank = 0) {
+    check(mcpt_set_target(c_, W, H, band_rows, world, rank), "mcpt_set_target");
+    W_ = W; H_ = H;
+    check(mcpt_local_rows(c_, &rows_), "mcpt_local_rows");
+  }
+  // numero_pass = first_pass .. first_pass + n_passes - 1, accumulated (blend ONE/ONE)
+  void render(const Camera& cam, int first_pass, int n_passes, float date, int bounces, float refract_ind,
+              int variant = MCPT_MONTECARLO) {
+    check(mcpt_render(c_, cam.invPV.m, cam.invV.m, first_pass, n_passes, date, bounces, refract_ind, variant),
+          "mcpt_render");
+  }
+  void clear_accum() { check(mcpt_clear_accum(c_), "mcpt_clear_accum"); }
+  // (local rows × W × 3 sums, pass count)
+  int read_accum(std::vector<float>& rgb) const {
+    rgb.assign((size_t)rows_ * W_ * 3, 0.0f);
+    int n = 0;
+    check(mcpt_read_accum(c_, rgb.data(), &n), "mcpt_read_accum");
+    return n;
+  }
+  // fs_frag: the averaged image (single-shard target)
+  std::vector<float> read_image() const {
+    std::vector<float> acc;
+    const int n = read_accum(acc);
+    std::vector<float> img(acc.size());
+    check(mcpt_average(acc.data(), (long long)acc.size(), n > 0 ? n : 1, img.data()), "mcpt_average");
+    return img;
+  }
+  float last_render_ms() const { float ms = 0; check(mcpt_last_render_ms(c_, &ms), "mcpt_last_render_ms"); return ms; }
+  void set_traversal(int mode) { check(mcpt_set_traversal(c_, mode), "mcpt_set_traversal"); }
+  int width() const { return W_; }
+  int height() const { return H_; }
+  mcpt_ctx* handle() const { return c_; }
+
+ private:
+  mcpt_ctx* c_ = nullptr;
+  int W_ = 0, H_ = 0, rows_ = 0;
+};
+
+inline void write_pfm(const std::string& path, const std::vector<float>& rgb, int W, int H) {
+  check(mcpt_write_pfm(path.c_str(), rgb.data(), W, H), "mcpt_write_pfm");
+}
+inline void write_png(const std::string& path, const std::vector<float>& rgb, int W, int H) {
+  check(mcpt_write_png(path.c_str(), rgb.data(), W, H), "mcpt_write_png");
+}
+
+}  // namespace mcpt
+
+#endif  // MCPT_HPP_

@@ -1,0 +1,117 @@
+// mcpt_render — headless entry point of the MI355X path tracer (the montecarlo.cpp main,
+// MontecarloGPU/montecarlo.cpp:797-803, without the GL window).
+//
+// Builds one of the 8 reference scenes (keys Q..I = 1..8), accumulates passes with the
+// reference's uniform ABI (numero_pass, date, NB_BOUNCES, refract_ind, shader variant),
+// progressively in chunks like the "lock" mode, then writes the averaged image (fs_frag,
+// montecarlo.cpp:59-70) as PFM (float) and/or PNG (8-bit framebuffer view).  Prints one JSON
+// line with the timing.  Host C++ over the C ABI (include/mcpt.hpp); no CPU fallback.
+//
+//   mcpt_render --scene 6 --width 1920 --height 1080 --spp 256 --bounces 8 --out s6.png
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "mcpt.hpp"
+
+namespace {
+
+struct Args {
+  int scene = 6, width = 1280, height = 1000, spp = 16, bounces = 3, first_pass = 1, chunk = 64;
+  int device = 0, subsampling = 0, variant = MCPT_MONTECARLO, traversal = MCPT_TRAVERSAL_AUTO;
+  float ior = 1.0f, light = 1.2f, date = 0.0f;
+  std::string png, pfm;
+};
+
+void usage() {
+  std::fprintf(stderr,
+               "usage: mcpt_render [--scene 1..8] [--width W] [--height H] [--subsampling k]\n"
+               "                   [--spp S] [--first-pass P] [--chunk C] [--bounces B] [--ior R]\n"
+               "                   [--light L] [--date T] [--variant montecarlo|mat|mat_tr]\n"
+               "                   [--traversal auto|lane|wave] [--device D] [--out img.png] [--pfm img.pfm]\n");
+}
+
+bool parse(int argc, char** argv, Args& a) {
+  for (int i = 1; i < argc; ++i) {
+    const std::string k = argv[i];
+    if (k == "-h" || k == "--help") return false;
+    if (i + 1 >= argc) return false;
+    const char* v = argv[++i];
+    if (k == "--scene") a.scene = std::atoi(v);
+    else if (k == "--width") a.width = std::atoi(v);
+    else if (k == "--height") a.height = std::atoi(v);
+    else if (k == "--subsampling") a.subsampling = std::atoi(v);
+    else if (k == "--spp") a.spp = std::atoi(v);
+    else if (k == "--first-pass") a.first_pass = std::atoi(v);
+    else if (k == "--chunk") a.chunk = std::atoi(v);
+    else if (k == "--bounces") a.bounces = std::atoi(v);
+    else if (k == "--ior") a.ior = (float)std::atof(v);
+    else if (k == "--light") a.light = (float)std::atof(v);
+    else if (k == "--date") a.date = (float)std::atof(v);
+    else if (k == "--device") a.device = std::atoi(v);
+    else if (k == "--out") a.png = v;
+    else if (k == "--pfm") a.pfm = v;
+    else if (k == "--variant") {
+      const std::string s = v;
+      a.variant = s == "mat" ? MCPT_MAT : (s == "mat_tr" ? MCPT_MAT_TR : MCPT_MONTECARLO);
+      if (s != "mat" && s != "mat_tr" && s != "montecarlo") return false;
+    } else if (k == "--traversal") {
+      const std::string s = v;
+      a.traversal = s == "lane" ? MCPT_TRAVERSAL_LANE : (s == "wave" ? MCPT_TRAVERSAL_WAVE : MCPT_TRAVERSAL_AUTO);
+    } else {
+      return false;
+    }
+  }
+  return a.width > 0 && a.height > 0 && a.spp >= 0 && a.chunk > 0 && a.subsampling >= 0 && a.subsampling < 16;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  Args a;
+  if (!parse(argc, argv, a)) {
+    usage();
+    return 2;
+  }
+  try {
+    mcpt::BVH_GPU_Scene scene;
+    scene.build_reference(a.scene, a.light);
+    // sub-sampling renders the FBO at (W>>k) x (H>>k) with the window's aspect (montecarlo.cpp:616-626)
+    const int W = a.width >> a.subsampling, H = a.height >> a.subsampling;
+    if (W <= 0 || H <= 0) throw std::runtime_error("sub-sampled framebuffer is empty");
+    const mcpt::Camera cam = mcpt::Camera::canonical(a.width, a.height);
+
+    mcpt::Renderer r(a.device);
+    r.set_traversal(a.traversal);
+    r.upload(scene);
+    r.set_target(W, H);
+    double kernel_ms = 0.0;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int done = 0; done < a.spp; done += a.chunk) {
+      const int n = std::min(a.chunk, a.spp - done);
+      r.render(cam, a.first_pass + done, n, a.date, a.bounces, a.ior, a.variant);
+      kernel_ms += r.last_render_ms();
+    }
+    std::vector<float> img = r.read_image();
+    const double wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (!a.pfm.empty()) mcpt::write_pfm(a.pfm, img, W, H);
+    if (!a.png.empty()) mcpt::write_png(a.png, img, W, H);
+    double mean = 0.0;
+    for (float v : img) mean += v;
+    mean /= (double)(img.size() ? img.size() : 1);
+    const double samples = (double)W * H * a.spp;
+    std::printf("{\"scene\": %d, \"width\": %d, \"height\": %d, \"spp\": %d, \"bounces\": %d, \"ior\": %g, "
+                "\"light\": %g, \"variant\": %d, \"prims\": %d, \"depth\": %d, \"kernel_ms\": %.3f, "
+                "\"wall_ms\": %.3f, \"msamples_per_s\": %.2f, \"mean\": %.6f}\n",
+                a.scene, W, H, a.spp, a.bounces, a.ior, a.light, a.variant, scene.nb_prim(), scene.depth(),
+                kernel_ms, wall_ms, kernel_ms > 0 ? samples / kernel_ms / 1e3 : 0.0, mean);
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "mcpt_render: %s\n", e.what());
+    return 1;
+  }
+  return 0;
+}

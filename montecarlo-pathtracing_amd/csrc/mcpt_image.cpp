@@ -1,0 +1,151 @@
+// mcpt_image.cpp — host half of the output step and the Transfo helpers
+// of the C ABI.
+//
+//  * mcpt_average: the display pass fs_frag, accum / nb (MontecarloGPU/montecarlo.cpp:59-70,
+//    470-476), one binary32 division per channel.
+//  * mcpt_write_pfm: the averaged RGB32F image as a little-endian PFM (row 0 = bottom, which
+//    is both GL's and PFM's row order).
+//  * mcpt_write_png: what the default framebuffer shows: each channel clamped to [0,1] and
+//    converted to 8-bit unorm by round(255·c) (GL float→unorm rule, no gamma), written as an
+//    8-bit RGB PNG (top row first) with stored (uncompressed) deflate blocks.
+//  * mcpt_transfo_*, mcpt_mat4_mul: easycppogl Transfo (gl_eigen.cpp:29-105, degrees) and
+//    Eigen's float product, evaluated with the same arithmetic as the scene producer, so a
+//    C++ caller composing transforms gets the reference's matrices bit for bit.
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "../../include/mcpt.h"
+
+namespace mcpt {
+namespace host {
+void transfo_translate(float x, float y, float z, float* out);
+void transfo_scale(float x, float y, float z, float* out);
+void transfo_rotate(int axis, float deg, float* out);
+void mat4_mul(const float* a, const float* b, float* out);
+}  // namespace host
+}  // namespace mcpt
+
+namespace {
+
+uint32_t crc_table[256];
+bool crc_ready = false;
+
+uint32_t crc32(const unsigned char* p, size_t n, uint32_t c = 0xFFFFFFFFu) {
+  if (!crc_ready) {
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t v = i;
+      for (int k = 0; k < 8; ++k) v = (v & 1) ? 0xEDB88320u ^ (v >> 1) : v >> 1;
+      crc_table[i] = v;
+    }
+    crc_ready = true;
+  }
+  for (size_t i = 0; i < n; ++i) c = crc_table[(c ^ p[i]) & 0xFF] ^ (c >> 8);
+  return c;
+}
+
+void be32(std::vector<unsigned char>& o, uint32_t v) {
+  o.push_back((unsigned char)(v >> 24)); o.push_back((unsigned char)(v >> 16));
+  o.push_back((unsigned char)(v >> 8)); o.push_back((unsigned char)v);
+}
+
+void chunk(std::vector<unsigned char>& out, const char* type, const std::vector<unsigned char>& data) {
+  be32(out, (uint32_t)data.size());
+  std::vector<unsigned char> td(type, type + 4);
+  td.insert(td.end(), data.begin(), data.end());
+  out.insert(out.end(), td.begin(), td.end());
+  be32(out, crc32(td.data(), td.size()) ^ 0xFFFFFFFFu);
+}
+
+unsigned char unorm8(float c) {
+  if (!(c > 0.0f)) return 0;            // also NaN -> 0
+  if (c >= 1.0f) return 255;
+  return (unsigned char)std::lround((double)c * 255.0);
+}
+
+}  // namespace
+
+extern "C" {
+
+int mcpt_average(const float* accum, long long n_values, int pass_count, float* out) {
+  if (!accum || !out || n_values < 0 || pass_count <= 0) return MCPT_ERR_INVALID_ARG;
+  const float nb = (float)pass_count;
+  for (long long i = 0; i < n_values; ++i) out[i] = accum[i] / nb;
+  return MCPT_OK;
+}
+
+int mcpt_write_pfm(const char* path, const float* rgb, int W, int H) {
+  if (!path || !rgb || W <= 0 || H <= 0) return MCPT_ERR_INVALID_ARG;
+  FILE* f = std::fopen(path, "wb");
+  if (!f) return MCPT_ERR_INVALID_ARG;
+  std::fprintf(f, "PF\n%d %d\n-1.0\n", W, H);   // negative scale = little endian
+  const size_t n = (size_t)W * H * 3;
+  const bool ok = std::fwrite(rgb, sizeof(float), n, f) == n;
+  return (std::fclose(f) == 0 && ok) ? MCPT_OK : MCPT_ERR_INVALID_ARG;
+}
+
+int mcpt_write_png(const char* path, const float* rgb, int W, int H) {
+  if (!path || !rgb || W <= 0 || H <= 0 || W > (1 << 24) || H > (1 << 24)) return MCPT_ERR_INVALID_ARG;
+  // raw scanlines, filter 0, top row first (the accumulator's row 0 is the bottom)
+  const size_t row = (size_t)W * 3 + 1;
+  std::vector<unsigned char> raw(row * H);
+  for (int y = 0; y < H; ++y) {
+    unsigned char* r = &raw[(size_t)y * row];
+    r[0] = 0;
+    const float* src = rgb + (size_t)(H - 1 - y) * W * 3;
+    for (int i = 0; i < W * 3; ++i) r[1 + i] = unorm8(src[i]);
+  }
+  // zlib stream of stored blocks (≤ 65535 bytes each) + adler32
+  std::vector<unsigned char> z = {0x78, 0x01};
+  size_t pos = 0;
+  do {
+    const size_t len = std::min<size_t>(65535, raw.size() - pos);
+    const bool last = pos + len == raw.size();
+    z.push_back(last ? 1 : 0);
+    z.push_back((unsigned char)(len & 0xFF)); z.push_back((unsigned char)(len >> 8));
+    z.push_back((unsigned char)(~len & 0xFF)); z.push_back((unsigned char)((~len >> 8) & 0xFF));
+    z.insert(z.end(), raw.begin() + pos, raw.begin() + pos + len);
+    pos += len;
+  } while (pos < raw.size());
+  uint32_t a = 1, b = 0;
+  for (unsigned char c : raw) { a = (a + c) % 65521; b = (b + a) % 65521; }
+  be32(z, (b << 16) | a);
+
+  std::vector<unsigned char> out = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1A, '\n'};
+  std::vector<unsigned char> ihdr;
+  be32(ihdr, (uint32_t)W); be32(ihdr, (uint32_t)H);
+  ihdr.push_back(8); ihdr.push_back(2); ihdr.push_back(0); ihdr.push_back(0); ihdr.push_back(0);
+  chunk(out, "IHDR", ihdr);
+  chunk(out, "IDAT", z);
+  chunk(out, "IEND", {});
+  FILE* f = std::fopen(path, "wb");
+  if (!f) return MCPT_ERR_INVALID_ARG;
+  const bool ok = std::fwrite(out.data(), 1, out.size(), f) == out.size();
+  return (std::fclose(f) == 0 && ok) ? MCPT_OK : MCPT_ERR_INVALID_ARG;
+}
+
+int mcpt_transfo_translate(float x, float y, float z, float* out16) {
+  if (!out16) return MCPT_ERR_INVALID_ARG;
+  mcpt::host::transfo_translate(x, y, z, out16);
+  return MCPT_OK;
+}
+int mcpt_transfo_scale(float x, float y, float z, float* out16) {
+  if (!out16) return MCPT_ERR_INVALID_ARG;
+  mcpt::host::transfo_scale(x, y, z, out16);
+  return MCPT_OK;
+}
+int mcpt_transfo_rotate(int axis, float degrees, float* out16) {
+  if (!out16 || axis < 0 || axis > 2) return MCPT_ERR_INVALID_ARG;
+  mcpt::host::transfo_rotate(axis, degrees, out16);
+  return MCPT_OK;
+}
+int mcpt_mat4_mul(const float* a16, const float* b16, float* out16) {
+  if (!a16 || !b16 || !out16) return MCPT_ERR_INVALID_ARG;
+  mcpt::host::mat4_mul(a16, b16, out16);
+  return MCPT_OK;
+}
+
+}  // extern "C"

@@ -437,6 +437,25 @@ static void canonical_camera(int W, int H, float* invPV, float* invV) {
 }  // namespace host
 }  // namespace mcpt
 
+namespace mcpt {
+namespace host {
+// Transfo / product entry points of the C ABI (mcpt_image.cpp)
+void transfo_translate(float x, float y, float z, float* out) { std::memcpy(out, xf::T(x, y, z).m, 64); }
+void transfo_scale(float x, float y, float z, float* out) { std::memcpy(out, xf::S(x, y, z).m, 64); }
+void transfo_rotate(int axis, float deg, float* out) {
+  const Mat4 r = axis == 0 ? xf::Rx(deg) : (axis == 1 ? xf::Ry(deg) : xf::Rz(deg));
+  std::memcpy(out, r.m, 64);
+}
+void mat4_mul(const float* a, const float* b, float* out) {
+  Mat4 A, B;
+  std::memcpy(A.m, a, 64);
+  std::memcpy(B.m, b, 64);
+  const Mat4 r = A * B;
+  std::memcpy(out, r.m, 64);
+}
+}  // namespace host
+}  // namespace mcpt
+
 // ======================================================================================
 // C ABI — scene half
 // ======================================================================================

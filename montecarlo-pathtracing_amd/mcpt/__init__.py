@@ -27,6 +27,7 @@ __all__ = [
     "MCPTError", "lib", "lib_path", "Scene", "Renderer", "camera_canonical",
     "MONTECARLO", "MAT", "MAT_TR", "EVENT_NAMES", "SCENE_KEYS",
     "TRAVERSAL_AUTO", "TRAVERSAL_LANE", "TRAVERSAL_WAVE",
+    "Transfo", "average", "write_pfm", "write_png", "material", "light",
 ]
 
 MONTECARLO, MAT, MAT_TR = 0, 1, 2
@@ -93,6 +94,13 @@ def _declare(L: ctypes.CDLL) -> None:
         "mcpt_scene_set_material": (i, [_vp, i, fp]),
         "mcpt_scene_build_reference": (i, [_vp, i, f]),
         "mcpt_camera_canonical": (i, [i, i, fp, fp]),
+        "mcpt_transfo_translate": (i, [f, f, f, fp]),
+        "mcpt_transfo_scale": (i, [f, f, f, fp]),
+        "mcpt_transfo_rotate": (i, [i, f, fp]),
+        "mcpt_mat4_mul": (i, [fp, fp, fp]),
+        "mcpt_average": (i, [fp, ctypes.c_longlong, i, fp]),
+        "mcpt_write_pfm": (i, [ctypes.c_char_p, fp, i, i]),
+        "mcpt_write_png": (i, [ctypes.c_char_p, fp, i, i]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -240,6 +248,70 @@ def camera_canonical(W: int, H: int) -> Tuple[np.ndarray, np.ndarray]:
     iv = np.zeros(16, np.float32)
     _check(lib().mcpt_camera_canonical(int(W), int(H), _fp(ipv), _fp(iv)), "mcpt_camera_canonical")
     return ipv, iv
+
+
+# ---- Transfo (easycppogl/gl_eigen.cpp:29-105) and GLMat4 product, computed by libmcpt
+def _m16(fn, *args) -> np.ndarray:
+    out = np.zeros(16, np.float32)
+    _check(getattr(lib(), fn)(*args, _fp(out)), fn)
+    return out
+
+
+class Transfo:
+    """Reference Transfo: 4x4 column-major float matrices (16 floats), angles in degrees."""
+
+    @staticmethod
+    def translate(x, y, z) -> np.ndarray:
+        return _m16("mcpt_transfo_translate", float(x), float(y), float(z))
+
+    @staticmethod
+    def scale(sx, sy=None, sz=None) -> np.ndarray:
+        sy = sx if sy is None else sy
+        sz = sx if sz is None else sz
+        return _m16("mcpt_transfo_scale", float(sx), float(sy), float(sz))
+
+    @staticmethod
+    def rotateX(deg) -> np.ndarray:
+        return _m16("mcpt_transfo_rotate", 0, float(deg))
+
+    @staticmethod
+    def rotateY(deg) -> np.ndarray:
+        return _m16("mcpt_transfo_rotate", 1, float(deg))
+
+    @staticmethod
+    def rotateZ(deg) -> np.ndarray:
+        return _m16("mcpt_transfo_rotate", 2, float(deg))
+
+    @staticmethod
+    def mul(*ms) -> np.ndarray:
+        """Product a * b * ... in the reference's float arithmetic (left to right)."""
+        acc = _f32(ms[0], 16)
+        for m in ms[1:]:
+            b = _f32(m, 16)
+            out = np.zeros(16, np.float32)
+            _check(lib().mcpt_mat4_mul(_fp(acc), _fp(b), _fp(out)), "mcpt_mat4_mul")
+            acc = out
+        return acc
+
+
+# ---- output step (SURVEY §8f row 1)
+def average(accum: np.ndarray, pass_count: int) -> np.ndarray:
+    """fs_frag: accum / nb (montecarlo.cpp:59-70), binary32 per channel."""
+    a = np.ascontiguousarray(accum, np.float32)
+    out = np.empty_like(a)
+    _check(lib().mcpt_average(_fp(a), a.size, int(pass_count), _fp(out)), "mcpt_average")
+    return out
+
+
+def write_pfm(path: str, rgb: np.ndarray) -> None:
+    a = np.ascontiguousarray(rgb, np.float32)
+    _check(lib().mcpt_write_pfm(str(path).encode(), _fp(a), a.shape[1], a.shape[0]), "mcpt_write_pfm")
+
+
+def write_png(path: str, rgb: np.ndarray) -> None:
+    """8-bit framebuffer view: clamp [0,1], round(255·c), no gamma (GL unorm conversion)."""
+    a = np.ascontiguousarray(rgb, np.float32)
+    _check(lib().mcpt_write_png(str(path).encode(), _fp(a), a.shape[1], a.shape[0]), "mcpt_write_png")
 
 
 class Renderer:
