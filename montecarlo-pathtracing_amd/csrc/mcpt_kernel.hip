@@ -94,6 +94,9 @@ struct Counters {
 template <bool COUNT>
 struct Ev {
   Counters c;
+#ifdef MCPT_STAMPS
+  unsigned long long st_leaf = 0;   // diagnostic: wave-cycles in the traversal's leaf blocks
+#endif
   __device__ __forceinline__ void init() { if (COUNT) for (int i = 0; i < EV_COUNT; ++i) c.v[i] = 0; }
   __device__ __forceinline__ void inc(int e) { if (COUNT) c.v[e]++; }
 };
@@ -257,13 +260,20 @@ __device__ __forceinline__ void traverse_lane(const SceneRef& s, f3 O, f3 D, Hit
   int node = 0, level = 0;
   uint32_t pending = 0;
   for (;;) {
-    bool pop;
-    if (node >= leaf0) {
+    bool pop = true;
+    const bool is_leaf = node >= leaf0;
+#ifdef MCPT_STAMPS
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();   // wave-uniform stamps
+#endif
+    if (is_leaf) {
       ev.inc(EV_LEAF);
       int p = s.leaves[node - leaf0];
       if (p >= 0) prim_test<COUNT, false>(s, p, O, D, h, ev);
-      pop = true;
-    } else {
+    }
+#ifdef MCPT_STAMPS
+    ev.st_leaf += __builtin_amdgcn_s_memtime() - t0;
+#endif
+    if (!is_leaf) {
       ev.inc(EV_NODE);
       const size_t j = 2 * (size_t)node + 1;
       const float4 l0 = s.nodes[j * 3], r0 = s.nodes[j * 3 + 3];
@@ -286,6 +296,55 @@ __device__ __forceinline__ void traverse_lane(const SceneRef& s, f3 O, f3 D, Hit
       node = ((node + 1) >> (level - L)) - 2;
       level = L;
     }
+  }
+}
+
+// intersect_bvh per lane, "while-while" schedule (Aila & Laine, non-speculative): the wave
+// runs internal-node steps while any lane sits on an internal node (lanes on a leaf wait),
+// then one leaf step for every lane on a leaf.  Each lane's own visit sequence is the
+// reference's; only the interleaving across lanes changes.  Diagnostic variant
+// (MCPT_WHILE_WHILE); the default is the if-if loop of traverse_lane.
+template <bool COUNT>
+__device__ __forceinline__ void traverse_lane_ww(const SceneRef& s, f3 O, f3 D, Hit& h, Ev<COUNT>& ev) {
+  ev.inc(EV_TRAV);
+  h.index = -1; h.dist = kFLTMAX; h.shape = -1; h.dir = -1; h.cull2 = cull_bound_sq(kFLTMAX);
+  const f3 invD = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);
+  const int leaf0 = (1 << s.depth) - 1;
+  int node = 0, level = 0;
+  uint32_t pending = 0;
+  bool done = false;
+  auto pop = [&]() {
+    if (pending == 0) { done = true; return; }
+    int L = 31 - __builtin_clz(pending);
+    pending &= ~(1u << L);
+    node = ((node + 1) >> (level - L)) - 2;
+    level = L;
+  };
+  for (;;) {
+    while (__ballot(!done && node < leaf0)) {
+      if (!done && node < leaf0) {
+        ev.inc(EV_NODE);
+        const size_t j = 2 * (size_t)node + 1;
+        const float4 l0 = s.nodes[j * 3], r0 = s.nodes[j * 3 + 3];
+        bool hl = (COUNT || l0.w != 0.0f) && box_test<false>(l0, s.nodes[j * 3 + 1], s.nodes[j * 3 + 2], O, D, invD, h.cull2);
+        bool hr = (COUNT || r0.w != 0.0f) && box_test<false>(r0, s.nodes[j * 3 + 4], s.nodes[j * 3 + 5], O, D, invD, h.cull2);
+        if (hr) {
+          if (hl) pending |= 1u << (level + 1);
+          node = (int)j + 1; level++;
+        } else if (hl) {
+          node = (int)j; level++;
+        } else {
+          pop();
+        }
+      }
+    }
+    if (!done) {   // every live lane is on a leaf
+      ev.inc(EV_LEAF);
+      int p = s.leaves[node - leaf0];
+      if (p >= 0) prim_test<COUNT, false>(s, p, O, D, h, ev);
+      pop();
+    }
+    if (__ballot(!done) == 0) break;
   }
 }
 
@@ -352,7 +411,11 @@ __device__ __forceinline__ void traverse_wave(const SceneRef& s, f3 O, f3 D, Hit
 template <bool COUNT, bool WAVE>
 __device__ __forceinline__ void traverse(const SceneRef& s, f3 O, f3 D, Hit& h, Ev<COUNT>& ev) {
   if (WAVE) traverse_wave<COUNT>(s, O, D, h, ev);
+#ifdef MCPT_WHILE_WHILE
+  else traverse_lane_ww<COUNT>(s, O, D, h, ev);
+#else
   else traverse_lane<COUNT>(s, O, D, h, ev);
+#endif
 }
 
 // intersection_info raytracer_func.frag:812-897 (hit only; misses leave N,P untouched)
@@ -649,16 +712,17 @@ __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParam
 #ifdef MCPT_STAMPS
   {
     // wave totals = the last-finishing lane's sums (max over lanes); lane-iterations summed
-    unsigned long long vals[5] = {__builtin_amdgcn_s_memtime() - st_k0, st_p, st_t, st_s, st_it};
+    unsigned long long vals[6] = {__builtin_amdgcn_s_memtime() - st_k0, st_p, st_t, st_s, st_it, ev.st_leaf};
     unsigned long long it_sum = st_it;
     for (int off = 32; off > 0; off >>= 1) {
-      for (int k = 0; k < 5; ++k) { unsigned long long o = __shfl_xor(vals[k], off); vals[k] = vals[k] > o ? vals[k] : o; }
+      for (int k = 0; k < 6; ++k) { unsigned long long o = __shfl_xor(vals[k], off); vals[k] = vals[k] > o ? vals[k] : o; }
       it_sum += __shfl_xor(it_sum, off);
     }
     if (lane == 0 && p.events) {
       for (int k = 0; k < 5; ++k) atomicAdd(p.events + k, vals[k]);
       atomicAdd(p.events + 5, it_sum);
       atomicAdd(p.events + 6, 1ull);
+      atomicAdd(p.events + 7, vals[5]);
     }
   }
 #endif

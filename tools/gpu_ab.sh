@@ -11,6 +11,10 @@ timeout -k 10 900 python -m pytest tests -m gpu -x -q > $O/pytest_gpu.log 2>&1; 
 tail -3 $O/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
 for w in $VARS; do
+  # parity of the variant itself (bit-exact vs the oracle) before timing it
+  MCPT_LIB=montecarlo-pathtracing_amd/mcpt/variants/libmcpt_$w.so timeout -k 10 600 \
+    python -m pytest tests/test_gpu_parity.py -m gpu -x -q -k "scene_parity or event_counters or full_hd" \
+    > $O/pytest_$w.log 2>&1 || { echo "variant $w parity FAILED"; tail -20 $O/pytest_$w.log; exit 1; }
   MCPT_LIB=montecarlo-pathtracing_amd/mcpt/variants/libmcpt_$w.so timeout -k 10 300 \
     python tools/ab_time.py --scenes $SCENES --modes 1 2 --tag $w >> $O/ab.jsonl 2>> $O/ab.err || exit $?
 done
