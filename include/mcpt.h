@@ -128,6 +128,31 @@ int mcpt_copy_accum_device(mcpt_ctx* ctx, void* dst_dev_ptr, size_t bytes);
 int mcpt_set_traversal(mcpt_ctx* ctx, int mode);
 int mcpt_get_traversal(mcpt_ctx* ctx, int* resolved_mode);
 
+/* Ray queries on the uploaded scene — the shader library calls a TP integrator may use
+ * (raytracer_func.frag:718-781, 874-907): traverse_all_bvh (any_hit = 0) or just_hit_bvh
+ * (any_hit = 1: stop at the first primitive hit), or with prim >= 0 intersect_one_prim /
+ * hit_one_prim (that primitive only), then intersection_info / _color_info / _mat_info.
+ * origins, dirs: n × 3 f32 host arrays (directions used as given, like the shader).  A miss
+ * has shape = -1, dist = FLT_MAX and zero N/P/colour/material.  Synchronous. */
+typedef struct mcpt_hit {
+  int shape;          /* primitive type code of the hit (1 sphere .. 5 quad), -1 = miss */
+  int prim;           /* primitive index (after sortEmissiveFirst) */
+  int dir;            /* face / part code of the hit (closest_intersection.dir) */
+  float dist;         /* world distance from the origin */
+  float pl[3], pg[3]; /* hit point in primitive space / world space */
+  float N[3], P[3];   /* intersection_info: normal and position */
+  float color[4];     /* intersection_color_info (rgb, opacity) */
+  float material[4];  /* intersection_mat_info (shininess, roughness, emissivity, area) */
+} mcpt_hit;
+int mcpt_trace(mcpt_ctx* ctx, const float* origins, const float* dirs, int n, int any_hit, int prim,
+               mcpt_hit* out);
+
+/* DrawSampling's point cloud (DrawSampling/draw_sampling.cpp:144-150, tp/sampling_base.vert
+ * seeding, tp/hsphere.vert random_ray): point k = random_ray(normalize(normal), roughness)
+ * with seed floatBitsToUint(fseed) + k * nb_used * (11, 43, 67).  out: n × 3 f32 (host). */
+int mcpt_sample_hemisphere(mcpt_ctx* ctx, const float* normal3, const float* fseed3, float roughness,
+                           int nb_used, int n, float* out_xyz);
+
 /* Use an external hipStream_t (e.g. torch's current stream); NULL = library stream. */
 int mcpt_set_stream(mcpt_ctx* ctx, void* hip_stream);
 int mcpt_synchronize(mcpt_ctx* ctx);

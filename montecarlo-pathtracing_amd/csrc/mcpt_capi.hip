@@ -352,6 +352,62 @@ int mcpt_copy_accum_device(mcpt_ctx* c, void* dst, size_t bytes) {
   return MCPT_OK;
 }
 
+int mcpt_trace(mcpt_ctx* c, const float* origins, const float* dirs, int n, int any_hit, int prim, mcpt_hit* out) {
+  if (!c || n < 0 || (n > 0 && (!origins || !dirs || !out))) return set_err(MCPT_ERR_INVALID_ARG, "mcpt_trace: bad arguments");
+  if (!c->has_scene) return set_err(MCPT_ERR_NO_SCENE, "no scene uploaded");
+  if (prim >= c->n_prims) return set_err(MCPT_ERR_INVALID_ARG, "mcpt_trace: primitive index out of range");
+  if (n == 0) return MCPT_OK;
+  HIP_OR_RETURN(hipSetDevice(c->device));
+  const size_t n3 = (size_t)n * 3 * sizeof(float), ni = (size_t)n * 3 * sizeof(int);
+  const size_t nf = (size_t)n * mcpt::kTraceFloats * sizeof(float);
+  char* buf = nullptr;
+  HIP_OR_RETURN(hipMalloc(&buf, 2 * n3 + ni + nf));
+  mcpt::TraceParams q;
+  q.nodes = c->d_nodes; q.leaves = c->d_leaves; q.ptype = c->d_ptype; q.prims = c->d_prims; q.depth = c->depth;
+  q.prim = prim < 0 ? -1 : prim;
+  q.orig = (const float*)buf; q.dir = (const float*)(buf + n3);
+  q.out_i = (int*)(buf + 2 * n3); q.out = (float*)(buf + 2 * n3 + ni); q.n = n;
+  std::vector<int> hi((size_t)n * 3);
+  std::vector<float> hf((size_t)n * mcpt::kTraceFloats);
+  hipError_t e = hipMemcpyAsync(buf, origins, n3, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(buf + n3, dirs, n3, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = mcpt_launch_trace(q, any_hit != 0, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(hi.data(), q.out_i, ni, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(hf.data(), q.out, nf, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(buf);
+  if (e != hipSuccess) return set_err(MCPT_ERR_HIP, "mcpt_trace", e);
+  for (int i = 0; i < n; ++i) {
+    mcpt_hit& h = out[i];
+    const int* a = &hi[(size_t)i * 3];
+    const float* f = &hf[(size_t)i * mcpt::kTraceFloats];
+    h.shape = a[0]; h.prim = a[1]; h.dir = a[2];
+    h.dist = f[0];
+    std::memcpy(h.pl, f + 1, 12); std::memcpy(h.pg, f + 4, 12);
+    std::memcpy(h.N, f + 7, 12); std::memcpy(h.P, f + 10, 12);
+    std::memcpy(h.color, f + 13, 16); std::memcpy(h.material, f + 17, 16);
+  }
+  return MCPT_OK;
+}
+
+int mcpt_sample_hemisphere(mcpt_ctx* c, const float* normal3, const float* fseed3, float roughness, int nb_used,
+                           int n, float* out_xyz) {
+  if (!c || !normal3 || !fseed3 || n < 0 || nb_used < 0 || (n > 0 && !out_xyz))
+    return set_err(MCPT_ERR_INVALID_ARG, "mcpt_sample_hemisphere: bad arguments");
+  if (n == 0) return MCPT_OK;
+  HIP_OR_RETURN(hipSetDevice(c->device));
+  mcpt::SampleParams q;
+  for (int k = 0; k < 3; ++k) { q.normal[k] = normal3[k]; q.fseed[k] = fseed3[k]; }
+  q.roughness = roughness; q.nb_used = (uint32_t)nb_used; q.n = n;
+  HIP_OR_RETURN(hipMalloc(&q.out, (size_t)n * 3 * sizeof(float)));
+  hipError_t e = mcpt_launch_sample(q, c->stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(out_xyz, q.out, (size_t)n * 3 * sizeof(float), hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(q.out);
+  if (e != hipSuccess) return set_err(MCPT_ERR_HIP, "mcpt_sample_hemisphere", e);
+  return MCPT_OK;
+}
+
 int mcpt_set_traversal(mcpt_ctx* c, int mode) {
   if (!c || mode < MCPT_TRAVERSAL_AUTO || mode > MCPT_TRAVERSAL_WAVE)
     return set_err(MCPT_ERR_INVALID_ARG, "mcpt_set_traversal: bad mode");

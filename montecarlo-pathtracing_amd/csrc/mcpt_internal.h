@@ -55,7 +55,34 @@ struct RenderParams {
   float date, ior;
 };
 
+// ray-query batch (mcpt_trace): per ray 3 ints (shape, prim, dir) and kTraceFloats floats
+// (dist, pl.xyz, pg.xyz, N.xyz, P.xyz, colour rgba, material rgba) — the mcpt_hit layout
+constexpr int kTraceFloats = 21;
+struct TraceParams {
+  const float4* nodes;
+  const int* leaves;
+  const int* ptype;
+  const float4* prims;
+  int depth;
+  int prim;                     // -1: whole BVH, >= 0: this primitive only
+  const float* orig;            // n × 3
+  const float* dir;             // n × 3
+  long long n;
+  int* out_i;                   // n × 3
+  float* out;                   // n × kTraceFloats
+};
+
+struct SampleParams {
+  float normal[3], fseed[3];
+  float roughness;
+  uint32_t nb_used;
+  long long n;
+  float* out;                   // n × 3
+};
+
 }  // namespace mcpt
 
+hipError_t mcpt_launch_trace(const mcpt::TraceParams& q, bool any_hit, hipStream_t stream);
+hipError_t mcpt_launch_sample(const mcpt::SampleParams& q, hipStream_t stream);
 hipError_t mcpt_launch_render(const mcpt::RenderParams& p, bool count, hipStream_t stream);
 hipError_t mcpt_launch_combine(const mcpt::RenderParams& p, hipStream_t stream);

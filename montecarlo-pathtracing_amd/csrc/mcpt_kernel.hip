@@ -251,7 +251,9 @@ __device__ __forceinline__ void prim_test(const SceneRef& s, int i, f3 Ow, f3 Dw
 // intersect_bvh raytracer_func.frag:734-769, per lane, stackless.  pending bit L = "a left
 // sibling at level L waits on the reference's stack"; popping the deepest pending bit is
 // exactly the reference's LIFO order (right child first, cull decided at push time).
-template <bool COUNT>
+// ANY: just_hit_bvh (raytracer_func.frag:771-775) — stop at the first leaf whose primitive
+// produced a hit (hit_only, :756-757); the render path always uses traverse_all_bvh.
+template <bool COUNT, bool ANY = false>
 __device__ __forceinline__ void traverse_lane(const SceneRef& s, f3 O, f3 D, Hit& h, Ev<COUNT>& ev) {
   ev.inc(EV_TRAV);
   h.index = -1; h.dist = kFLTMAX; h.shape = -1; h.dir = -1; h.cull2 = cull_bound_sq(kFLTMAX);
@@ -269,6 +271,7 @@ __device__ __forceinline__ void traverse_lane(const SceneRef& s, f3 O, f3 D, Hit
       ev.inc(EV_LEAF);
       int p = s.leaves[node - leaf0];
       if (p >= 0) prim_test<COUNT, false>(s, p, O, D, h, ev);
+      if (ANY && h.shape >= 0) break;
     }
 #ifdef MCPT_STAMPS
     ev.st_leaf += __builtin_amdgcn_s_memtime() - t0;
@@ -758,7 +761,75 @@ __global__ __launch_bounds__(256) void combine_kernel(float* __restrict__ accum,
   accum[i * 3] = a0; accum[i * 3 + 1] = a1; accum[i * 3 + 2] = a2;
 }
 
+// ------------------------------------------------------------------------------------
+// ray queries: the shader library's traverse_all_bvh / just_hit_bvh / intersect_one_prim /
+// hit_one_prim + intersection_info + intersection_color_info / _mat_info
+// (raytracer_func.frag:718-781, 874-907) for caller-supplied rays, one lane per ray
+// ------------------------------------------------------------------------------------
+template <bool ANY>
+__global__ __launch_bounds__(256) void trace_kernel(TraceParams q) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= q.n) return;
+  SceneRef s{q.nodes, q.leaves, q.ptype, q.prims, q.depth};
+  Ev<false> ev;
+  const f3 O = mk(q.orig[3 * i], q.orig[3 * i + 1], q.orig[3 * i + 2]);
+  const f3 D = mk(q.dir[3 * i], q.dir[3 * i + 1], q.dir[3 * i + 2]);
+  Hit h;
+  h.pl = mk(0.0f, 0.0f, 0.0f); h.pg = h.pl; h.cull2 = 0.0;
+  if (q.prim < 0) {
+    traverse_lane<false, ANY>(s, O, D, h, ev);
+  } else {                                       // intersect_one_prim / hit_one_prim
+    h.index = -1; h.dist = kFLTMAX; h.shape = -1; h.dir = -1; h.cull2 = cull_bound_sq(kFLTMAX);
+    prim_test<false, false>(s, q.prim, O, D, h, ev);
+  }
+  float* o = q.out + i * kTraceFloats;
+  int* oi = q.out_i + i * 3;
+  oi[0] = h.shape; oi[1] = h.index; oi[2] = h.dir;
+  f3 N = mk(0.0f, 0.0f, 0.0f), P = N;
+  float4 col = make_float4(0.0f, 0.0f, 0.0f, 0.0f), mat = col;
+  if (h.shape >= 0) {
+    geom_info<false>(s, h, N, P, ev);
+    col = s.prims[(size_t)h.index * 8 + 6];
+    mat = s.prims[(size_t)h.index * 8 + 7];
+  }
+  const float v[kTraceFloats] = {h.shape >= 0 ? h.dist : kFLTMAX, h.pl.x, h.pl.y, h.pl.z, h.pg.x, h.pg.y, h.pg.z,
+                                 N.x, N.y, N.z, P.x, P.y, P.z, col.x, col.y, col.z, col.w, mat.x, mat.y, mat.z, mat.w};
+#pragma unroll
+  for (int k = 0; k < kTraceFloats; ++k) o[k] = v[k];
+}
+
+// DrawSampling's point cloud (tp/sampling_base.vert:23-26 seeding + tp/hsphere.vert
+// random_ray): point k = random_ray(normalize(normal), roughness) with the RNG seeded at
+// floatBitsToUint(fseed) + k * nb_used * (11, 43, 67)
+__global__ __launch_bounds__(256) void sample_kernel(SampleParams q) {
+  const long long k = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (k >= q.n) return;
+  const uint32_t step = (uint32_t)k * q.nb_used;
+  Rng rng;
+  rng.x = fbits(q.fseed[0]) + step * 11u;
+  rng.y = fbits(q.fseed[1]) + step * 43u;
+  rng.z = fbits(q.fseed[2]) + step * 67u;
+  const f3 n = normalize3(mk(q.normal[0], q.normal[1], q.normal[2]));
+  const f3 r = random_ray(rng, n, q.roughness);
+  q.out[3 * k] = r.x; q.out[3 * k + 1] = r.y; q.out[3 * k + 2] = r.z;
+}
+
 }  // namespace mcpt
+
+hipError_t mcpt_launch_trace(const mcpt::TraceParams& q, bool any_hit, hipStream_t stream) {
+  if (q.n <= 0) return hipSuccess;
+  dim3 block(256), grid((unsigned)((q.n + 255) / 256));
+  if (any_hit) hipLaunchKernelGGL(mcpt::trace_kernel<true>, grid, block, 0, stream, q);
+  else hipLaunchKernelGGL(mcpt::trace_kernel<false>, grid, block, 0, stream, q);
+  return hipGetLastError();
+}
+
+hipError_t mcpt_launch_sample(const mcpt::SampleParams& q, hipStream_t stream) {
+  if (q.n <= 0) return hipSuccess;
+  dim3 block(256), grid((unsigned)((q.n + 255) / 256));
+  hipLaunchKernelGGL(mcpt::sample_kernel, grid, block, 0, stream, q);
+  return hipGetLastError();
+}
 
 // ------------------------------------------------------------------------------------
 // launch wrapper (host)

@@ -27,7 +27,7 @@ __all__ = [
     "MCPTError", "lib", "lib_path", "Scene", "Renderer", "camera_canonical",
     "MONTECARLO", "MAT", "MAT_TR", "EVENT_NAMES", "SCENE_KEYS",
     "TRAVERSAL_AUTO", "TRAVERSAL_LANE", "TRAVERSAL_WAVE",
-    "Transfo", "average", "write_pfm", "write_png", "material", "light",
+    "Transfo", "average", "write_pfm", "write_png", "material", "light", "Hit", "HIT_DTYPE",
 ]
 
 MONTECARLO, MAT, MAT_TR = 0, 1, 2
@@ -41,6 +41,18 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 
 class MCPTError(RuntimeError):
     pass
+
+
+class Hit(ctypes.Structure):
+    """mcpt_hit (include/mcpt.h): one ray-query result."""
+    _fields_ = [("shape", ctypes.c_int), ("prim", ctypes.c_int), ("dir", ctypes.c_int), ("dist", ctypes.c_float),
+                ("pl", ctypes.c_float * 3), ("pg", ctypes.c_float * 3), ("N", ctypes.c_float * 3),
+                ("P", ctypes.c_float * 3), ("color", ctypes.c_float * 4), ("material", ctypes.c_float * 4)]
+
+
+HIT_DTYPE = np.dtype([("shape", "<i4"), ("prim", "<i4"), ("dir", "<i4"), ("dist", "<f4"), ("pl", "<f4", 3),
+                      ("pg", "<f4", 3), ("N", "<f4", 3), ("P", "<f4", 3), ("color", "<f4", 4),
+                      ("material", "<f4", 4)])
 
 
 def lib_path() -> str:
@@ -73,6 +85,8 @@ def _declare(L: ctypes.CDLL) -> None:
         "mcpt_accum_device_ptr": (i, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(ctypes.c_size_t)]),
         "mcpt_copy_accum_device": (i, [_vp, _vp, ctypes.c_size_t]),
         "mcpt_set_traversal": (i, [_vp, i]),
+        "mcpt_trace": (i, [_vp, fp, fp, i, i, i, _vp]),
+        "mcpt_sample_hemisphere": (i, [_vp, fp, fp, f, i, i, fp]),
         "mcpt_get_traversal": (i, [_vp, ip]),
         "mcpt_set_stream": (i, [_vp, _vp]),
         "mcpt_synchronize": (i, [_vp]),
@@ -415,6 +429,28 @@ class Renderer:
         """D2D copy of the local accumulator into a device buffer (ordered on our stream)."""
         _check(lib().mcpt_copy_accum_device(self._h, _vp(dst_ptr), ctypes.c_size_t(nbytes)),
                "mcpt_copy_accum_device")
+
+    def trace(self, origins, dirs, any_hit: bool = False, prim: int = -1) -> np.ndarray:
+        """Ray queries (traverse_all_bvh / just_hit_bvh, or one primitive) + intersection_info.
+        Returns a structured array of HIT_DTYPE records (shape -1 = miss)."""
+        o = np.ascontiguousarray(np.asarray(origins, np.float32).reshape(-1, 3))
+        d = np.ascontiguousarray(np.asarray(dirs, np.float32).reshape(-1, 3))
+        if o.shape != d.shape:
+            raise ValueError("origins and dirs must have the same shape")
+        out = np.zeros(o.shape[0], HIT_DTYPE)
+        assert HIT_DTYPE.itemsize == ctypes.sizeof(Hit)
+        _check(lib().mcpt_trace(self._h, _fp(o), _fp(d), o.shape[0], int(bool(any_hit)), int(prim),
+                                out.ctypes.data_as(_vp)), "mcpt_trace")
+        return out
+
+    def sample_hemisphere(self, normal, fseed, n: int, roughness: float = 1.0, nb_used: int = 3) -> np.ndarray:
+        """DrawSampling point cloud: n directions random_ray(normalize(normal), roughness)."""
+        nrm = _f32(normal, 3)
+        sd = _f32(fseed, 3)
+        out = np.zeros((int(n), 3), np.float32)
+        _check(lib().mcpt_sample_hemisphere(self._h, _fp(nrm), _fp(sd), float(roughness), int(nb_used), int(n),
+                                            _fp(out)), "mcpt_sample_hemisphere")
+        return out
 
     def set_traversal(self, mode: int) -> None:
         """BVH traversal strategy: TRAVERSAL_AUTO / _LANE / _WAVE (same results)."""

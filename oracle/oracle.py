@@ -57,6 +57,8 @@ def lib() -> ctypes.CDLL:
             "orc_random_ray": (None, [_up, _fp, f, _fp, _up]),
             "orc_intersect_prim": (i, [_fp, _fp, _fp, _fp, _ip, _fp, _fp]),
             "orc_corner_rays": (None, [_fp, _fp, _fp]),
+            "orc_trace": (i, [_fp, i, _fp, _ip, i, _fp, _fp, i, i, i, _ip, _fp]),
+            "orc_sample_hemisphere": (None, [_fp, _fp, f, i, i, _fp]),
         }
         for name, (res, args) in sigs.items():
             fn = getattr(L, name)
@@ -157,6 +159,30 @@ def intersect_prim(rec64, O, D):
     pg = np.zeros(3, np.float32)
     shape = lib().orc_intersect_prim(P(rec), P(o), P(d), ctypes.byref(dist), ctypes.byref(dr), P(pl), P(pg))
     return shape, dist.value, dr.value, pl, pg
+
+
+def trace(prims, nodes, leaves, depth, origins, dirs, any_hit=False, prim=-1):
+    """(ints n×3 [shape, prim, dir], floats n×21 [dist, pl, pg, N, P, colour, material])."""
+    prims = np.ascontiguousarray(prims, np.float32)
+    nodes = np.ascontiguousarray(nodes, np.float32)
+    leaves = np.ascontiguousarray(leaves, np.int32)
+    o = np.ascontiguousarray(np.asarray(origins, np.float32).reshape(-1, 3))
+    d = np.ascontiguousarray(np.asarray(dirs, np.float32).reshape(-1, 3))
+    n = o.shape[0]
+    oi = np.zeros((n, 3), np.int32)
+    of = np.zeros((n, 21), np.float32)
+    r = lib().orc_trace(P(prims), prims.size // 64, P(nodes), P(leaves, _ip), int(depth), P(o), P(d), n,
+                        int(bool(any_hit)), int(prim), P(oi, _ip), P(of))
+    if r != 0:
+        raise RuntimeError("orc_trace failed")
+    return oi, of
+
+
+def sample_hemisphere(normal, fseed, n, roughness=1.0, nb_used=3):
+    out = np.zeros((int(n), 3), np.float32)
+    lib().orc_sample_hemisphere(P(np.ascontiguousarray(normal, np.float32)), P(np.ascontiguousarray(fseed, np.float32)),
+                                float(roughness), int(nb_used), int(n), P(out))
+    return out
 
 
 def corner_rays(invPV, invV) -> np.ndarray:

@@ -294,6 +294,32 @@ def intersect_prim(rec, Ow, Dw):
                     cl, al = 2, a
         if al < FMAX:
             cand(al, 3, cl)
+    elif t == 4:   # Cone_intersect :579-640 (backward roots accepted: no a > EPS check)
+        cl, tl = -1, FMAX
+        if abs(D[2]) > EPS:
+            t0 = f32(f32(f32(-1.0) - O[2]) / D[2])
+            if t0 > EPS:
+                rx, ry = f32(O[0] + f32(t0 * D[0])), f32(O[1] + f32(t0 * D[1]))
+                if fma32(ry, ry, f32(rx * rx)) < 1 and t0 < tl:
+                    cl, tl = 0, t0
+        co = [O[0], O[1], f32(O[2] - f32(1.0))]
+        a = f32(f32(D[2] * D[2]) - f32(0.8))
+        b = f32(f32(2.0) * f32(f32(D[2] * co[2]) - f32(dot3(D, co) * f32(0.8))))
+        c = f32(f32(co[2] * co[2]) - f32(dot3(co, co) * f32(0.8)))
+        det = f32(f32(b * b) - f32(f32(f32(4.0) * a) * c))
+        if det > 0:
+            det = f32(np.sqrt(det))
+            t1 = f32(f32(-b - det) / f32(f32(2.0) * a))
+            if abs(f32(O[2] + f32(t1 * D[2]))) > 1:
+                t1 = FMAX
+            t2 = f32(f32(-b + det) / f32(f32(2.0) * a))
+            if abs(f32(O[2] + f32(t2 * D[2]))) > 1:
+                t2 = FMAX
+            tt = t2 if t2 < t1 else t1          # GLSL min
+            if tt < tl:
+                cl, tl = 2, tt
+        if tl < FMAX:
+            cand(tl, 4, cl)
     return best
 
 
@@ -377,6 +403,68 @@ def make_prim_kat(rng, prims_by_scene):
             "ip_dir": np.array(dr, np.int32), "ip_pl": np.array(pl, np.float32), "ip_pg": np.array(pg, np.float32)}
 
 
+def cone_record(rng):
+    """A PrimData record (scene.h:64-73) of a cone at a random pose: T·Rz·Ry·S in float32,
+    inverse via float64."""
+    ang = rng.uniform(-np.pi, np.pi, 2)
+    cz, sz, cy, sy = np.cos(ang[0]), np.sin(ang[0]), np.cos(ang[1]), np.sin(ang[1])
+    Rz = np.array([[cz, -sz, 0, 0], [sz, cz, 0, 0], [0, 0, 1, 0], [0, 0, 0, 1]])
+    Ry = np.array([[cy, 0, sy, 0], [0, 1, 0, 0], [-sy, 0, cy, 0], [0, 0, 0, 1]])
+    S = np.diag(list(rng.uniform(5, 40, 3)) + [1.0])
+    T = np.eye(4)
+    T[:3, 3] = rng.uniform(-100, 100, 3)
+    M = (T @ Rz @ Ry @ S).astype(np.float32)
+    inv = np.linalg.inv(M.astype(np.float64)).astype(np.float32)
+    rec = np.zeros(64, np.float32)
+    rec[0:16] = M.T.reshape(-1)          # column-major
+    rec[16:32] = inv.T.reshape(-1)
+    rec[32:48] = rec[0:16]
+    rec[48] = 4.0
+    rec[52:56] = [0.9, 0.9, 0.0, 1.0]
+    rec[56:60] = [0.3, 0.6, 0.0, 0.0]
+    return rec
+
+
+def make_cone_kat(rng):
+    recs, O, D, shape, dist, dr, pl, pg = [], [], [], [], [], [], [], []
+    for _ in range(8):
+        rec = cone_record(rng)
+        c = rec[12:15].astype(np.float64)
+        for _ in range(12):
+            o = (c + rng.normal(scale=120, size=3)).astype(np.float32)
+            d = (c + rng.normal(scale=15, size=3) - o)
+            d = (d / np.linalg.norm(d)).astype(np.float32)
+            b = intersect_prim(rec, list(o), list(d))
+            recs.append(rec); O.append(o); D.append(d)
+            shape.append(b["shape"]); dist.append(b["dist"]); dr.append(b["dir"]); pl.append(b["pl"]); pg.append(b["pg"])
+    return {"cone_rec": np.array(recs, np.float32), "cone_O": np.array(O, np.float32),
+            "cone_D": np.array(D, np.float32), "cone_shape": np.array(shape, np.int32),
+            "cone_dist": np.array(dist, np.float32), "cone_dir": np.array(dr, np.int32),
+            "cone_pl": np.array(pl, np.float32), "cone_pg": np.array(pg, np.float32)}
+
+
+def make_sampler_kat(rng, k=24):
+    """DrawSampling point clouds: tp/sampling_base.vert:23-26 seeding, tp/hsphere.vert main."""
+    nrm, seeds, rough, nbu, out = [], [], [], [], []
+    for case in range(6):
+        n = rng.normal(size=3).astype(np.float32)
+        fs = rng.uniform(0, 1, 3).astype(np.float32)
+        r = np.float32([1.0, 0.5, 0.9, 0.0, 1.0, 0.25][case])
+        nb = [3, 3, 2, 3, 5, 3][case]
+        D = normalize([f32(v) for v in n])
+        pts = []
+        for v in range(k):
+            step = (v * nb) & 0xFFFFFFFF
+            base = [int(x) for x in fs.view(np.uint32)]
+            seed = [(base[0] + step * 11) & 0xFFFFFFFF, (base[1] + step * 43) & 0xFFFFFFFF,
+                    (base[2] + step * 67) & 0xFFFFFFFF]
+            pts.append(random_ray(seed, D, r))
+        nrm.append(n); seeds.append(fs); rough.append(r); nbu.append(nb); out.append(pts)
+    return {"smp_normal": np.array(nrm, np.float32), "smp_fseed": np.array(seeds, np.float32),
+            "smp_rough": np.array(rough, np.float32), "smp_nb": np.array(nbu, np.int32),
+            "smp_out": np.array(out, np.float32)}
+
+
 IMAGES = [  # (scene, variant, W, H, first_pass, spp, bounces, ior, light)
     (1, 0, 32, 24, 1, 4, 3, 1.0, 1.2), (2, 0, 32, 24, 1, 2, 8, 1.0, 1.2), (3, 0, 32, 24, 1, 2, 8, 1.0, 1.2),
     (4, 0, 32, 24, 1, 2, 8, 1.0, 1.2), (5, 0, 32, 24, 1, 2, 8, 1.0, 1.2), (6, 0, 32, 24, 1, 4, 8, 1.0, 1.2),
@@ -397,6 +485,9 @@ def main():
     prims = [orc.scene(s)[0] for s in (1, 2, 3, 6, 8)]
     prims = [p[: 24] for p in prims]
     kat.update(make_prim_kat(rng, prims))
+    rng2 = np.random.default_rng(20241009)          # round-1 additions: cone + sampler
+    kat.update(make_cone_kat(rng2))
+    kat.update(make_sampler_kat(rng2))
     np.savez_compressed(os.path.join(HERE, "kat.npz"), **kat)
     for c in IMAGES:
         s, v, W, H, p, n, B, ior, li = c

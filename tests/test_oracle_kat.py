@@ -90,3 +90,51 @@ def test_golden_images(oracle_mod):
         acc, _ = oracle_mod.render(pr, nodes, leaves, d, ipv, iv, W, H, p, n, 0.0, B, ior, v)
         want = np.load(os.path.join(GOLD, g.image_name(c)))
         assert np.array_equal(bits(acc), bits(want)), c
+
+
+def test_cone_intersect(oracle_mod, kat):
+    """Cone_intersect (raytracer_func.frag:579-640) vs the numpy restatement; cones accept
+    backward roots (no a > EPSILON check on the lateral surface), kept."""
+    n = len(kat["cone_rec"])
+    hits = 0
+    for i in range(n):
+        shape, dist, dr, pl, pg = oracle_mod.intersect_prim(kat["cone_rec"][i], kat["cone_O"][i], kat["cone_D"][i])
+        assert shape == kat["cone_shape"][i], i
+        assert bits(dist) == bits(kat["cone_dist"][i]), i
+        if shape >= 0:
+            hits += 1
+            assert dr == kat["cone_dir"][i], i
+            assert np.array_equal(bits(pl), bits(kat["cone_pl"][i])), i
+            assert np.array_equal(bits(pg), bits(kat["cone_pg"][i])), i
+    assert hits > n // 4
+
+
+def test_sampler_point_cloud(oracle_mod, kat):
+    """DrawSampling seeding (tp/sampling_base.vert:23-26) + random_ray, bit-exact."""
+    for nrm, fs, r, nb, want in zip(kat["smp_normal"], kat["smp_fseed"], kat["smp_rough"], kat["smp_nb"],
+                                    kat["smp_out"]):
+        got = oracle_mod.sample_hemisphere(nrm, fs, len(want), float(r), int(nb))
+        assert np.array_equal(bits(got), bits(want))
+        n = nrm / np.linalg.norm(nrm)
+        if r > 0:
+            assert (got @ n > 0).all()            # the lobe stays in the upper hemisphere
+
+
+def test_any_hit_queries(oracle_mod):
+    """just_hit_bvh finds a hit exactly when traverse_all_bvh does, never closer; one-prim
+    queries agree with the closest hit on that primitive."""
+    rng = np.random.default_rng(5)
+    for sid in (1, 6, 8):
+        prims, nodes, leaves, d, _ = oracle_mod.scene(sid)
+        o = rng.uniform(-250, 250, (400, 3)).astype(np.float32)
+        dd = rng.normal(size=(400, 3)).astype(np.float32)
+        ci, cf = oracle_mod.trace(prims, nodes, leaves, d, o, dd)
+        ai, af = oracle_mod.trace(prims, nodes, leaves, d, o, dd, any_hit=True)
+        assert np.array_equal(ci[:, 0] >= 0, ai[:, 0] >= 0)
+        hit = ci[:, 0] >= 0
+        assert (af[hit, 0] >= cf[hit, 0]).all()
+        assert hit.sum() > 20
+        k = int(ci[hit][0, 1])
+        pi, pf = oracle_mod.trace(prims, nodes, leaves, d, o, dd, prim=k)
+        same = hit & (ci[:, 1] == k)
+        assert np.array_equal(bits(pf[same]), bits(cf[same]))
