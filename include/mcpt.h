@@ -53,7 +53,7 @@ enum mcpt_traversal {
 /* algorithmic-byte event counters, index order */
 enum mcpt_event {
   MCPT_EV_NODE = 0, MCPT_EV_LEAF, MCPT_EV_PRIM, MCPT_EV_CAND, MCPT_EV_GEOM, MCPT_EV_COLMAT,
-  MCPT_EV_SAMPLE, MCPT_EV_TRAV, MCPT_EV_COUNT
+  MCPT_EV_SAMPLE, MCPT_EV_TRAV, MCPT_EV_MESH, MCPT_EV_TRI, MCPT_EV_MGEOM, MCPT_EV_COUNT
 };
 
 typedef struct mcpt_ctx mcpt_ctx;
@@ -79,6 +79,18 @@ int mcpt_destroy(mcpt_ctx* ctx);
  * (row 3 = 0,0,0,1: the shader only uses .xyz).  Synchronous. */
 int mcpt_upload_scene(mcpt_ctx* ctx, const float* prims, int n_prims, const float* nodes,
                       const int* leaves, int depth, int nb_emissives);
+
+/* Upload the scene's meshes (replaces the tex_tri_/tex_p_/tex_n_ textures and the per-mesh
+ * BVH rows of tex_bb_/tex_ind_, gpu_bvh_scene.cpp:87-118, 160-186).  Layouts: see
+ * mcpt_scene_get_mesh_buffers.  n_meshes = 0 removes them.  Call after mcpt_upload_scene;
+ * a CODE_MESH primitive's record holds its mesh id (texel 12 .y, "mesh_line"). */
+int mcpt_upload_meshes(mcpt_ctx* ctx, int n_meshes, const int* info, int n_nodes, const float* nodes, int n_leaves,
+                       const int* leaves, int n_tris, const int* tris, int n_verts, const float* verts,
+                       const float* normals);
+
+/* uniform flat_face (raytracer_func.frag:26, location 3): flat triangle normals instead of
+ * the area-weighted vertex normals.  The reference never sets it (false); default 0. */
+int mcpt_set_flat_face(mcpt_ctx* ctx, int flat_face);
 
 /* Set the framebuffer (replaces FBO RGB32F + resize_ogl, montecarlo.cpp:384-386, 616-626).
  * Row-band sharding for multi-GPU: this context renders global rows y whose band
@@ -177,6 +189,22 @@ int mcpt_scene_add_cube(mcpt_scene* s, const float* trf16, const float* material
 int mcpt_scene_add_cylinder(mcpt_scene* s, const float* trf16, const float* material7); /* scene.h:144-152 */
 int mcpt_scene_add_cone(mcpt_scene* s, const float* trf16, const float* material7);     /* scene.h:154-163 */
 int mcpt_scene_add_oriented_quad(mcpt_scene* s, const float* trf16, const float* material7); /* scene.h:166-172 */
+/* Triangle meshes (BVH_GPU_Scene::add_mesh / place_mesh, gpu_bvh_scene.cpp:51-74,
+ * gpu_bvh_scene.h:89-92; ScenePrimitives::add_mesh scene.cpp:56-67).  add_mesh stores a mesh
+ * (n_vertices × 3 positions and normals, n_triangles × 3 vertex indices) and builds its own
+ * median-split BVH over the triangles (SceneMesh::prim_bb); bb6 = the Mesh::BB() box
+ * (min.xyz, max.xyz), NULL = the vertices' bounding box.  place_mesh adds an instance (a
+ * CODE_MESH primitive) with transform trf and a material, like the reference. */
+int mcpt_scene_add_mesh(mcpt_scene* s, const float* vertices, const float* normals, int n_vertices,
+                        const unsigned* tri_indices, int n_triangles, const float* bb6, int* mesh_id);
+int mcpt_scene_place_mesh(mcpt_scene* s, int mesh_id, const float* trf16, const float* material7);
+/* sizes and flat buffers of all meshes, in the layouts mcpt_upload_meshes takes:
+ *   info   : n_meshes × 4 i32 (first node, first leaf, BVH depth, first triangle)
+ *   nodes  : n_nodes × 6 f32 (bbmin, bbmax; mesh space)   leaves : n_leaves i32 (triangle or -1)
+ *   tris   : n_tris × 3 i32 global vertex ids             verts, normals : n_verts × 3 f32 */
+int mcpt_scene_mesh_sizes(mcpt_scene* s, int* n_meshes, int* n_nodes, int* n_leaves, int* n_tris, int* n_verts);
+int mcpt_scene_get_mesh_buffers(mcpt_scene* s, int* info, float* nodes, int* leaves, int* tris, float* verts,
+                                float* normals);
 /* sortEmissiveFirst + BVH_KDtree::compute (scene.cpp:70-88, bvh.cpp:34-93) */
 int mcpt_scene_finalize(mcpt_scene* s);
 int mcpt_scene_nb_prim(mcpt_scene* s, int* n);

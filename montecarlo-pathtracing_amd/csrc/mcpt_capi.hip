@@ -43,6 +43,15 @@ struct mcpt_ctx {
   float4* d_prims = nullptr;
   int n_prims = 0, depth = 0, nb_emissive = 0;
   bool has_scene = false;
+  // triangle meshes
+  int4* d_minfo = nullptr;
+  float4* d_mnodes = nullptr;
+  int* d_mleaves = nullptr;
+  int4* d_mtris = nullptr;
+  float4* d_mverts = nullptr;
+  float4* d_mnorms = nullptr;
+  int n_meshes = 0, flat_face = 0;
+  std::vector<int> mesh_ids;     // per primitive: mesh id of a CODE_MESH record, else -1
   // framebuffer
   float* d_accum = nullptr;
   size_t accum_bytes = 0;
@@ -100,6 +109,14 @@ int mcpt_create(int device_ordinal, mcpt_ctx** out) {
   return MCPT_OK;
 }
 
+static void free_meshes(mcpt_ctx* c) {
+  (void)hipFree(c->d_minfo); (void)hipFree(c->d_mnodes); (void)hipFree(c->d_mleaves);
+  (void)hipFree(c->d_mtris); (void)hipFree(c->d_mverts); (void)hipFree(c->d_mnorms);
+  c->d_minfo = nullptr; c->d_mnodes = nullptr; c->d_mleaves = nullptr;
+  c->d_mtris = nullptr; c->d_mverts = nullptr; c->d_mnorms = nullptr;
+  c->n_meshes = 0;
+}
+
 static void free_scene(mcpt_ctx* c) {
   (void)hipFree(c->d_nodes); (void)hipFree(c->d_leaves); (void)hipFree(c->d_ptype); (void)hipFree(c->d_prims);
   c->d_nodes = nullptr; c->d_leaves = nullptr; c->d_ptype = nullptr; c->d_prims = nullptr;
@@ -111,6 +128,7 @@ int mcpt_destroy(mcpt_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   free_scene(c);
+  free_meshes(c);
   (void)hipFree(c->d_accum);
   (void)hipFree(c->d_events);
   (void)hipFree(c->d_partial);
@@ -145,19 +163,32 @@ int mcpt_upload_scene(mcpt_ctx* c, const float* prims, int n_prims, const float*
     hn[(size_t)i * 3 + 1] = make_float4(wx, wy, wz, 0.0f);
     hn[(size_t)i * 3 + 2] = make_float4(1.0f / wx, 1.0f / wy, 1.0f / wz, 0.0f);
   }
-  // prims → rows of the inverse and of the transform (the shader uses .xyz of mat4·v)
-  std::vector<int> ht(n_prims);
+  // prims → rows of the inverse and of the transform (the shader uses .xyz of mat4·v).  A
+  // CODE_MESH record's transform rows are its mesh transform (texel 8-11, read_mesh_transfo:
+  // the only transform Mesh_intersect / mesh_inter_geom_info use); its mesh id (texel 12 .y,
+  // "mesh_line") goes into ptype's high bits.
+  std::vector<int> ht(n_prims), mesh_ids(n_prims, -1);
   std::vector<float4> hp((size_t)n_prims * mcpt::kPrimF4);
   for (int i = 0; i < n_prims; ++i) {
     const float* r = prims + (size_t)i * 64;
     float tcode = r[48];
-    if (!(tcode >= 0.0f && tcode <= 5.0f)) return set_err(MCPT_ERR_BAD_SCENE, "primitive type code not in 0..5");
+    if (!(tcode >= 0.0f && tcode <= 5.0f) || tcode != (float)(int)tcode)
+      return set_err(MCPT_ERR_BAD_SCENE, "primitive type code not in 0..5");
     ht[i] = (int)tcode;
+    const float* trf = r;
+    if (ht[i] == 0) {
+      const float ml = r[49];
+      if (!(ml >= 0.0f && ml < (float)(1 << 26)) || ml != (float)(int)ml)
+        return set_err(MCPT_ERR_BAD_SCENE, "mesh primitive without a valid mesh id");
+      mesh_ids[i] = (int)ml;
+      ht[i] |= mesh_ids[i] << 4;
+      trf = r + 32;
+    }
     float4* o = &hp[(size_t)i * mcpt::kPrimF4];
     for (int row = 0; row < 3; ++row) {
       const float* inv = r + 16;
       o[row] = make_float4(inv[row], inv[4 + row], inv[8 + row], inv[12 + row]);
-      o[3 + row] = make_float4(r[row], r[4 + row], r[8 + row], r[12 + row]);
+      o[3 + row] = make_float4(trf[row], trf[4 + row], trf[8 + row], trf[12 + row]);
     }
     o[6] = make_float4(r[52], r[53], r[54], r[55]);
     o[7] = make_float4(r[56], r[57], r[58], r[59]);
@@ -174,7 +205,92 @@ int mcpt_upload_scene(mcpt_ctx* c, const float* prims, int n_prims, const float*
   HIP_OR_RETURN(hipMemcpy(c->d_ptype, ht.data(), (size_t)n_prims * sizeof(int), hipMemcpyHostToDevice));
   HIP_OR_RETURN(hipMemcpy(c->d_prims, hp.data(), hp.size() * sizeof(float4), hipMemcpyHostToDevice));
   c->n_prims = n_prims; c->depth = depth; c->nb_emissive = nb_emissives;
+  c->mesh_ids = mesh_ids;
+  free_meshes(c);                 // a new scene drops the previous meshes (upload them again)
   c->has_scene = true;
+  return MCPT_OK;
+}
+
+// nodes (bbmin, bbmax) → device node records with the subtree-holds-an-item flag
+static void pack_nodes(const float* nodes, const int* leaves, int depth, float4* out) {
+  const int n_leaf = 1 << depth, n_node = 2 * n_leaf - 1;
+  std::vector<char> has(n_node, 0);
+  for (int i = n_node - 1; i >= 0; --i)
+    has[i] = (i >= n_leaf - 1) ? (leaves[i - (n_leaf - 1)] >= 0) : (has[2 * i + 1] || has[2 * i + 2]);
+  for (int i = 0; i < n_node; ++i) {
+    const float* b = nodes + (size_t)i * 6;
+    float cx = (b[0] + b[3]) / 2.0f, cy = (b[1] + b[4]) / 2.0f, cz = (b[2] + b[5]) / 2.0f;
+    float wx = 0.5f * (b[3] - b[0]), wy = 0.5f * (b[4] - b[1]), wz = 0.5f * (b[5] - b[2]);
+    out[(size_t)i * 3 + 0] = make_float4(cx, cy, cz, has[i] ? 1.0f : 0.0f);
+    out[(size_t)i * 3 + 1] = make_float4(wx, wy, wz, 0.0f);
+    out[(size_t)i * 3 + 2] = make_float4(1.0f / wx, 1.0f / wy, 1.0f / wz, 0.0f);
+  }
+}
+
+int mcpt_upload_meshes(mcpt_ctx* c, int n_meshes, const int* info, int n_nodes, const float* nodes, int n_leaves,
+                       const int* leaves, int n_tris, const int* tris, int n_verts, const float* verts,
+                       const float* normals) {
+  if (!c || n_meshes < 0) return set_err(MCPT_ERR_INVALID_ARG, "mcpt_upload_meshes: bad arguments");
+  if (!c->has_scene) return set_err(MCPT_ERR_NO_SCENE, "upload the scene before its meshes");
+  HIP_OR_RETURN(hipSetDevice(c->device));
+  HIP_OR_RETURN(hipStreamSynchronize(c->stream));
+  free_meshes(c);
+  if (n_meshes == 0) {
+    for (int id : c->mesh_ids)
+      if (id >= 0) return set_err(MCPT_ERR_BAD_SCENE, "the scene has mesh instances but no meshes were uploaded");
+    return MCPT_OK;
+  }
+  if (!info || !nodes || !leaves || !tris || !verts || !normals || n_nodes <= 0 || n_leaves <= 0 || n_tris <= 0 ||
+      n_verts <= 0)
+    return set_err(MCPT_ERR_INVALID_ARG, "mcpt_upload_meshes: bad arguments");
+  // validate the layout: each mesh's BVH within the node / leaf arrays, leaf triangle ids
+  // within the mesh's triangles, vertex ids within the vertex array
+  std::vector<float4> hn((size_t)n_nodes * 3);
+  for (int m = 0; m < n_meshes; ++m) {
+    const int no = info[4 * m], lo = info[4 * m + 1], d = info[4 * m + 2], to = info[4 * m + 3];
+    if (d < 0 || d > 24 || no < 0 || lo < 0 || to < 0) return set_err(MCPT_ERR_BAD_SCENE, "bad mesh info");
+    const int nl = 1 << d, nn = 2 * nl - 1;
+    if (no + nn > n_nodes || lo + nl > n_leaves) return set_err(MCPT_ERR_BAD_SCENE, "mesh BVH out of range");
+    const int nt = (m + 1 < n_meshes ? info[4 * (m + 1) + 3] : n_tris) - to;
+    if (nt <= 0 || to + nt > n_tris) return set_err(MCPT_ERR_BAD_SCENE, "mesh triangles out of range");
+    for (int k = 0; k < nl; ++k)
+      if (leaves[lo + k] < -1 || leaves[lo + k] >= nt) return set_err(MCPT_ERR_BAD_SCENE, "mesh leaf id out of range");
+    pack_nodes(nodes + (size_t)no * 6, leaves + lo, d, &hn[(size_t)no * 3]);
+  }
+  for (int id : c->mesh_ids)
+    if (id >= n_meshes) return set_err(MCPT_ERR_BAD_SCENE, "mesh instance refers to a missing mesh");
+  std::vector<int4> hi(n_meshes), ht(n_tris);
+  for (int m = 0; m < n_meshes; ++m) hi[m] = make_int4(info[4 * m], info[4 * m + 1], info[4 * m + 2], info[4 * m + 3]);
+  for (int t = 0; t < n_tris; ++t) {
+    const int* v = tris + (size_t)t * 3;
+    for (int k = 0; k < 3; ++k)
+      if (v[k] < 0 || v[k] >= n_verts) return set_err(MCPT_ERR_BAD_SCENE, "vertex id out of range");
+    ht[t] = make_int4(v[0], v[1], v[2], 0);
+  }
+  std::vector<float4> hv(n_verts), hm(n_verts);
+  for (int i = 0; i < n_verts; ++i) {
+    hv[i] = make_float4(verts[3 * i], verts[3 * i + 1], verts[3 * i + 2], 0.0f);
+    hm[i] = make_float4(normals[3 * i], normals[3 * i + 1], normals[3 * i + 2], 0.0f);
+  }
+  HIP_OR_RETURN(hipMalloc(&c->d_minfo, hi.size() * sizeof(int4)));
+  HIP_OR_RETURN(hipMalloc(&c->d_mnodes, hn.size() * sizeof(float4)));
+  HIP_OR_RETURN(hipMalloc(&c->d_mleaves, (size_t)n_leaves * sizeof(int)));
+  HIP_OR_RETURN(hipMalloc(&c->d_mtris, ht.size() * sizeof(int4)));
+  HIP_OR_RETURN(hipMalloc(&c->d_mverts, hv.size() * sizeof(float4)));
+  HIP_OR_RETURN(hipMalloc(&c->d_mnorms, hm.size() * sizeof(float4)));
+  HIP_OR_RETURN(hipMemcpy(c->d_minfo, hi.data(), hi.size() * sizeof(int4), hipMemcpyHostToDevice));
+  HIP_OR_RETURN(hipMemcpy(c->d_mnodes, hn.data(), hn.size() * sizeof(float4), hipMemcpyHostToDevice));
+  HIP_OR_RETURN(hipMemcpy(c->d_mleaves, leaves, (size_t)n_leaves * sizeof(int), hipMemcpyHostToDevice));
+  HIP_OR_RETURN(hipMemcpy(c->d_mtris, ht.data(), ht.size() * sizeof(int4), hipMemcpyHostToDevice));
+  HIP_OR_RETURN(hipMemcpy(c->d_mverts, hv.data(), hv.size() * sizeof(float4), hipMemcpyHostToDevice));
+  HIP_OR_RETURN(hipMemcpy(c->d_mnorms, hm.data(), hm.size() * sizeof(float4), hipMemcpyHostToDevice));
+  c->n_meshes = n_meshes;
+  return MCPT_OK;
+}
+
+int mcpt_set_flat_face(mcpt_ctx* c, int flat_face) {
+  if (!c) return MCPT_ERR_INVALID_ARG;
+  c->flat_face = flat_face ? 1 : 0;
   return MCPT_OK;
 }
 
@@ -248,6 +364,9 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
     return set_err(MCPT_ERR_INVALID_ARG, "mcpt_render: bad arguments");
   if (!c->has_scene) return set_err(MCPT_ERR_NO_SCENE, "no scene uploaded");
   if (!c->has_target) return set_err(MCPT_ERR_NO_TARGET, "no render target");
+  if (c->n_meshes == 0)
+    for (int id : c->mesh_ids)
+      if (id >= 0) return set_err(MCPT_ERR_BAD_SCENE, "mesh instances present: call mcpt_upload_meshes");
   HIP_OR_RETURN(hipSetDevice(c->device));
   mcpt::RenderParams p;
   std::memset(&p, 0, sizeof(p));
@@ -256,6 +375,8 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   corner_rays(invPV, invV, p);
   p.W = c->W; p.H = c->H; p.band_rows = c->band_rows; p.world = c->world; p.rank = c->rank;
   p.n_local_rows = c->n_local_rows; p.depth = c->depth;
+  p.minfo = c->d_minfo; p.mnodes = c->d_mnodes; p.mleaves = c->d_mleaves; p.mtris = c->d_mtris;
+  p.mverts = c->d_mverts; p.mnorms = c->d_mnorms; p.n_meshes = c->n_meshes; p.flat_face = c->flat_face;
   p.wave_traversal = (resolve_traversal(c) == MCPT_TRAVERSAL_WAVE) ? 1 : 0;
   p.first_pass = first_pass; p.n_passes = n_passes; p.bounces = bounces; p.variant = variant;
   p.date = date; p.ior = refract_ind;
@@ -356,6 +477,9 @@ int mcpt_trace(mcpt_ctx* c, const float* origins, const float* dirs, int n, int 
   if (!c || n < 0 || (n > 0 && (!origins || !dirs || !out))) return set_err(MCPT_ERR_INVALID_ARG, "mcpt_trace: bad arguments");
   if (!c->has_scene) return set_err(MCPT_ERR_NO_SCENE, "no scene uploaded");
   if (prim >= c->n_prims) return set_err(MCPT_ERR_INVALID_ARG, "mcpt_trace: primitive index out of range");
+  if (c->n_meshes == 0)
+    for (int id : c->mesh_ids)
+      if (id >= 0) return set_err(MCPT_ERR_BAD_SCENE, "mesh instances present: call mcpt_upload_meshes");
   if (n == 0) return MCPT_OK;
   HIP_OR_RETURN(hipSetDevice(c->device));
   const size_t n3 = (size_t)n * 3 * sizeof(float), ni = (size_t)n * 3 * sizeof(int);
@@ -365,6 +489,8 @@ int mcpt_trace(mcpt_ctx* c, const float* origins, const float* dirs, int n, int 
   mcpt::TraceParams q;
   q.nodes = c->d_nodes; q.leaves = c->d_leaves; q.ptype = c->d_ptype; q.prims = c->d_prims; q.depth = c->depth;
   q.prim = prim < 0 ? -1 : prim;
+  q.minfo = c->d_minfo; q.mnodes = c->d_mnodes; q.mleaves = c->d_mleaves; q.mtris = c->d_mtris;
+  q.mverts = c->d_mverts; q.mnorms = c->d_mnorms; q.n_meshes = c->n_meshes; q.flat_face = c->flat_face;
   q.orig = (const float*)buf; q.dir = (const float*)(buf + n3);
   q.out_i = (int*)(buf + 2 * n3); q.out = (float*)(buf + 2 * n3 + ni); q.n = n;
   std::vector<int> hi((size_t)n * 3);

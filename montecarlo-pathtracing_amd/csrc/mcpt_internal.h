@@ -6,7 +6,8 @@
 namespace mcpt {
 
 // algorithmic-byte events; same order as the oracle's counters
-enum { EV_NODE = 0, EV_LEAF, EV_PRIM, EV_CAND, EV_GEOM, EV_COLMAT, EV_SAMPLE, EV_TRAV, EV_COUNT };
+enum { EV_NODE = 0, EV_LEAF, EV_PRIM, EV_CAND, EV_GEOM, EV_COLMAT, EV_SAMPLE, EV_TRAV, EV_MESH, EV_TRI, EV_MGEOM,
+       EV_COUNT };
 
 // bytes per event in the reference's texel model
 constexpr int kEventBytes[EV_COUNT] = {
@@ -18,6 +19,9 @@ constexpr int kEventBytes[EV_COUNT] = {
     32,   // colour + material texels                               (:899-907)
     24,   // accumulate: RGB32F read + write (blend)                (montecarlo.cpp:450-452)
     0,    // traversal count (no bytes of its own)
+    12 + 64 + 64,  // mesh instance entry: mesh info + mesh transform + transform   (:652-656)
+    12 + 36,       // triangle test: index triplet + 3 positions (RGB32I/RGB32F)   (:145-153)
+    12 + 72 + 64,  // mesh hit info: triplet + 3 × (position, normal) + mesh transform (:156-169, :792)
 };
 
 // device record layout (built by mcpt_upload_scene from the reference texture layout)
@@ -50,6 +54,14 @@ struct RenderParams {
   long long n_local_px;         // n_local_rows × W
   int n_tiles, n_segments;      // 16x16 tiles of the local rows; pass segments of this launch
   int depth;
+  // triangle meshes (mcpt_upload_meshes); n_meshes == 0: none
+  const int4* minfo;
+  const float4* mnodes;
+  const int* mleaves;
+  const int4* mtris;
+  const float4* mverts;
+  const float4* mnorms;
+  int n_meshes, flat_face;
   int wave_traversal;           // 1: wave-coherent BVH walk (traverse_wave), 0: per lane
   int first_pass, n_passes, bounces, variant;
   float date, ior;
@@ -64,6 +76,14 @@ struct TraceParams {
   const int* ptype;
   const float4* prims;
   int depth;
+  // triangle meshes (mcpt_upload_meshes); n_meshes == 0: none
+  const int4* minfo;
+  const float4* mnodes;
+  const int* mleaves;
+  const int4* mtris;
+  const float4* mverts;
+  const float4* mnorms;
+  int n_meshes, flat_face;
   int prim;                     // -1: whole BVH, >= 0: this primitive only
   const float* orig;            // n × 3
   const float* dir;             // n × 3

@@ -58,12 +58,24 @@ enum { CODE_MESH = 0, CODE_SPHERE = 1, CODE_CUBE = 2, CODE_CYLINDER = 3, CODE_CO
 // ------------------------------------------------------------------------------------
 // scene views: global memory or LDS-staged copy (same record layout)
 // ------------------------------------------------------------------------------------
-struct SceneRef {
+// MESH: the scene has triangle-mesh instances (CODE_MESH); a compile-time switch so scenes
+// without meshes do not pay the mesh code's registers.
+template <bool MESH>
+struct SceneT {
+  static constexpr bool kMesh = MESH;
   const float4* __restrict__ nodes;   // 3 per node: (c, has-prim) (w, 0) (1/w, 0)
   const int* __restrict__ leaves;
-  const int* __restrict__ ptype;
+  const int* __restrict__ ptype;      // type code | mesh id << 4
   const float4* __restrict__ prims;   // 8 per prim: inv r0..r2, trf r0..r2, colour, material
   int depth;
+  // meshes (mcpt_upload_meshes): per mesh (first node, first leaf, depth, first triangle)
+  const int4* __restrict__ minfo;
+  const float4* __restrict__ mnodes;  // 3 per node, mesh space
+  const int* __restrict__ mleaves;    // mesh-local triangle ids or -1
+  const int4* __restrict__ mtris;     // global vertex ids (a, b, c, 0)
+  const float4* __restrict__ mverts;  // (x, y, z, 0)
+  const float4* __restrict__ mnorms;
+  int flat_face;                      // uniform flat_face (raytracer_func.frag:26; never set: 0)
 };
 
 // Wave-uniform records are read through the constant address space so the compiler emits
@@ -141,8 +153,43 @@ __device__ __forceinline__ bool box_test(float4 a0, float4 a1, float4 a2, f3 O, 
   return false;
 }
 
-template <bool COUNT, bool UNI>
-__device__ __forceinline__ void accept_cand(const SceneRef& s, int index, int shape, int dir, f3 Pl, f3 Ol,
+// intersect_bvm raytracer_func.frag:273-311: the mesh BVH's box test, in mesh space (O, D),
+// with the entry point taken to world space through the mesh transform (rows t0..t2) and
+// compared with the world distance from Ol.  Same face loop as box_test.
+__device__ __forceinline__ bool box_test_mesh(float4 a0, float4 a1, float4 a2, f3 O, f3 D, f3 invD, f3 Ol,
+                                              float4 t0, float4 t1, float4 t2, double cull2) {
+  f3 c = mk(a0.x, a0.y, a0.z), w = mk(a1.x, a1.y, a1.z), iw = mk(a2.x, a2.y, a2.z);
+  f3 Oi = mulv(sub(O, c), iw);
+  f3 Di = mulv(D, iw);
+  if (__builtin_fabsf(Oi.x) < 1.0f && __builtin_fabsf(Oi.y) < 1.0f && __builtin_fabsf(Oi.z) < 1.0f) return true;
+  f3 rD = mulv(invD, w);
+  const bool dx = __builtin_fabsf(Di.x) > kEPS, dy = __builtin_fabsf(Di.y) > kEPS, dz = __builtin_fabsf(Di.z) > kEPS;
+  float al = kFLTMAX;
+#define MCPT_FACE(CD, OA, DV, RA, OB, DB, OC, DC)                                              \
+  {                                                                                            \
+    const float a = ((CD) - (OA)) * (RA);                                                      \
+    const bool ok = (DV) & (a > kEPS) & (__builtin_fabsf(OB + a * DB) <= 1.0f) &               \
+                    (__builtin_fabsf(OC + a * DC) <= 1.0f);                                    \
+    al = __builtin_fminf(al, ok ? a : kFLTMAX);                                                \
+  }
+  MCPT_FACE(-1.0f, Oi.x, dx, rD.x, Oi.y, Di.y, Oi.z, Di.z)
+  MCPT_FACE(1.0f, Oi.x, dx, rD.x, Oi.y, Di.y, Oi.z, Di.z)
+  MCPT_FACE(-1.0f, Oi.y, dy, rD.y, Oi.z, Di.z, Oi.x, Di.x)
+  MCPT_FACE(1.0f, Oi.y, dy, rD.y, Oi.z, Di.z, Oi.x, Di.x)
+  MCPT_FACE(-1.0f, Oi.z, dz, rD.z, Oi.x, Di.x, Oi.y, Di.y)
+  MCPT_FACE(1.0f, Oi.z, dz, rD.z, Oi.x, Di.x, Oi.y, Di.y)
+#undef MCPT_FACE
+  if (al < kFLTMAX) {
+    f3 Pl = add(Oi, muls(Di, al));
+    f3 Pg = xpoint(t0, t1, t2, add(mulv(Pl, w), c));
+    f3 v = sub(Ol, Pg);
+    return (double)dot3(v, v) < cull2;
+  }
+  return false;
+}
+
+template <bool COUNT, bool UNI, class SR>
+__device__ __forceinline__ void accept_cand(const SR& s, int index, int shape, int dir, f3 Pl, f3 Ol,
                                             Hit& h, Ev<COUNT>& ev) {
   ev.inc(EV_CAND);
   const size_t b = (size_t)index * 8;
@@ -154,12 +201,94 @@ __device__ __forceinline__ void accept_cand(const SceneRef& s, int index, int sh
   }
 }
 
+// Triangle_intersect raytracer_func.frag:354-396 (Möller–Trumbore, mesh space); a hit keeps
+// the mesh-local triangle index in Hit::dir (the reference's tri_index; its dir is 0)
+template <bool COUNT, class SR>
+__device__ __forceinline__ void tri_test(const SR& s, int tri_base, int t, int index, f3 O, f3 D, f3 Ol,
+                                         float4 t0, float4 t1, float4 t2, Hit& h, Ev<COUNT>& ev) {
+  ev.inc(EV_TRI);
+  const int4 vi = s.mtris[tri_base + t];
+  const float4 a4 = s.mverts[vi.x], b4 = s.mverts[vi.y], c4 = s.mverts[vi.z];
+  const f3 vA = mk(a4.x, a4.y, a4.z), vB = mk(b4.x, b4.y, b4.z), vC = mk(c4.x, c4.y, c4.z);
+  const f3 edge1 = sub(vB, vA), edge2 = sub(vC, vA);
+  const f3 hv = cross3(D, edge2);
+  const float det = dot3(edge1, hv);
+  if (__builtin_fabsf(det) < kEPS) return;
+  const float invdet = 1.0f / det;
+  const f3 sv = sub(O, vA);
+  const float u = dot3(sv, hv) * invdet;
+  if (u < 0.0f || u > 1.0f) return;
+  const f3 q = cross3(sv, edge1);
+  const float v = dot3(D, q) * invdet;
+  if (v < 0.0f || (u + v) > 1.0f) return;
+  const float a = dot3(edge2, q) * invdet;
+  if (a > kEPS) {
+    const f3 Pl = add(O, muls(D, a));
+    const f3 Pg = xpoint(t0, t1, t2, Pl);
+    const float dist = length3(sub(Ol, Pg));
+    if (dist < h.dist) {
+      h.dist = dist; h.pl = Pl; h.pg = Pg; h.index = index; h.shape = CODE_MESH; h.dir = t;
+      h.cull2 = cull_bound_sq(dist);
+    }
+  }
+}
+
+// Mesh_intersect raytracer_func.frag:642-678: the instance's own BVH, same DFS as
+// intersect_bvh (right child first, cull at push with intersect_bvm), stackless per lane
+template <bool COUNT, bool ANY, class SR>
+__device__ __forceinline__ void mesh_test(const SR& s, int mesh, int index, f3 O, f3 D, f3 Ol, Hit& h,
+                                          Ev<COUNT>& ev) {
+  ev.inc(EV_MESH);
+  const int4 mi = s.minfo[mesh];   // first node, first leaf, depth, first triangle
+  const size_t b = (size_t)index * 8;
+  const float4 t0 = s.prims[b + 3], t1 = s.prims[b + 4], t2 = s.prims[b + 5];   // read_mesh_transfo
+  const float4* nodes = s.mnodes + (size_t)mi.x * 3;
+  const f3 invD = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);
+  const int leaf0 = (1 << mi.z) - 1;
+  int node = 0, level = 0;
+  uint32_t pending = 0;
+  for (;;) {
+    bool pop = true;
+    if (node >= leaf0) {
+      ev.inc(EV_LEAF);
+      const int t = s.mleaves[mi.y + node - leaf0];
+      if (t >= 0) {
+        tri_test<COUNT>(s, mi.w, t, index, O, D, Ol, t0, t1, t2, h, ev);
+        if (ANY && h.shape >= 0) return;   // hit_only (:664-665)
+      }
+    } else {
+      ev.inc(EV_NODE);
+      const size_t j = 2 * (size_t)node + 1;
+      const float4 l0 = nodes[j * 3], r0 = nodes[j * 3 + 3];
+      bool hl = (COUNT || l0.w != 0.0f) &&
+                box_test_mesh(l0, nodes[j * 3 + 1], nodes[j * 3 + 2], O, D, invD, Ol, t0, t1, t2, h.cull2);
+      bool hr = (COUNT || r0.w != 0.0f) &&
+                box_test_mesh(r0, nodes[j * 3 + 4], nodes[j * 3 + 5], O, D, invD, Ol, t0, t1, t2, h.cull2);
+      pop = !(hl || hr);
+      if (hr) {
+        if (hl) pending |= 1u << (level + 1);
+        node = (int)j + 1; level++;
+      } else if (hl) {
+        node = (int)j; level++;
+      }
+    }
+    if (pop) {
+      if (pending == 0) break;
+      int L = 31 - __builtin_clz(pending);
+      pending &= ~(1u << L);
+      node = ((node + 1) >> (level - L)) - 2;
+      level = L;
+    }
+  }
+}
+
 // intersect_prim raytracer_func.frag:681-705 + Sphere/Cube/Cylinder/Cone/OrientedQuad :398-640
-template <bool COUNT, bool UNI>
-__device__ __forceinline__ void prim_test(const SceneRef& s, int i, f3 Ow, f3 Dw, Hit& h, Ev<COUNT>& ev) {
+template <bool COUNT, bool UNI, bool ANY = false, class SR>
+__device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit& h, Ev<COUNT>& ev) {
   ev.inc(EV_PRIM);
-  int t = ld1<UNI>(s.ptype, i);
-  if (t < 0) return;
+  const int pt = ld1<UNI>(s.ptype, i);
+  if (pt < 0) return;
+  const int t = pt & 15;
   const size_t b = (size_t)i * 8;
   float4 r0 = ld4<UNI>(s.prims, b), r1 = ld4<UNI>(s.prims, b + 1), r2 = ld4<UNI>(s.prims, b + 2);
   f3 O = xpoint(r0, r1, r2, Ow);
@@ -244,8 +373,9 @@ __device__ __forceinline__ void prim_test(const SceneRef& s, int i, f3 Ow, f3 Dw
       if (tt < tl) { cl = 2; tl = tt; }
     }
     if (tl < kFLTMAX) accept_cand<COUNT, UNI>(s, i, CODE_CONE, cl, add(O, muls(D, tl)), Ow, h, ev);
+  } else if (t == CODE_MESH) {
+    if constexpr (SR::kMesh) mesh_test<COUNT, ANY>(s, pt >> 4, i, O, D, Ow, h, ev);
   }
-  // CODE_MESH: no mesh instance in any reference scene: no hit
 }
 
 // intersect_bvh raytracer_func.frag:734-769, per lane, stackless.  pending bit L = "a left
@@ -253,8 +383,8 @@ __device__ __forceinline__ void prim_test(const SceneRef& s, int i, f3 Ow, f3 Dw
 // exactly the reference's LIFO order (right child first, cull decided at push time).
 // ANY: just_hit_bvh (raytracer_func.frag:771-775) — stop at the first leaf whose primitive
 // produced a hit (hit_only, :756-757); the render path always uses traverse_all_bvh.
-template <bool COUNT, bool ANY = false>
-__device__ __forceinline__ void traverse_lane(const SceneRef& s, f3 O, f3 D, Hit& h, Ev<COUNT>& ev) {
+template <bool COUNT, bool ANY = false, class SR>
+__device__ __forceinline__ void traverse_lane(const SR& s, f3 O, f3 D, Hit& h, Ev<COUNT>& ev) {
   ev.inc(EV_TRAV);
   h.index = -1; h.dist = kFLTMAX; h.shape = -1; h.dir = -1; h.cull2 = cull_bound_sq(kFLTMAX);
   const f3 invD = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);
@@ -270,7 +400,7 @@ __device__ __forceinline__ void traverse_lane(const SceneRef& s, f3 O, f3 D, Hit
     if (is_leaf) {
       ev.inc(EV_LEAF);
       int p = s.leaves[node - leaf0];
-      if (p >= 0) prim_test<COUNT, false>(s, p, O, D, h, ev);
+      if (p >= 0) prim_test<COUNT, false, ANY>(s, p, O, D, h, ev);
       if (ANY && h.shape >= 0) break;
     }
 #ifdef MCPT_STAMPS
@@ -307,8 +437,8 @@ __device__ __forceinline__ void traverse_lane(const SceneRef& s, f3 O, f3 D, Hit
 // then one leaf step for every lane on a leaf.  Each lane's own visit sequence is the
 // reference's; only the interleaving across lanes changes.  Diagnostic variant
 // (MCPT_WHILE_WHILE); the default is the if-if loop of traverse_lane.
-template <bool COUNT>
-__device__ __forceinline__ void traverse_lane_ww(const SceneRef& s, f3 O, f3 D, Hit& h, Ev<COUNT>& ev) {
+template <bool COUNT, class SR>
+__device__ __forceinline__ void traverse_lane_ww(const SR& s, f3 O, f3 D, Hit& h, Ev<COUNT>& ev) {
   ev.inc(EV_TRAV);
   h.index = -1; h.dist = kFLTMAX; h.shape = -1; h.dir = -1; h.cull2 = cull_bound_sq(kFLTMAX);
   const f3 invD = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);
@@ -360,8 +490,8 @@ __device__ __forceinline__ void traverse_lane_ww(const SceneRef& s, f3 O, f3 D, 
 // Gains: node records, leaf ids and prim records are wave-uniform (scalar loads into
 // SGPRs), the primitive-type switch is a uniform branch, and leaf and internal-node
 // work never diverge inside a wave.  Per lane: 1 bit per level for a pushed left child.
-template <bool COUNT>
-__device__ __forceinline__ void traverse_wave(const SceneRef& s, f3 O, f3 D, Hit& h, Ev<COUNT>& ev) {
+template <bool COUNT, class SR>
+__device__ __forceinline__ void traverse_wave(const SR& s, f3 O, f3 D, Hit& h, Ev<COUNT>& ev) {
   ev.inc(EV_TRAV);
   h.index = -1; h.dist = kFLTMAX; h.shape = -1; h.dir = -1; h.cull2 = cull_bound_sq(kFLTMAX);
   const f3 invD = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);
@@ -411,8 +541,8 @@ __device__ __forceinline__ void traverse_wave(const SceneRef& s, f3 O, f3 D, Hit
   }
 }
 
-template <bool COUNT, bool WAVE>
-__device__ __forceinline__ void traverse(const SceneRef& s, f3 O, f3 D, Hit& h, Ev<COUNT>& ev) {
+template <bool COUNT, bool WAVE, class SR>
+__device__ __forceinline__ void traverse(const SR& s, f3 O, f3 D, Hit& h, Ev<COUNT>& ev) {
   if (WAVE) traverse_wave<COUNT>(s, O, D, h, ev);
 #ifdef MCPT_WHILE_WHILE
   else traverse_lane_ww<COUNT>(s, O, D, h, ev);
@@ -422,8 +552,8 @@ __device__ __forceinline__ void traverse(const SceneRef& s, f3 O, f3 D, Hit& h, 
 }
 
 // intersection_info raytracer_func.frag:812-897 (hit only; misses leave N,P untouched)
-template <bool COUNT>
-__device__ __forceinline__ void geom_info(const SceneRef& s, const Hit& h, f3& N, f3& P, Ev<COUNT>& ev) {
+template <bool COUNT, class SR>
+__device__ __forceinline__ void geom_info(const SR& s, const Hit& h, f3& N, f3& P, Ev<COUNT>& ev) {
   ev.inc(EV_GEOM);
   const float4* pr = s.prims + (size_t)h.index * 8;
   float4 t0 = pr[3], t1 = pr[4], t2 = pr[5];
@@ -445,8 +575,28 @@ __device__ __forceinline__ void geom_info(const SceneRef& s, const Hit& h, f3& N
       float lxy = __builtin_sqrtf(__builtin_fmaf(h.pl.y, h.pl.y, h.pl.x * h.pl.x));
       q = add(h.pl, mk(h.pl.x, h.pl.y, lxy / 2.0f));
     }
-  } else {   // CODE_QUAD
+  } else if (h.shape == CODE_QUAD) {
     q = add(h.pl, mk(0.0f, 0.0f, 1.0f));
+  } else {   // CODE_MESH: mesh_inter_geom_info :783-810 (smooth unless flat_face)
+    if constexpr (SR::kMesh) {
+      ev.inc(EV_MGEOM);
+      const int4 mi = s.minfo[s.ptype[h.index] >> 4];
+      const int4 vi = s.mtris[mi.w + h.dir];
+      const float4 a4 = s.mverts[vi.x], b4 = s.mverts[vi.y], c4 = s.mverts[vi.z];
+      const f3 A = mk(a4.x, a4.y, a4.z), Bv = mk(b4.x, b4.y, b4.z), C = mk(c4.x, c4.y, c4.z);
+      if (s.flat_face) {
+        q = add(h.pl, cross3(sub(Bv, A), sub(C, A)));
+      } else {
+        const float4 na = s.mnorms[vi.x], nb = s.mnorms[vi.y], nc = s.mnorms[vi.z];
+        const f3 PA = sub(A, h.pl), PB = sub(Bv, h.pl), PC = sub(C, h.pl);
+        const float tA = length3(cross3(PB, PC)), tB = length3(cross3(PA, PC)), tC = length3(cross3(PA, PB));
+        const f3 No = add(add(muls(mk(na.x, na.y, na.z), tA), muls(mk(nb.x, nb.y, nb.z), tB)),
+                          muls(mk(nc.x, nc.y, nc.z), tC));
+        q = add(h.pl, No);
+      }
+    } else {
+      return;
+    }
   }
   N = normalize3(sub(xpoint(t0, t1, t2, q), P));
 }
@@ -486,7 +636,7 @@ __device__ __forceinline__ int floordiv(int a, int b) { return (a >= 0) ? a / b 
 // pass range inside one accumulation chunk of kPassChunk absolute passes:
 // segments of one pixel are independent items (strong-scaling parallelism beyond one
 // lane per pixel); their sums are combined in chunk order by combine_kernel.
-template <bool COUNT, bool WAVE>
+template <bool COUNT, bool WAVE, bool MESH>
 __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParams p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -501,7 +651,8 @@ __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParam
   const int pass_end = min(p.first_pass + p.n_passes, (c0 + 1) * kPassChunk + 1);
   const int y = ((lr / p.band_rows) * p.world + p.rank) * p.band_rows + (lr % p.band_rows);
 
-  SceneRef s{p.nodes, p.leaves, p.ptype, p.prims, p.depth};
+  SceneT<MESH> s{p.nodes, p.leaves, p.ptype, p.prims, p.depth, p.minfo, p.mnodes, p.mleaves, p.mtris, p.mverts,
+                 p.mnorms, p.flat_face};
   Ev<COUNT> ev;
   ev.init();
 
@@ -766,11 +917,12 @@ __global__ __launch_bounds__(256) void combine_kernel(float* __restrict__ accum,
 // hit_one_prim + intersection_info + intersection_color_info / _mat_info
 // (raytracer_func.frag:718-781, 874-907) for caller-supplied rays, one lane per ray
 // ------------------------------------------------------------------------------------
-template <bool ANY>
+template <bool ANY, bool MESH>
 __global__ __launch_bounds__(256) void trace_kernel(TraceParams q) {
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   if (i >= q.n) return;
-  SceneRef s{q.nodes, q.leaves, q.ptype, q.prims, q.depth};
+  SceneT<MESH> s{q.nodes, q.leaves, q.ptype, q.prims, q.depth, q.minfo, q.mnodes, q.mleaves, q.mtris, q.mverts,
+                 q.mnorms, q.flat_face};
   Ev<false> ev;
   const f3 O = mk(q.orig[3 * i], q.orig[3 * i + 1], q.orig[3 * i + 2]);
   const f3 D = mk(q.dir[3 * i], q.dir[3 * i + 1], q.dir[3 * i + 2]);
@@ -780,7 +932,7 @@ __global__ __launch_bounds__(256) void trace_kernel(TraceParams q) {
     traverse_lane<false, ANY>(s, O, D, h, ev);
   } else {                                       // intersect_one_prim / hit_one_prim
     h.index = -1; h.dist = kFLTMAX; h.shape = -1; h.dir = -1; h.cull2 = cull_bound_sq(kFLTMAX);
-    prim_test<false, false>(s, q.prim, O, D, h, ev);
+    prim_test<false, false, ANY>(s, q.prim, O, D, h, ev);
   }
   float* o = q.out + i * kTraceFloats;
   int* oi = q.out_i + i * 3;
@@ -819,8 +971,13 @@ __global__ __launch_bounds__(256) void sample_kernel(SampleParams q) {
 hipError_t mcpt_launch_trace(const mcpt::TraceParams& q, bool any_hit, hipStream_t stream) {
   if (q.n <= 0) return hipSuccess;
   dim3 block(256), grid((unsigned)((q.n + 255) / 256));
-  if (any_hit) hipLaunchKernelGGL(mcpt::trace_kernel<true>, grid, block, 0, stream, q);
-  else hipLaunchKernelGGL(mcpt::trace_kernel<false>, grid, block, 0, stream, q);
+  if (q.n_meshes > 0) {
+    if (any_hit) hipLaunchKernelGGL((mcpt::trace_kernel<true, true>), grid, block, 0, stream, q);
+    else hipLaunchKernelGGL((mcpt::trace_kernel<false, true>), grid, block, 0, stream, q);
+  } else {
+    if (any_hit) hipLaunchKernelGGL((mcpt::trace_kernel<true, false>), grid, block, 0, stream, q);
+    else hipLaunchKernelGGL((mcpt::trace_kernel<false, false>), grid, block, 0, stream, q);
+  }
   return hipGetLastError();
 }
 
@@ -838,14 +995,16 @@ hipError_t mcpt_launch_render(const mcpt::RenderParams& p, bool count, hipStream
   const long long items = (long long)p.n_tiles * p.n_segments;
   if (items <= 0) return hipSuccess;
   dim3 block(256), grid((unsigned)items);
-  const bool wave = p.wave_traversal != 0;
+  const bool wave = p.wave_traversal != 0, mesh = p.n_meshes > 0;
+#define MCPT_RENDER(C, W, M) hipLaunchKernelGGL((mcpt::render_kernel<C, W, M>), grid, block, 0, stream, p)
   if (count) {
-    if (wave) hipLaunchKernelGGL((mcpt::render_kernel<true, true>), grid, block, 0, stream, p);
-    else hipLaunchKernelGGL((mcpt::render_kernel<true, false>), grid, block, 0, stream, p);
+    if (wave) { if (mesh) MCPT_RENDER(true, true, true); else MCPT_RENDER(true, true, false); }
+    else { if (mesh) MCPT_RENDER(true, false, true); else MCPT_RENDER(true, false, false); }
   } else {
-    if (wave) hipLaunchKernelGGL((mcpt::render_kernel<false, true>), grid, block, 0, stream, p);
-    else hipLaunchKernelGGL((mcpt::render_kernel<false, false>), grid, block, 0, stream, p);
+    if (wave) { if (mesh) MCPT_RENDER(false, true, true); else MCPT_RENDER(false, true, false); }
+    else { if (mesh) MCPT_RENDER(false, false, true); else MCPT_RENDER(false, false, false); }
   }
+#undef MCPT_RENDER
   return hipGetLastError();
 }
 

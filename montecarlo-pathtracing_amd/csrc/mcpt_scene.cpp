@@ -110,6 +110,9 @@ static Vec3 apply_pt(const Mat4& t, float x, float y, float z) {
   return {o[0], o[1], o[2]};
 }
 
+static void kd_build(const std::vector<Vec3>& centre, const std::vector<float>& box, int& depth,
+                     std::vector<float>& nodes, std::vector<int>& leaves);
+
 // PrimData record (scene.h:64-73) + the BVH built over the records
 class PrimScene {
  public:
@@ -123,7 +126,10 @@ class PrimScene {
   float* rec(int i) { return records.data() + (size_t)i * 64; }
   const float* rec(int i) const { return records.data() + (size_t)i * 64; }
 
-  void clear() { records.clear(); nodes.clear(); leaves.clear(); depth = 0; nb_emissive = 0; finalized = false; }
+  void clear() {
+    records.clear(); nodes.clear(); leaves.clear(); meshes.clear();
+    depth = 0; nb_emissive = 0; finalized = false;
+  }
 
   int push(int code, const Mat4& trf, const Material& mat, float area) {   // scene.cpp:44-53
     Mat4 inv = trf.inverse();
@@ -206,60 +212,136 @@ class PrimScene {
     nb_emissive = emissive_first();
     std::vector<Vec3> centre(n);
     std::vector<float> box((size_t)n * 6);
-    std::vector<int> order(n);
-    for (int i = 0; i < n; ++i) { order[i] = i; centre[i] = prim_box(i, &box[(size_t)i * 6]); }
-    depth = (int)std::ceil(std::log2((float)n));
-    // median splits, one round per level above the leaf pairs, axis x → y → z
-    std::vector<int> bounds{0, n}, next;
-    int axis = 0;
-    for (int round = 1; round < depth; ++round) {
-      next.assign(1, bounds[0]);
-      for (size_t s = 1; s < bounds.size(); ++s) {
-        int64_t lo = bounds[s - 1], hi = bounds[s], mid = (lo + hi) / 2;
-        auto key = [&](int id) { return axis == 0 ? centre[id].x : (axis == 1 ? centre[id].y : centre[id].z); };
-        std::nth_element(order.begin() + lo, order.begin() + mid, order.begin() + hi,
-                         [&](int a, int b) { return key(a) < key(b); });
-        next.push_back((int)mid);
-        next.push_back((int)hi);
-      }
-      bounds.swap(next);
-      axis = (axis + 1) % 3;
-    }
-    const int n_leaf = 1 << depth, n_node = 2 * n_leaf - 1;
-    leaves.assign(n_leaf, -1);
-    nodes.assign((size_t)n_node * 6, 0.0f);
-    auto put = [&](int node, int prim) { std::memcpy(&nodes[(size_t)node * 6], &box[(size_t)prim * 6], 24); };
-    if (n == 1) {
-      put(0, 0);   // depth 0: the root is the only leaf and keeps id -1 (bvh.cpp writes ind[-1])
-    } else {
-      // every final segment holds 1 or 2 prims and fills a pair of leaves from the right
-      int node = n_node - 1, leaf = n_leaf - 1;
-      for (int s = (int)bounds.size() - 1; s > 0; --s, node -= 2, leaf -= 2) {
-        int first = bounds[s - 1];
-        if (bounds[s] - first == 1) {
-          int id = order[first];
-          leaves[leaf] = -1; leaves[leaf - 1] = id;
-          put(node, id); put(node - 1, id);
-        } else {
-          leaves[leaf] = order[first + 1]; put(node, order[first + 1]);
-          leaves[leaf - 1] = order[first]; put(node - 1, order[first]);
-        }
-      }
-      // internal boxes: merge of the two children, bottom-up (scene.cpp:91-100)
-      for (int k = n_node - 1; k >= 2; k -= 2) {
-        float* parent = &nodes[(size_t)((k - 2) / 2) * 6];
-        const float* c1 = &nodes[(size_t)k * 6];
-        const float* c2 = &nodes[(size_t)(k - 1) * 6];
-        for (int q = 0; q < 3; ++q) {
-          parent[q] = std::min(c1[q], c2[q]);
-          parent[3 + q] = std::max(c1[3 + q], c2[3 + q]);
-        }
-      }
-    }
+    for (int i = 0; i < n; ++i) centre[i] = prim_box(i, &box[(size_t)i * 6]);
+    kd_build(centre, box, depth, nodes, leaves);
     finalized = true;
     return MCPT_OK;
   }
+
+  // ---- triangle meshes (BVH_GPU_Scene::add_mesh / place_mesh, gpu_bvh_scene.cpp:51-74,
+  //      gpu_bvh_scene.h:89-92; ScenePrimitives::add_mesh scene.cpp:56-67)
+  struct Mesh {
+    std::vector<float> verts, normals;   // 3 per vertex
+    std::vector<uint32_t> tris;          // 3 per triangle, mesh-local vertex indices
+    float bbmin[3], bbmax[3];            // Mesh::BB()
+    int depth = 0;
+    std::vector<float> nodes;            // (2^(d+1)-1) × 6, mesh-local space
+    std::vector<int> leaves;             // 2^d mesh-local triangle ids or -1
+  };
+  std::vector<Mesh> meshes;
+
+  // SceneMesh::prim_bb (scene.cpp:106-122): triangle AABB grown by 0.001, its centre
+  static Vec3 tri_box(const Mesh& m, int t, float* bb) {
+    const float* P[3];
+    for (int k = 0; k < 3; ++k) P[k] = &m.verts[(size_t)m.tris[(size_t)t * 3 + k] * 3];
+    for (int i = 0; i < 3; ++i) {
+      bb[i] = std::min({P[0][i], P[1][i], P[2][i]}) - 0.001f;
+      bb[3 + i] = std::max({P[0][i], P[1][i], P[2][i]}) + 0.001f;
+    }
+    return Vec3{(bb[0] + bb[3]) / 2.0f, (bb[1] + bb[4]) / 2.0f, (bb[2] + bb[5]) / 2.0f};
+  }
+
+  int add_mesh(const float* v, const float* nrm, int nv, const uint32_t* t, int nt, const float* bb6) {
+    if (!v || !nrm || !t || nv <= 0 || nt <= 0) return -1;
+    for (int i = 0; i < nt * 3; ++i)
+      if (t[i] >= (uint32_t)nv) return -1;
+    Mesh m;
+    m.verts.assign(v, v + (size_t)nv * 3);
+    m.normals.assign(nrm, nrm + (size_t)nv * 3);
+    m.tris.assign(t, t + (size_t)nt * 3);
+    if (bb6) {
+      for (int k = 0; k < 3; ++k) { m.bbmin[k] = bb6[k]; m.bbmax[k] = bb6[3 + k]; }
+    } else {   // BoundingBox::add_point over the vertices (easycppogl/mesh.h:38-76)
+      for (int k = 0; k < 3; ++k) { m.bbmin[k] = v[k]; m.bbmax[k] = v[k]; }
+      for (int i = 1; i < nv; ++i)
+        for (int k = 0; k < 3; ++k) {
+          m.bbmin[k] = std::min(m.bbmin[k], v[(size_t)i * 3 + k]);
+          m.bbmax[k] = std::max(m.bbmax[k], v[(size_t)i * 3 + k]);
+        }
+    }
+    std::vector<Vec3> centre(nt);
+    std::vector<float> box((size_t)nt * 6);
+    for (int i = 0; i < nt; ++i) centre[i] = tri_box(m, i, &box[(size_t)i * 6]);
+    kd_build(centre, box, m.depth, m.nodes, m.leaves);   // BVH_GPU_Scene::add_bvh → compute
+    meshes.push_back(std::move(m));
+    finalized = false;
+    return (int)meshes.size() - 1;
+  }
+
+  // ScenePrimitives::add_mesh: transfo = trf · BB.matrix(), inverse = trf^-1, mesh transfo = trf,
+  // type (0, mesh line) — the mesh id here; area 0
+  int place_mesh(int mesh, const Mat4& trf, const Material& mat) {
+    if (mesh < 0 || mesh >= (int)meshes.size()) return -1;
+    const Mesh& m = meshes[mesh];
+    const float c[3] = {(m.bbmin[0] + m.bbmax[0]) / 2.0f, (m.bbmin[1] + m.bbmax[1]) / 2.0f,
+                        (m.bbmin[2] + m.bbmax[2]) / 2.0f};
+    const float sc[3] = {(m.bbmax[0] - m.bbmin[0]) / 2.0f, (m.bbmax[1] - m.bbmin[1]) / 2.0f,
+                         (m.bbmax[2] - m.bbmin[2]) / 2.0f};
+    const Mat4 trBB = trf * (xf::T(c[0], c[1], c[2]) * xf::S(sc[0], sc[1], sc[2]));   // BoundingBox::matrix()
+    int i = push(kMesh, trBB, mat, 0.0f);
+    float* r = rec(i);
+    const Mat4 inv = trf.inverse();
+    std::memcpy(r + 16, inv.m, 64);
+    std::memcpy(r + 32, trf.m, 64);
+    r[49] = (float)mesh;
+    return i;
+  }
 };
+
+// BVH_KDtree::compute (bvh.cpp:34-93) over precomputed boxes / centres: ceil(log2 n) levels,
+// depth-1 rounds of std::nth_element median splits on x → y → z, leaf pairs from the right
+// (a lone item: left leaf + -1, its box twice), internal boxes merged bottom-up.
+static void kd_build(const std::vector<Vec3>& centre, const std::vector<float>& box, int& depth,
+                     std::vector<float>& nodes, std::vector<int>& leaves) {
+  const int n = (int)centre.size();
+  std::vector<int> order(n);
+  for (int i = 0; i < n; ++i) order[i] = i;
+  depth = (int)std::ceil(std::log2((float)n));
+  std::vector<int> bounds{0, n}, next;
+  int axis = 0;
+  for (int round = 1; round < depth; ++round) {
+    next.assign(1, bounds[0]);
+    for (size_t s = 1; s < bounds.size(); ++s) {
+      int64_t lo = bounds[s - 1], hi = bounds[s], mid = (lo + hi) / 2;
+      auto key = [&](int id) { return axis == 0 ? centre[id].x : (axis == 1 ? centre[id].y : centre[id].z); };
+      std::nth_element(order.begin() + lo, order.begin() + mid, order.begin() + hi,
+                       [&](int a, int b) { return key(a) < key(b); });
+      next.push_back((int)mid);
+      next.push_back((int)hi);
+    }
+    bounds.swap(next);
+    axis = (axis + 1) % 3;
+  }
+  const int n_leaf = 1 << depth, n_node = 2 * n_leaf - 1;
+  leaves.assign(n_leaf, -1);
+  nodes.assign((size_t)n_node * 6, 0.0f);
+  auto put = [&](int node, int item) { std::memcpy(&nodes[(size_t)node * 6], &box[(size_t)item * 6], 24); };
+  if (n == 1) {
+    put(0, 0);   // depth 0: the root is the only leaf and keeps id -1 (bvh.cpp writes ind[-1])
+    return;
+  }
+  int node = n_node - 1, leaf = n_leaf - 1;
+  for (int s = (int)bounds.size() - 1; s > 0; --s, node -= 2, leaf -= 2) {
+    int first = bounds[s - 1];
+    if (bounds[s] - first == 1) {
+      int id = order[first];
+      leaves[leaf] = -1; leaves[leaf - 1] = id;
+      put(node, id); put(node - 1, id);
+    } else {
+      leaves[leaf] = order[first + 1]; put(node, order[first + 1]);
+      leaves[leaf - 1] = order[first]; put(node - 1, order[first]);
+    }
+  }
+  for (int k = n_node - 1; k >= 2; k -= 2) {   // merge (scene.cpp:91-100)
+    float* parent = &nodes[(size_t)((k - 2) / 2) * 6];
+    const float* c1 = &nodes[(size_t)k * 6];
+    const float* c2 = &nodes[(size_t)(k - 1) * 6];
+    for (int q = 0; q < 3; ++q) {
+      parent[q] = std::min(c1[q], c2[q]);
+      parent[3 + q] = std::max(c1[3 + q], c2[3 + q]);
+    }
+  }
+}
 
 // ------------------------------------------------------------------------------------
 // the reference scenes (montecarlo.cpp:629-795); colours montecarlo.cpp:33-44
@@ -496,6 +578,50 @@ MCPT_ADD(mcpt_scene_add_cylinder, cylinder)
 MCPT_ADD(mcpt_scene_add_cone, cone)
 MCPT_ADD(mcpt_scene_add_oriented_quad, quad)
 #undef MCPT_ADD
+
+int mcpt_scene_add_mesh(mcpt_scene* s, const float* vertices, const float* normals, int n_vertices,
+                        const unsigned* tri_indices, int n_triangles, const float* bb6, int* mesh_id) {
+  if (!s) return MCPT_ERR_INVALID_ARG;
+  int id = s->s.add_mesh(vertices, normals, n_vertices, tri_indices, n_triangles, bb6);
+  if (id < 0) return MCPT_ERR_INVALID_ARG;
+  if (mesh_id) *mesh_id = id;
+  return MCPT_OK;
+}
+int mcpt_scene_place_mesh(mcpt_scene* s, int mesh_id, const float* trf16, const float* m7) {
+  Mat4 t; Material m;
+  if (!s || !unpack(trf16, m7, t, m)) return MCPT_ERR_INVALID_ARG;
+  return s->s.place_mesh(mesh_id, t, m) >= 0 ? MCPT_OK : MCPT_ERR_INVALID_ARG;
+}
+int mcpt_scene_mesh_sizes(mcpt_scene* s, int* n_meshes, int* n_nodes, int* n_leaves, int* n_tris, int* n_verts) {
+  if (!s || !n_meshes || !n_nodes || !n_leaves || !n_tris || !n_verts) return MCPT_ERR_INVALID_ARG;
+  *n_meshes = (int)s->s.meshes.size();
+  *n_nodes = *n_leaves = *n_tris = *n_verts = 0;
+  for (const auto& m : s->s.meshes) {
+    *n_nodes += (int)(m.nodes.size() / 6);
+    *n_leaves += (int)m.leaves.size();
+    *n_tris += (int)(m.tris.size() / 3);
+    *n_verts += (int)(m.verts.size() / 3);
+  }
+  return MCPT_OK;
+}
+int mcpt_scene_get_mesh_buffers(mcpt_scene* s, int* info, float* nodes, int* leaves, int* tris, float* verts,
+                                float* normals) {
+  if (!s) return MCPT_ERR_INVALID_ARG;
+  int no = 0, lo = 0, to = 0, vo = 0, k = 0;
+  for (const auto& m : s->s.meshes) {
+    if (info) { info[4 * k] = no; info[4 * k + 1] = lo; info[4 * k + 2] = m.depth; info[4 * k + 3] = to; }
+    if (nodes) std::memcpy(nodes + (size_t)no * 6, m.nodes.data(), m.nodes.size() * 4);
+    if (leaves) std::memcpy(leaves + lo, m.leaves.data(), m.leaves.size() * 4);
+    if (tris)
+      for (size_t i = 0; i < m.tris.size(); ++i) tris[(size_t)to * 3 + i] = (int)m.tris[i] + vo;   // global vertex ids
+    if (verts) std::memcpy(verts + (size_t)vo * 3, m.verts.data(), m.verts.size() * 4);
+    if (normals) std::memcpy(normals + (size_t)vo * 3, m.normals.data(), m.normals.size() * 4);
+    no += (int)(m.nodes.size() / 6); lo += (int)m.leaves.size(); to += (int)(m.tris.size() / 3);
+    vo += (int)(m.verts.size() / 3);
+    ++k;
+  }
+  return MCPT_OK;
+}
 
 int mcpt_scene_finalize(mcpt_scene* s) { return s ? s->s.finalize() : MCPT_ERR_INVALID_ARG; }
 int mcpt_scene_nb_prim(mcpt_scene* s, int* n) { if (!s || !n) return MCPT_ERR_INVALID_ARG; *n = s->s.count(); return MCPT_OK; }

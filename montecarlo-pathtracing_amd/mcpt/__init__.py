@@ -32,7 +32,7 @@ __all__ = [
 
 MONTECARLO, MAT, MAT_TR = 0, 1, 2
 TRAVERSAL_AUTO, TRAVERSAL_LANE, TRAVERSAL_WAVE = 0, 1, 2
-EVENT_NAMES = ("node", "leaf", "prim", "cand", "geom", "colmat", "sample", "trav")
+EVENT_NAMES = ("node", "leaf", "prim", "cand", "geom", "colmat", "sample", "trav", "mesh", "tri", "mgeom")
 # key bindings of montecarlo.cpp:251-290: scene id -> key
 SCENE_KEYS = {1: "Q", 2: "W", 3: "E", 4: "R", 5: "T", 6: "Y", 7: "U", 8: "I"}
 
@@ -101,6 +101,12 @@ def _declare(L: ctypes.CDLL) -> None:
         "mcpt_scene_add_cone": (i, [_vp, fp, fp]),
         "mcpt_scene_add_oriented_quad": (i, [_vp, fp, fp]),
         "mcpt_scene_finalize": (i, [_vp]),
+        "mcpt_scene_add_mesh": (i, [_vp, fp, fp, i, ctypes.POINTER(ctypes.c_uint), i, fp, ip]),
+        "mcpt_scene_place_mesh": (i, [_vp, i, fp, fp]),
+        "mcpt_scene_mesh_sizes": (i, [_vp, ip, ip, ip, ip, ip]),
+        "mcpt_scene_get_mesh_buffers": (i, [_vp, ip, fp, ip, ip, fp, fp]),
+        "mcpt_upload_meshes": (i, [_vp, i, ip, i, fp, i, ip, i, ip, i, fp, fp]),
+        "mcpt_set_flat_face": (i, [_vp, i]),
         "mcpt_scene_nb_prim": (i, [_vp, ip]),
         "mcpt_scene_depth": (i, [_vp, ip]),
         "mcpt_scene_nb_emissives": (i, [_vp, ip]),
@@ -222,6 +228,43 @@ class Scene:
         self._add("mcpt_scene_add_oriented_quad", self._colmajor(trf), mat)
 
     add_orientedQuad = add_oriented_quad   # reference spelling (gpu_bvh_scene.h:103)
+
+    def add_mesh(self, vertices, normals, tri_indices, bb=None) -> int:
+        """BVH_GPU_Scene::add_mesh: store a mesh (positions, normals, triangle vertex indices)
+        and build its BVH; bb = (min.xyz, max.xyz) of Mesh::BB(), default the vertices' box.
+        Returns the mesh id for place_mesh."""
+        v = np.ascontiguousarray(np.asarray(vertices, np.float32).reshape(-1, 3))
+        n = np.ascontiguousarray(np.asarray(normals, np.float32).reshape(-1, 3))
+        t = np.ascontiguousarray(np.asarray(tri_indices, np.uint32).reshape(-1, 3))
+        if n.shape != v.shape:
+            raise ValueError("one normal per vertex")
+        b = None if bb is None else _f32(bb, 6)
+        mid = ctypes.c_int()
+        _check(lib().mcpt_scene_add_mesh(self._h, _fp(v), _fp(n), v.shape[0],
+                                         t.ctypes.data_as(ctypes.POINTER(ctypes.c_uint)), t.shape[0],
+                                         _fp(b) if b is not None else None, ctypes.byref(mid)), "mcpt_scene_add_mesh")
+        return mid.value
+
+    def place_mesh(self, mesh_id: int, trf, mat) -> None:
+        """BVH_GPU_Scene::place_mesh: an instance of mesh `mesh_id` (a CODE_MESH primitive)."""
+        t = _f32(self._colmajor(trf), 16)
+        m = _f32(mat, 7)
+        _check(lib().mcpt_scene_place_mesh(self._h, int(mesh_id), _fp(t), _fp(m)), "mcpt_scene_place_mesh")
+
+    def mesh_buffers(self):
+        """dict of the flat mesh buffers (mcpt_scene_get_mesh_buffers layouts), or None."""
+        sz = [ctypes.c_int() for _ in range(5)]
+        _check(lib().mcpt_scene_mesh_sizes(self._h, *[ctypes.byref(x) for x in sz]), "mcpt_scene_mesh_sizes")
+        nm, nn, nl, nt, nv = (x.value for x in sz)
+        if nm == 0:
+            return None
+        b = {"info": np.zeros((nm, 4), np.int32), "nodes": np.zeros((nn, 6), np.float32),
+             "leaves": np.zeros(nl, np.int32), "tris": np.zeros((nt, 3), np.int32),
+             "verts": np.zeros((nv, 3), np.float32), "normals": np.zeros((nv, 3), np.float32)}
+        _check(lib().mcpt_scene_get_mesh_buffers(self._h, _ip(b["info"]), _fp(b["nodes"]), _ip(b["leaves"]),
+                                                 _ip(b["tris"]), _fp(b["verts"]), _fp(b["normals"])),
+               "mcpt_scene_get_mesh_buffers")
+        return b
 
     def finalize(self) -> None:
         _check(lib().mcpt_scene_finalize(self._h), "mcpt_scene_finalize")
@@ -362,6 +405,29 @@ class Renderer:
         n = prims.size // 64
         _check(lib().mcpt_upload_scene(self._h, _fp(prims), int(n), _fp(nodes), _ip(leaves),
                                        int(depth), int(nb_emissives)), "mcpt_upload_scene")
+        if scene is not None:
+            mb = scene.mesh_buffers()
+            if mb is not None:
+                self.upload_meshes(mb)
+
+    def upload_meshes(self, mb) -> None:
+        """mcpt_upload_meshes from a Scene.mesh_buffers() dict (None/empty: no meshes)."""
+        if not mb:
+            _check(lib().mcpt_upload_meshes(self._h, 0, None, 0, None, 0, None, 0, None, 0, None, None),
+                   "mcpt_upload_meshes")
+            return
+        info = np.ascontiguousarray(mb["info"], np.int32)
+        nodes = np.ascontiguousarray(mb["nodes"], np.float32)
+        leaves = np.ascontiguousarray(mb["leaves"], np.int32)
+        tris = np.ascontiguousarray(mb["tris"], np.int32)
+        verts = np.ascontiguousarray(mb["verts"], np.float32)
+        norms = np.ascontiguousarray(mb["normals"], np.float32)
+        _check(lib().mcpt_upload_meshes(self._h, info.shape[0], _ip(info), nodes.shape[0], _fp(nodes), leaves.size,
+                                        _ip(leaves), tris.shape[0], _ip(tris), verts.shape[0], _fp(verts),
+                                        _fp(norms)), "mcpt_upload_meshes")
+
+    def set_flat_face(self, flat: bool) -> None:
+        _check(lib().mcpt_set_flat_face(self._h, int(bool(flat))), "mcpt_set_flat_face")
 
     def set_target(self, W: int, H: int, band_rows: int = 8, world: int = 1, rank: int = 0) -> None:
         _check(lib().mcpt_set_target(self._h, int(W), int(H), int(band_rows), int(world), int(rank)),

@@ -14,9 +14,9 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
-EV_NAMES = ("node", "leaf", "prim", "cand", "geom", "colmat", "sample", "trav")
+EV_NAMES = ("node", "leaf", "prim", "cand", "geom", "colmat", "sample", "trav", "mesh", "tri", "mgeom")
 # bytes per event: node 48, leaf 4, prim 16+64, cand 64, geom 64, col+mat 32, sample 24
-EV_BYTES = np.array([48, 4, 80, 64, 64, 32, 24, 0], np.int64)
+EV_BYTES = np.array([48, 4, 80, 64, 64, 32, 24, 0, 140, 48, 148], np.int64)
 
 _fp = ctypes.POINTER(ctypes.c_float)
 _ip = ctypes.POINTER(ctypes.c_int)
@@ -46,7 +46,7 @@ def lib() -> ctypes.CDLL:
             "orc_scene_n_emissive": (i, [_vp]),
             "orc_scene_export": (i, [_vp, _fp, _fp, _ip]),
             "orc_camera": (None, [i, i, _fp, _fp]),
-            "orc_render": (i, [_fp, i, _fp, _ip, i, _fp, _fp, i, i, i, i, f, i, f, i, i, i, i, _fp, _u64p, _up]),
+            "orc_render": (i, [_fp, i, _fp, _ip, i, _fp, _fp, i, i, i, i, f, i, f, i, i, i, i, _fp, _u64p, _up, _vp]),
             "orc_xxhash32": (ctypes.c_uint, [ctypes.c_uint, ctypes.c_uint, ctypes.c_uint]),
             "orc_srand": (None, [f, f, i, f, _up]),
             "orc_random_floats": (None, [_up, i, _fp]),
@@ -57,7 +57,10 @@ def lib() -> ctypes.CDLL:
             "orc_random_ray": (None, [_up, _fp, f, _fp, _up]),
             "orc_intersect_prim": (i, [_fp, _fp, _fp, _fp, _ip, _fp, _fp]),
             "orc_corner_rays": (None, [_fp, _fp, _fp]),
-            "orc_trace": (i, [_fp, i, _fp, _ip, i, _fp, _fp, i, i, i, _ip, _fp]),
+            "orc_trace": (i, [_fp, i, _fp, _ip, i, _fp, _fp, i, i, i, _ip, _fp, _vp]),
+            "orc_mesh_view": (_vp, [_ip, _fp, _ip, _ip, _fp, _fp, i, i]),
+            "orc_mesh_view_free": (None, [_vp]),
+            "orc_mesh_bvh": (i, [_fp, _ip, i, _fp, _ip]),
             "orc_sample_hemisphere": (None, [_fp, _fp, f, i, i, _fp]),
         }
         for name, (res, args) in sigs.items():
@@ -96,8 +99,37 @@ def camera(W: int, H: int) -> Tuple[np.ndarray, np.ndarray]:
     return ipv, iv
 
 
+class MeshView:
+    """Holds flat mesh buffers (a Scene.mesh_buffers()-style dict) for orc_render/orc_trace."""
+
+    def __init__(self, mb, flat_face=False):
+        self.arrays = {k: np.ascontiguousarray(mb[k], np.int32 if k in ("info", "leaves", "tris") else np.float32)
+                       for k in ("info", "nodes", "leaves", "tris", "verts", "normals")}
+        a = self.arrays
+        self.h = lib().orc_mesh_view(P(a["info"], _ip), P(a["nodes"]), P(a["leaves"], _ip), P(a["tris"], _ip),
+                                     P(a["verts"]), P(a["normals"]), a["info"].shape[0], int(bool(flat_face)))
+
+    def __del__(self):
+        if getattr(self, "h", None) and _L is not None:
+            _L.orc_mesh_view_free(self.h)
+            self.h = None
+
+
+def mesh_bvh(verts, tris):
+    """Independent mesh BVH (SceneMesh::prim_bb + BVH_KDtree): (depth, nodes, leaves)."""
+    v = np.ascontiguousarray(verts, np.float32).reshape(-1, 3)
+    t = np.ascontiguousarray(tris, np.int32).reshape(-1, 3)
+    d = int(np.ceil(np.log2(np.float32(t.shape[0])))) if t.shape[0] > 1 else 0
+    nodes = np.zeros((2 ** (d + 1) - 1, 6), np.float32)
+    leaves = np.zeros(2 ** d, np.int32)
+    depth = lib().orc_mesh_bvh(P(v), P(t, _ip), t.shape[0], P(nodes), P(leaves, _ip))
+    assert depth == d, (depth, d)
+    return depth, nodes, leaves
+
+
 def render(prims, nodes, leaves, depth, invPV, invV, W, H, first_pass=1, n_passes=1, date=0.0,
-           bounces=3, ior=1.0, variant=0, row_step=1, row_offset=0, n_threads=0, accum=None, trav_px=None):
+           bounces=3, ior=1.0, variant=0, row_step=1, row_offset=0, n_threads=0, accum=None, trav_px=None,
+           meshes=None):
     """Accumulate passes into accum (H×W×3 f32, row 0 = bottom); returns (accum, events[8]).
     trav_px: optional H×W uint32 array receiving each pixel's traversal count (analysis)."""
     prims = np.ascontiguousarray(prims, np.float32)
@@ -107,11 +139,11 @@ def render(prims, nodes, leaves, depth, invPV, invV, W, H, first_pass=1, n_passe
     invV = np.ascontiguousarray(invV, np.float32)
     if accum is None:
         accum = np.zeros((H, W, 3), np.float32)
-    ev = np.zeros(8, np.uint64)
+    ev = np.zeros(len(EV_NAMES), np.uint64)
     r = lib().orc_render(P(prims), prims.size // 64, P(nodes), P(leaves, _ip), int(depth), P(invPV), P(invV),
                          int(W), int(H), int(first_pass), int(n_passes), float(date), int(bounces), float(ior),
                          int(variant), int(row_step), int(row_offset), int(n_threads), P(accum), P(ev, _u64p),
-                         P(trav_px, _up) if trav_px is not None else None)
+                         P(trav_px, _up) if trav_px is not None else None, meshes.h if meshes is not None else None)
     if r != 0:
         raise RuntimeError(f"orc_render failed ({r})")
     return accum, ev
@@ -161,7 +193,7 @@ def intersect_prim(rec64, O, D):
     return shape, dist.value, dr.value, pl, pg
 
 
-def trace(prims, nodes, leaves, depth, origins, dirs, any_hit=False, prim=-1):
+def trace(prims, nodes, leaves, depth, origins, dirs, any_hit=False, prim=-1, meshes=None):
     """(ints n×3 [shape, prim, dir], floats n×21 [dist, pl, pg, N, P, colour, material])."""
     prims = np.ascontiguousarray(prims, np.float32)
     nodes = np.ascontiguousarray(nodes, np.float32)
@@ -172,7 +204,7 @@ def trace(prims, nodes, leaves, depth, origins, dirs, any_hit=False, prim=-1):
     oi = np.zeros((n, 3), np.int32)
     of = np.zeros((n, 21), np.float32)
     r = lib().orc_trace(P(prims), prims.size // 64, P(nodes), P(leaves, _ip), int(depth), P(o), P(d), n,
-                        int(bool(any_hit)), int(prim), P(oi, _ip), P(of))
+                        int(bool(any_hit)), int(prim), P(oi, _ip), P(of), meshes.h if meshes is not None else None)
     if r != 0:
         raise RuntimeError("orc_trace failed")
     return oi, of
