@@ -147,9 +147,10 @@ int mcpt_get_traversal(mcpt_ctx* ctx, int* resolved_mode);
  * origins, dirs: n × 3 f32 host arrays (directions used as given, like the shader).  A miss
  * has shape = -1, dist = FLT_MAX and zero N/P/colour/material.  Synchronous. */
 typedef struct mcpt_hit {
-  int shape;          /* primitive type code of the hit (1 sphere .. 5 quad), -1 = miss */
+  int shape;          /* primitive type code of the hit (0 mesh, 1 sphere .. 5 quad), -1 = miss */
   int prim;           /* primitive index (after sortEmissiveFirst) */
-  int dir;            /* face / part code of the hit (closest_intersection.dir) */
+  int dir;            /* face / part code of the hit (closest_intersection.dir); for a mesh
+                         hit the mesh-local triangle index (Mesh_intersect's tri_index) */
   float dist;         /* world distance from the origin */
   float pl[3], pg[3]; /* hit point in primitive space / world space */
   float N[3], P[3];   /* intersection_info: normal and position */
