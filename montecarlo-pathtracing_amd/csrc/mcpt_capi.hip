@@ -142,7 +142,8 @@ int mcpt_destroy(mcpt_ctx* c) {
 
 int mcpt_upload_scene(mcpt_ctx* c, const float* prims, int n_prims, const float* nodes, const int* leaves,
                       int depth, int nb_emissives) {
-  if (!c || !prims || !nodes || !leaves || n_prims <= 0 || depth < 0 || depth > 24)
+  // n_prims < 2^28: the kernel packs a primitive index with its type code in one word
+  if (!c || !prims || !nodes || !leaves || n_prims <= 0 || n_prims >= (1 << 28) || depth < 0 || depth > 24)
     return set_err(MCPT_ERR_INVALID_ARG, "mcpt_upload_scene: bad arguments");
   const int n_leaf = 1 << depth, n_node = 2 * n_leaf - 1;
   for (int i = 0; i < n_leaf; ++i)
@@ -374,7 +375,15 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   p.accum = c->d_accum; p.events = c->d_events;
   corner_rays(invPV, invV, p);
   p.W = c->W; p.H = c->H; p.band_rows = c->band_rows; p.world = c->world; p.rank = c->rank;
-  p.n_local_rows = c->n_local_rows; p.depth = c->depth;
+  p.n_local_rows = c->n_local_rows; p.depth = c->depth; p.n_prims = c->n_prims;
+#ifndef MCPT_LDS_SCENE
+#define MCPT_LDS_SCENE 1
+#endif
+  {
+    const long long lds = ((3LL * ((2LL << c->depth) - 1) + (long long)mcpt::kPrimF4 * c->n_prims) * 16) +
+                          (((1LL << c->depth) + c->n_prims) * 4);
+    p.lds_scene_bytes = (MCPT_LDS_SCENE && c->n_meshes == 0 && lds <= mcpt::kLdsSceneBytes) ? (int)lds : 0;
+  }
   p.minfo = c->d_minfo; p.mnodes = c->d_mnodes; p.mleaves = c->d_mleaves; p.mtris = c->d_mtris;
   p.mverts = c->d_mverts; p.mnorms = c->d_mnorms; p.n_meshes = c->n_meshes; p.flat_face = c->flat_face;
   p.wave_traversal = (resolve_traversal(c) == MCPT_TRAVERSAL_WAVE) ? 1 : 0;

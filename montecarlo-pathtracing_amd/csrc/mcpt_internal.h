@@ -32,6 +32,8 @@ constexpr int kNodeF4 = 3;
 // inside each chunk of kPassChunk consecutive absolute pass numbers, chunk sums added to
 // the accumulator in chunk order
 constexpr int kPassChunk = 32;
+// largest scene render_kernel stages into LDS: 160 KB / 7 workgroups - 19 KB of per-pixel rows
+constexpr int kLdsSceneBytes = 3584;
 constexpr int kPrimF4 = 8;
 // MCPT_TRAVERSAL_AUTO picks the wave-coherent walk for BVHs up to this depth.  Since the
 // per-pixel state moved to LDS (7 waves/SIMD), the per-lane walk is faster on every
@@ -53,7 +55,8 @@ struct RenderParams {
   int band_rows, world, rank, n_local_rows;
   long long n_local_px;         // n_local_rows × W
   int n_tiles, n_segments;      // 16x16 tiles of the local rows; pass segments of this launch
-  int depth;
+  int depth, n_prims;
+  int lds_scene_bytes;          // > 0: stage the scene into LDS (<= kLdsSceneBytes, no meshes)
   // triangle meshes (mcpt_upload_meshes); n_meshes == 0: none
   const int4* minfo;
   const float4* mnodes;

@@ -60,9 +60,12 @@ enum { CODE_MESH = 0, CODE_SPHERE = 1, CODE_CUBE = 2, CODE_CYLINDER = 3, CODE_CO
 // ------------------------------------------------------------------------------------
 // MESH: the scene has triangle-mesh instances (CODE_MESH); a compile-time switch so scenes
 // without meshes do not pay the mesh code's registers.
-template <bool MESH>
+// LDS: the node / leaf / primitive arrays were staged into the workgroup's LDS (small
+// scenes; render_kernel): plain loads (ds_read), no constant-address-space casts.
+template <bool MESH, bool LDS = false>
 struct SceneT {
   static constexpr bool kMesh = MESH;
+  static constexpr bool kLds = LDS;
   const float4* __restrict__ nodes;   // 3 per node: (c, has-prim) (w, 0) (1/w, 0)
   const int* __restrict__ leaves;
   const int* __restrict__ ptype;      // type code | mesh id << 4
@@ -193,7 +196,8 @@ __device__ __forceinline__ void accept_cand(const SR& s, int index, int shape, i
                                             Hit& h, Ev<COUNT>& ev) {
   ev.inc(EV_CAND);
   const size_t b = (size_t)index * 8;
-  f3 Pg = xpoint(ld4<UNI>(s.prims, b + 3), ld4<UNI>(s.prims, b + 4), ld4<UNI>(s.prims, b + 5), Pl);
+  constexpr bool U = UNI && !SR::kLds;
+  f3 Pg = xpoint(ld4<U>(s.prims, b + 3), ld4<U>(s.prims, b + 4), ld4<U>(s.prims, b + 5), Pl);
   float dist = length3(sub(Ol, Pg));
   if (dist < h.dist) {
     h.dist = dist; h.pl = Pl; h.pg = Pg; h.index = index; h.shape = shape; h.dir = dir;
@@ -286,11 +290,12 @@ __device__ __forceinline__ void mesh_test(const SR& s, int mesh, int index, f3 O
 template <bool COUNT, bool UNI, bool ANY = false, class SR>
 __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit& h, Ev<COUNT>& ev) {
   ev.inc(EV_PRIM);
-  const int pt = ld1<UNI>(s.ptype, i);
+  constexpr bool U = UNI && !SR::kLds;
+  const int pt = ld1<U>(s.ptype, i);
   if (pt < 0) return;
   const int t = pt & 15;
   const size_t b = (size_t)i * 8;
-  float4 r0 = ld4<UNI>(s.prims, b), r1 = ld4<UNI>(s.prims, b + 1), r2 = ld4<UNI>(s.prims, b + 2);
+  float4 r0 = ld4<U>(s.prims, b), r1 = ld4<U>(s.prims, b + 1), r2 = ld4<U>(s.prims, b + 2);
   f3 O = xpoint(r0, r1, r2, Ow);
   f3 D = normalize3(xdir(r0, r1, r2, Dw));
   if (t == CODE_SPHERE) {
@@ -504,7 +509,7 @@ __device__ __forceinline__ void traverse_wave(const SR& s, f3 O, f3 D, Hit& h, E
     if (node >= leaf0) {
       if (act) {
         ev.inc(EV_LEAF);
-        int p = ld1<true>(s.leaves, node - leaf0);
+        int p = ld1<!SR::kLds>(s.leaves, node - leaf0);
         if (p >= 0) prim_test<COUNT, true>(s, p, O, D, h, ev);
       }
     } else {
@@ -512,12 +517,13 @@ __device__ __forceinline__ void traverse_wave(const SR& s, f3 O, f3 D, Hit& h, E
       bool hl = false, hr = false;
       if (act) {
         ev.inc(EV_NODE);
-        const float4 l0 = ld4<true>(s.nodes, j * 3), r0 = ld4<true>(s.nodes, j * 3 + 3);
+        constexpr bool U = !SR::kLds;
+        const float4 l0 = ld4<U>(s.nodes, j * 3), r0 = ld4<U>(s.nodes, j * 3 + 3);
         // empty subtrees (c.w == 0) are never visited (wave-uniform skip; see traverse_lane)
         if (COUNT || l0.w != 0.0f)
-          hl = box_test<true>(l0, ld4<true>(s.nodes, j * 3 + 1), ld4<true>(s.nodes, j * 3 + 2), O, D, invD, h.cull2);
+          hl = box_test<true>(l0, ld4<U>(s.nodes, j * 3 + 1), ld4<U>(s.nodes, j * 3 + 2), O, D, invD, h.cull2);
         if (COUNT || r0.w != 0.0f)
-          hr = box_test<true>(r0, ld4<true>(s.nodes, j * 3 + 4), ld4<true>(s.nodes, j * 3 + 5), O, D, invD, h.cull2);
+          hr = box_test<true>(r0, ld4<U>(s.nodes, j * 3 + 4), ld4<U>(s.nodes, j * 3 + 5), O, D, invD, h.cull2);
       }
       const uint32_t bit = 1u << (level + 1);
       lpend = hl ? (lpend | bit) : (lpend & ~bit);
@@ -636,7 +642,10 @@ __device__ __forceinline__ int floordiv(int a, int b) { return (a >= 0) ? a / b 
 // pass range inside one accumulation chunk of kPassChunk absolute passes:
 // segments of one pixel are independent items (strong-scaling parallelism beyond one
 // lane per pixel); their sums are combined in chunk order by combine_kernel.
-template <bool COUNT, bool WAVE, bool MESH>
+// LDSS: the scene (nodes, primitive records, leaves, type codes: RenderParams::lds_scene_bytes
+// <= kLdsSceneBytes) is copied into the workgroup's LDS first, so the traversal's dependent
+// node loads are LDS reads instead of L1/L2 gathers.
+template <bool COUNT, bool WAVE, bool MESH, bool LDSS>
 __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParams p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -645,16 +654,32 @@ __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParam
   const int tiles_x = (p.W + 15) >> 4;
   const int x = (tile % tiles_x) * 16 + (wave & 1) * 8 + (lane & 7);
   const int lr = (tile / tiles_x) * 16 + (wave >> 1) * 8 + (lane >> 3);
-  if (x >= p.W || lr >= p.n_local_rows) return;
+  const bool live = x < p.W && lr < p.n_local_rows;   // (no early return: LDS staging barrier)
   const int c0 = floordiv(p.first_pass - 1, kPassChunk) + seg;
   const int pass_begin = max(p.first_pass, c0 * kPassChunk + 1);
   const int pass_end = min(p.first_pass + p.n_passes, (c0 + 1) * kPassChunk + 1);
   const int y = ((lr / p.band_rows) * p.world + p.rank) * p.band_rows + (lr % p.band_rows);
 
-  SceneT<MESH> s{p.nodes, p.leaves, p.ptype, p.prims, p.depth, p.minfo, p.mnodes, p.mleaves, p.mtris, p.mverts,
-                 p.mnorms, p.flat_face};
+  SceneT<MESH, LDSS> s{p.nodes, p.leaves, p.ptype, p.prims, p.depth, p.minfo, p.mnodes, p.mleaves, p.mtris,
+                       p.mverts, p.mnorms, p.flat_face};
+  if constexpr (LDSS) {
+    // staged layout: nodes (3 float4 each), prims (8 float4 each), leaves, type codes
+    extern __shared__ float4 s_scene[];
+    const int n_nodes = (2 << p.depth) - 1, n_leaves = 1 << p.depth;
+    const int n4 = 3 * n_nodes + 8 * p.n_prims;
+    for (int i = tid; i < n4; i += 256) s_scene[i] = i < 3 * n_nodes ? p.nodes[i] : p.prims[i - 3 * n_nodes];
+    int* s_int = (int*)(s_scene + n4);
+    for (int i = tid; i < n_leaves + p.n_prims; i += 256)
+      s_int[i] = i < n_leaves ? p.leaves[i] : p.ptype[i - n_leaves];
+    __syncthreads();
+    s.nodes = s_scene;
+    s.prims = s_scene + 3 * n_nodes;
+    s.leaves = s_int;
+    s.ptype = s_int + n_leaves;
+  }
   Ev<COUNT> ev;
   ev.init();
+  if (!live) return;
 
   // raytracer.vert:9-22 corner rays, interpolated over the strip (v0,v1,v2) / (v1,v3,v2)
   const float u = ((float)x + 0.5f) / (float)p.W;
@@ -673,15 +698,15 @@ __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParam
   }
   // Per-pixel constants live in LDS (SoA by thread: conflict-free), not in VGPRs: the
   // camera direction and the cached primary hit are read once per pass, and keeping them
-  // out of the register file is what lets 6 waves/SIMD fit with fewer spills.
-  // rows: 0-2 Dcam, 3-5 N0, 6-8 P0 (primary hit), 9-11 N / 17-19 P saved across the inner
-  // traversal, 12-14 this segment's sum (from 0 in pass order), 15-16 screen_tc
-  __shared__ float s_pix[20][256];
-  __shared__ int s_hit0[2][256];     // primary hit shape, index
+  // out of the register file is what lets 7 waves/SIMD fit.  rows: 0-2 Dcam, 3-5 N0, 6-8 P0
+  // (primary hit), 9-11 N / 15-17 P saved across the inner traversal, 12-14 this segment's
+  // sum (from 0 in pass order); s_hit0 = primary hit shape << 28 | index (-1: miss).
+  // 19 KB per workgroup, + the staged scene (LDSS, <= kLdsSceneBytes): 7 workgroups/CU.
+  __shared__ float s_pix[18][256];
+  __shared__ int s_hit0[256];
   const f3 Dcam0 = normalize3(dir);
   s_pix[0][tid] = Dcam0.x; s_pix[1][tid] = Dcam0.y; s_pix[2][tid] = Dcam0.z;
   s_pix[12][tid] = 0.0f; s_pix[13][tid] = 0.0f; s_pix[14][tid] = 0.0f;   // this segment's sum
-  s_pix[15][tid] = u; s_pix[16][tid] = v;
   const f3 Ocam = mk(p.ox, p.oy, p.oz);
 
 
@@ -717,7 +742,7 @@ __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParam
   }
   s_pix[3][tid] = N0.x; s_pix[4][tid] = N0.y; s_pix[5][tid] = N0.z;
   s_pix[6][tid] = P0.x; s_pix[7][tid] = P0.y; s_pix[8][tid] = P0.z;
-  s_hit0[0][tid] = shape0; s_hit0[1][tid] = idx0;
+  s_hit0[tid] = shape0 < 0 ? -1 : (shape0 << 28) | idx0;   // idx0 < 2^28 (mcpt_upload_scene)
 
 #ifdef MCPT_STAMPS
   const unsigned long long st_p = __builtin_amdgcn_s_memtime() - st_k0;
@@ -733,7 +758,11 @@ __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParam
     if (!run) {
       done = true;   // for(i=0; i<NB_BOUNCES ...) never runs: black
     } else {
-      if (first) { h.shape = s_hit0[0][tid]; h.index = s_hit0[1][tid]; }
+      if (first) {
+        const int hv = s_hit0[tid];
+        h.shape = hv < 0 ? -1 : hv >> 28;
+        h.index = hv < 0 ? -1 : hv & 0x0FFFFFFF;
+      }
       else traverse<COUNT, WAVE>(s, O, D, h, ev);
 #ifdef MCPT_STAMPS
       const unsigned long long st_b = __builtin_amdgcn_s_memtime();
@@ -825,7 +854,7 @@ __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParam
               // inner hit in LDS rather than across the traversal in registers
               phase = 1;
               s_pix[9][tid] = N.x; s_pix[10][tid] = N.y; s_pix[11][tid] = N.z;
-              s_pix[17][tid] = P.x; s_pix[18][tid] = P.y; s_pix[19][tid] = P.z;
+              s_pix[15][tid] = P.x; s_pix[16][tid] = P.y; s_pix[17][tid] = P.z;
             }
             else if (bounce >= B) done = true;   // budget exhausted: black (res = 0)
           } else {
@@ -839,7 +868,7 @@ __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParam
           geom_info<COUNT>(s, h, N, P, ev);
         } else {
           N = mk(s_pix[9][tid], s_pix[10][tid], s_pix[11][tid]);
-          P = mk(s_pix[17][tid], s_pix[18][tid], s_pix[19][tid]);
+          P = mk(s_pix[15][tid], s_pix[16][tid], s_pix[17][tid]);
         }
         O = add(P, muls(N, kBIAS));
         D = grefract(D, neg(N), 1.0f / ior);
@@ -854,7 +883,7 @@ __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParam
       s_pix[14][tid] = s_pix[14][tid] + res.z;
       ev.inc(EV_SAMPLE);
       pass++;
-      rng = seed_for(s_pix[15][tid], s_pix[16][tid], pass, p.date);
+      rng = seed_for(((float)x + 0.5f) / (float)p.W, ((float)y + 0.5f) / (float)p.H, pass, p.date);   // = (u, v)
       O = Ocam; D = mk(s_pix[0][tid], s_pix[1][tid], s_pix[2][tid]);
       att = mk(0.8f, 0.8f, 0.8f); total = mk(0.0f, 0.0f, 0.0f);
       bounce = 0; phase = 0;
@@ -996,14 +1025,19 @@ hipError_t mcpt_launch_render(const mcpt::RenderParams& p, bool count, hipStream
   if (items <= 0) return hipSuccess;
   dim3 block(256), grid((unsigned)items);
   const bool wave = p.wave_traversal != 0, mesh = p.n_meshes > 0;
-#define MCPT_RENDER(C, W, M) hipLaunchKernelGGL((mcpt::render_kernel<C, W, M>), grid, block, 0, stream, p)
+  const bool lds = !mesh && p.lds_scene_bytes > 0;
+  const size_t shm = lds ? (size_t)p.lds_scene_bytes : 0;
+#define MCPT_RENDER(C, W, M, L) hipLaunchKernelGGL((mcpt::render_kernel<C, W, M, L>), grid, block, shm, stream, p)
+#define MCPT_RENDER_CW(C, W)                  \
+  if (mesh) MCPT_RENDER(C, W, true, false);   \
+  else if (lds) MCPT_RENDER(C, W, false, true); \
+  else MCPT_RENDER(C, W, false, false)
   if (count) {
-    if (wave) { if (mesh) MCPT_RENDER(true, true, true); else MCPT_RENDER(true, true, false); }
-    else { if (mesh) MCPT_RENDER(true, false, true); else MCPT_RENDER(true, false, false); }
+    if (wave) { MCPT_RENDER_CW(true, true); } else { MCPT_RENDER_CW(true, false); }
   } else {
-    if (wave) { if (mesh) MCPT_RENDER(false, true, true); else MCPT_RENDER(false, true, false); }
-    else { if (mesh) MCPT_RENDER(false, false, true); else MCPT_RENDER(false, false, false); }
+    if (wave) { MCPT_RENDER_CW(false, true); } else { MCPT_RENDER_CW(false, false); }
   }
+#undef MCPT_RENDER_CW
 #undef MCPT_RENDER
   return hipGetLastError();
 }
