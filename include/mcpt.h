@@ -140,6 +140,13 @@ int mcpt_copy_accum_device(mcpt_ctx* ctx, void* dst_dev_ptr, size_t bytes);
 int mcpt_set_traversal(mcpt_ctx* ctx, int mode);
 int mcpt_get_traversal(mcpt_ctx* ctx, int* resolved_mode);
 
+/* Per-lane walks (MCPT_TRAVERSAL_LANE): the wave suspends its BVH walk loop once at most
+ * `lanes` lanes are still walking, shades the finished lanes and resumes the rest with
+ * their next rays (0 = never suspend; -1 = default: 8 for BVH depth >= 8, else 0).  Same
+ * results for every value; a scheduling knob.  mcpt_get_walk_exit reports the value used. */
+int mcpt_set_walk_exit(mcpt_ctx* ctx, int lanes);
+int mcpt_get_walk_exit(mcpt_ctx* ctx, int* resolved_lanes);
+
 /* Ray queries on the uploaded scene — the shader library calls a TP integrator may use
  * (raytracer_func.frag:718-781, 874-907): traverse_all_bvh (any_hit = 0) or just_hit_bvh
  * (any_hit = 1: stop at the first primitive hit), or with prim >= 0 intersect_one_prim /

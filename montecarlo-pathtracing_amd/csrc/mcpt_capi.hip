@@ -64,7 +64,16 @@ struct mcpt_ctx {
   hipEvent_t ev_start = nullptr, ev_mid = nullptr, ev_stop = nullptr;
   bool timed = false;
   int traversal = MCPT_TRAVERSAL_AUTO;
+  int walk_exit = -1;               // mcpt_set_walk_exit; -1: by BVH depth
 };
+
+// per-lane walks leave the traversal loop at <= this many walking lanes (walk_run): pays off
+// when traversals are long (deep BVHs: +34-43 % on scenes 3/7/8), costs extra shading rounds
+// when they are short (-15-30 % on scenes 1/2/6; scene 5, depth 7: -4 %)
+static int resolve_walk_exit(const mcpt_ctx* c) {
+  if (c->walk_exit >= 0) return c->walk_exit;
+  return c->depth >= 8 ? 8 : 0;
+}
 
 static int resolve_traversal(const mcpt_ctx* c) {
   if (c->traversal != MCPT_TRAVERSAL_AUTO) return c->traversal;
@@ -387,6 +396,7 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   p.minfo = c->d_minfo; p.mnodes = c->d_mnodes; p.mleaves = c->d_mleaves; p.mtris = c->d_mtris;
   p.mverts = c->d_mverts; p.mnorms = c->d_mnorms; p.n_meshes = c->n_meshes; p.flat_face = c->flat_face;
   p.wave_traversal = (resolve_traversal(c) == MCPT_TRAVERSAL_WAVE) ? 1 : 0;
+  p.walk_exit = resolve_walk_exit(c);
   p.first_pass = first_pass; p.n_passes = n_passes; p.bounces = bounces; p.variant = variant;
   p.date = date; p.ior = refract_ind;
   p.n_local_px = (long long)c->n_local_rows * c->W;
@@ -547,6 +557,18 @@ int mcpt_set_traversal(mcpt_ctx* c, int mode) {
   if (!c || mode < MCPT_TRAVERSAL_AUTO || mode > MCPT_TRAVERSAL_WAVE)
     return set_err(MCPT_ERR_INVALID_ARG, "mcpt_set_traversal: bad mode");
   c->traversal = mode;
+  return MCPT_OK;
+}
+
+int mcpt_set_walk_exit(mcpt_ctx* c, int lanes) {
+  if (!c || lanes < -1 || lanes > 64) return set_err(MCPT_ERR_INVALID_ARG, "mcpt_set_walk_exit: bad lane count");
+  c->walk_exit = lanes;
+  return MCPT_OK;
+}
+
+int mcpt_get_walk_exit(mcpt_ctx* c, int* resolved) {
+  if (!c || !resolved) return MCPT_ERR_INVALID_ARG;
+  *resolved = resolve_walk_exit(c);
   return MCPT_OK;
 }
 

@@ -66,6 +66,7 @@ struct RenderParams {
   const float4* mnorms;
   int n_meshes, flat_face;
   int wave_traversal;           // 1: wave-coherent BVH walk (traverse_wave), 0: per lane
+  int walk_exit;                // per-lane walks: leave the loop at <= this many walking lanes
   int first_pass, n_passes, bounces, variant;
   float date, ior;
 };

@@ -32,6 +32,7 @@
 #define MCPT_MIN_WAVES 7
 #endif
 
+
 namespace mcpt {
 
 struct Hit {
@@ -111,6 +112,7 @@ struct Ev {
   Counters c;
 #ifdef MCPT_STAMPS
   unsigned long long st_leaf = 0;   // diagnostic: wave-cycles in the traversal's leaf blocks
+  unsigned long long st_lit = 0, st_wit = 0;   // traversal loop: lane iterations, wave iterations
 #endif
   __device__ __forceinline__ void init() { if (COUNT) for (int i = 0; i < EV_COUNT; ++i) c.v[i] = 0; }
   __device__ __forceinline__ void inc(int e) { if (COUNT) c.v[e]++; }
@@ -410,6 +412,8 @@ __device__ __forceinline__ void traverse_lane(const SR& s, f3 O, f3 D, Hit& h, E
     }
 #ifdef MCPT_STAMPS
     ev.st_leaf += __builtin_amdgcn_s_memtime() - t0;
+    ev.st_lit++;
+    ev.st_wit += (int)__lane_id() == __builtin_ffsll((long long)__ballot(1)) - 1;
 #endif
     if (!is_leaf) {
       ev.inc(EV_NODE);
@@ -433,6 +437,74 @@ __device__ __forceinline__ void traverse_lane(const SR& s, f3 O, f3 D, Hit& h, E
       pending &= ~(1u << L);
       node = ((node + 1) >> (level - L)) - 2;
       level = L;
+    }
+  }
+}
+
+// Resumable form of traverse_lane for the render loop.  The wave leaves the traversal loop
+// once at most `exit` lanes are still walking (and at least one lane finished in this call):
+// the finished lanes shade and start their next ray while the stragglers keep their walk
+// state (node, level, pending, invD, hit record) and continue in the next round.  Each
+// lane's own sequence of visits is traverse_lane's; only the interleaving changes.
+struct Walk {
+  f3 invD;
+  int node, level;
+  uint32_t pending;
+};
+
+template <bool COUNT, class SR>
+__device__ __forceinline__ void walk_begin(const SR& s, f3 D, Hit& h, Walk& w, Ev<COUNT>& ev) {
+  ev.inc(EV_TRAV);
+  h.index = -1; h.dist = kFLTMAX; h.shape = -1; h.dir = -1; h.cull2 = cull_bound_sq(kFLTMAX);
+  w.invD = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);
+  w.node = 0; w.level = 0; w.pending = 0;
+}
+
+// true: this lane's walk is complete; false: suspended (wave-level early exit)
+template <bool COUNT, bool SUSPEND, class SR>
+__device__ __forceinline__ bool walk_run(const SR& s, f3 O, f3 D, Hit& h, Walk& w, Ev<COUNT>& ev, int exit) {
+  const int leaf0 = (1 << s.depth) - 1;
+  const int n0 = SUSPEND ? __builtin_popcountll(__ballot(1)) : 0;
+  for (;;) {
+    bool pop = true;
+    const bool is_leaf = w.node >= leaf0;
+#ifdef MCPT_STAMPS
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();   // wave-uniform stamps
+#endif
+    if (is_leaf) {
+      ev.inc(EV_LEAF);
+      int p = s.leaves[w.node - leaf0];
+      if (p >= 0) prim_test<COUNT, false, false>(s, p, O, D, h, ev);
+    }
+#ifdef MCPT_STAMPS
+    ev.st_leaf += __builtin_amdgcn_s_memtime() - t0;
+    ev.st_lit++;
+    ev.st_wit += (int)__lane_id() == __builtin_ffsll((long long)__ballot(1)) - 1;
+#endif
+    if (!is_leaf) {
+      ev.inc(EV_NODE);
+      const size_t j = 2 * (size_t)w.node + 1;
+      const float4 l0 = s.nodes[j * 3], r0 = s.nodes[j * 3 + 3];
+      bool hl = (COUNT || l0.w != 0.0f) && box_test<false>(l0, s.nodes[j * 3 + 1], s.nodes[j * 3 + 2], O, D, w.invD, h.cull2);
+      bool hr = (COUNT || r0.w != 0.0f) && box_test<false>(r0, s.nodes[j * 3 + 4], s.nodes[j * 3 + 5], O, D, w.invD, h.cull2);
+      pop = !(hl || hr);
+      if (hr) {
+        if (hl) w.pending |= 1u << (w.level + 1);
+        w.node = (int)j + 1; w.level++;
+      } else if (hl) {
+        w.node = (int)j; w.level++;
+      }
+    }
+    if (pop) {
+      if (w.pending == 0) return true;
+      int L = 31 - __builtin_clz(w.pending);
+      w.pending &= ~(1u << L);
+      w.node = ((w.node + 1) >> (w.level - L)) - 2;
+      w.level = L;
+    }
+    if (SUSPEND) {   // wave-uniform
+      const int n = __builtin_popcountll(__ballot(1));
+      if (n <= exit && n < n0) return false;
     }
   }
 }
@@ -645,7 +717,8 @@ __device__ __forceinline__ int floordiv(int a, int b) { return (a >= 0) ? a / b 
 // LDSS: the scene (nodes, primitive records, leaves, type codes: RenderParams::lds_scene_bytes
 // <= kLdsSceneBytes) is copied into the workgroup's LDS first, so the traversal's dependent
 // node loads are LDS reads instead of L1/L2 gathers.
-template <bool COUNT, bool WAVE, bool MESH, bool LDSS>
+// SUSPEND: per-lane walks may be suspended (RenderParams::walk_exit > 0; walk_run)
+template <bool COUNT, bool WAVE, bool MESH, bool LDSS, bool SUSPEND>
 __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParams p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -747,6 +820,9 @@ __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParam
 #ifdef MCPT_STAMPS
   const unsigned long long st_p = __builtin_amdgcn_s_memtime() - st_k0;
 #endif
+  Walk walk;
+  walk.invD = mk(0.0f, 0.0f, 0.0f); walk.node = 0; walk.level = 0; walk.pending = 0;
+  bool walking = false;   // a suspended per-lane walk is waiting to be continued
   while (pass < pass_end) {
 #ifdef MCPT_STAMPS
     const unsigned long long st_a = __builtin_amdgcn_s_memtime();
@@ -755,6 +831,7 @@ __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParam
     bool done = false;
     f3 res = mk(0.0f, 0.0f, 0.0f);
     const bool first = !COUNT && bounce == 0 && phase == 0;   // camera ray of this pass
+    bool ready = true;   // this lane's hit record is complete
     if (!run) {
       done = true;   // for(i=0; i<NB_BOUNCES ...) never runs: black
     } else {
@@ -762,13 +839,20 @@ __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParam
         const int hv = s_hit0[tid];
         h.shape = hv < 0 ? -1 : hv >> 28;
         h.index = hv < 0 ? -1 : hv & 0x0FFFFFFF;
+      } else if (WAVE) {
+        traverse<COUNT, WAVE>(s, O, D, h, ev);
+      } else {
+        if (!walking) { walk_begin<COUNT>(s, D, h, walk, ev); walking = true; }
+        walking = !walk_run<COUNT, SUSPEND>(s, O, D, h, walk, ev, p.walk_exit);
+        ready = !walking;
       }
-      else traverse<COUNT, WAVE>(s, O, D, h, ev);
+    }
 #ifdef MCPT_STAMPS
-      const unsigned long long st_b = __builtin_amdgcn_s_memtime();
-      st_t += st_b - st_a;
-      st_s -= st_b;
+    const unsigned long long st_b = __builtin_amdgcn_s_memtime();
+    st_t += st_b - st_a;
+    st_s -= st_b;
 #endif
+    if (ready && run) {
       if (p.variant != 0) {
         // tp/montecarlo_mat.frag:5-20 / montecarlo_mat_tr.frag:5-20
         if (h.shape < 0) {
@@ -889,23 +973,27 @@ __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParam
       bounce = 0; phase = 0;
     }
 #ifdef MCPT_STAMPS
-    if (run) st_s += __builtin_amdgcn_s_memtime();
+    st_s += __builtin_amdgcn_s_memtime();
 #endif
   }
 #ifdef MCPT_STAMPS
   {
     // wave totals = the last-finishing lane's sums (max over lanes); lane-iterations summed
     unsigned long long vals[6] = {__builtin_amdgcn_s_memtime() - st_k0, st_p, st_t, st_s, st_it, ev.st_leaf};
-    unsigned long long it_sum = st_it;
+    unsigned long long it_sum = st_it, lit = ev.st_lit, wit = ev.st_wit;
     for (int off = 32; off > 0; off >>= 1) {
       for (int k = 0; k < 6; ++k) { unsigned long long o = __shfl_xor(vals[k], off); vals[k] = vals[k] > o ? vals[k] : o; }
       it_sum += __shfl_xor(it_sum, off);
+      lit += __shfl_xor(lit, off);
+      wit += __shfl_xor(wit, off);
     }
     if (lane == 0 && p.events) {
       for (int k = 0; k < 5; ++k) atomicAdd(p.events + k, vals[k]);
       atomicAdd(p.events + 5, it_sum);
       atomicAdd(p.events + 6, 1ull);
       atomicAdd(p.events + 7, vals[5]);
+      atomicAdd(p.events + 9, lit);
+      atomicAdd(p.events + 10, wit);
     }
   }
 #endif
@@ -1026,16 +1114,22 @@ hipError_t mcpt_launch_render(const mcpt::RenderParams& p, bool count, hipStream
   dim3 block(256), grid((unsigned)items);
   const bool wave = p.wave_traversal != 0, mesh = p.n_meshes > 0;
   const bool lds = !mesh && p.lds_scene_bytes > 0;
+  const bool susp = !count && !wave && p.walk_exit > 0;
   const size_t shm = lds ? (size_t)p.lds_scene_bytes : 0;
-#define MCPT_RENDER(C, W, M, L) hipLaunchKernelGGL((mcpt::render_kernel<C, W, M, L>), grid, block, shm, stream, p)
-#define MCPT_RENDER_CW(C, W)                  \
-  if (mesh) MCPT_RENDER(C, W, true, false);   \
-  else if (lds) MCPT_RENDER(C, W, false, true); \
-  else MCPT_RENDER(C, W, false, false)
+#define MCPT_RENDER(C, W, M, L, S) \
+  hipLaunchKernelGGL((mcpt::render_kernel<C, W, M, L, S>), grid, block, shm, stream, p)
+#define MCPT_RENDER_CW(C, W, S)                       \
+  if (mesh) MCPT_RENDER(C, W, true, false, S);        \
+  else if (lds) MCPT_RENDER(C, W, false, true, S);    \
+  else MCPT_RENDER(C, W, false, false, S)
   if (count) {
-    if (wave) { MCPT_RENDER_CW(true, true); } else { MCPT_RENDER_CW(true, false); }
+    if (wave) { MCPT_RENDER_CW(true, true, false); } else { MCPT_RENDER_CW(true, false, false); }
+  } else if (wave) {
+    MCPT_RENDER_CW(false, true, false);
+  } else if (susp) {
+    MCPT_RENDER_CW(false, false, true);
   } else {
-    if (wave) { MCPT_RENDER_CW(false, true); } else { MCPT_RENDER_CW(false, false); }
+    MCPT_RENDER_CW(false, false, false);
   }
 #undef MCPT_RENDER_CW
 #undef MCPT_RENDER

@@ -88,6 +88,8 @@ def _declare(L: ctypes.CDLL) -> None:
         "mcpt_trace": (i, [_vp, fp, fp, i, i, i, _vp]),
         "mcpt_sample_hemisphere": (i, [_vp, fp, fp, f, i, i, fp]),
         "mcpt_get_traversal": (i, [_vp, ip]),
+        "mcpt_set_walk_exit": (i, [_vp, i]),
+        "mcpt_get_walk_exit": (i, [_vp, ip]),
         "mcpt_set_stream": (i, [_vp, _vp]),
         "mcpt_synchronize": (i, [_vp]),
         "mcpt_last_render_ms": (i, [_vp, fp]),
@@ -521,6 +523,15 @@ class Renderer:
     def set_traversal(self, mode: int) -> None:
         """BVH traversal strategy: TRAVERSAL_AUTO / _LANE / _WAVE (same results)."""
         _check(lib().mcpt_set_traversal(self._h, int(mode)), "mcpt_set_traversal")
+
+    def set_walk_exit(self, lanes: int) -> None:
+        """mcpt_set_walk_exit: suspend per-lane walks at <= lanes walking lanes (-1: default)."""
+        _check(lib().mcpt_set_walk_exit(self._h, int(lanes)), "mcpt_set_walk_exit")
+
+    def walk_exit(self) -> int:
+        n = ctypes.c_int()
+        _check(lib().mcpt_get_walk_exit(self._h, ctypes.byref(n)), "mcpt_get_walk_exit")
+        return n.value
 
     def traversal(self) -> int:
         """The strategy AUTO resolves to for the uploaded scene."""

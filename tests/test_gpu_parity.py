@@ -197,3 +197,19 @@ def test_sharded_renderer_single_rank(mcpt_mod):
     acc, _ = sr.r.read_accum()
     sr.close()
     assert np.array_equal(frame.cpu().numpy().view(np.uint32), acc.view(np.uint32))
+
+
+@pytest.mark.parametrize("walk_exit", [0, 8, 40])
+@pytest.mark.parametrize("scene_id,B,variant,ior", [(6, 8, 0, 1.5), (3, 8, 0, 1.0), (2, 5, 0, 1.3), (6, 4, 2, 1.0)])
+def test_walk_exit_parity(mcpt_mod, oracle_mod, renderer, walk_exit, scene_id, B, variant, ior):
+    """Suspended per-lane walks (mcpt_set_walk_exit) change only the interleaving: bit-exact."""
+    W, H, S = 48, 40, 5
+    renderer.set_walk_exit(walk_exit)
+    try:
+        gpu = _gpu(mcpt_mod, renderer, scene_id, W, H, 3, S, B, ior=ior, variant=variant, traversal=1)
+        assert renderer.walk_exit() == walk_exit
+    finally:
+        renderer.set_walk_exit(-1)
+    ref, _ = _oracle(oracle_mod, scene_id, W, H, 3, S, B, ior=ior, variant=variant)
+    _compare(gpu, ref, f"scene {scene_id} walk_exit {walk_exit}")
+

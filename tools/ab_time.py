@@ -32,14 +32,17 @@ def main():
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--tag", default=os.path.basename(mcpt.lib_path()))
+    ap.add_argument("--walk-exit", type=int, nargs="+", default=[-1])
     a = ap.parse_args()
     r = mcpt.Renderer(0)
     r.set_target(a.width, a.height)
     ipv, iv = mcpt.camera_canonical(a.width, a.height)
     for sid in a.scenes:
         r.upload_scene(mcpt.Scene.reference(sid))
-        for mode in a.modes:
+        for mode, wx in [(m, w) for m in a.modes for w in (a.walk_exit if m == 1 else [-1])]:
             r.set_traversal(mode)
+            if hasattr(r, "set_walk_exit"):
+                r.set_walk_exit(wx)
             B = BOUNCES[sid]
             r.render(ipv, iv, 1, a.spp, 0.0, B, 1.0, 0)   # warm-up
             ms = []
@@ -47,7 +50,7 @@ def main():
                 r.render(ipv, iv, 1 + (k + 1) * a.spp, a.spp, 0.0, B, 1.0, 0)
                 ms.append(r.last_kernel_ms()[0])
             t = float(np.mean(ms))
-            print(json.dumps({"lib": a.tag, "scene": sid, "mode": mode, "bounces": B, "spp": a.spp,
+            print(json.dumps({"lib": a.tag, "scene": sid, "mode": mode, "walk_exit": wx, "bounces": B, "spp": a.spp,
                               "kernel_ms": round(t, 3),
                               "msamples_s": round(a.width * a.height * a.spp / t / 1e3, 1)}), flush=True)
     r.close()
