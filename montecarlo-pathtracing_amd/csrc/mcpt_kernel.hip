@@ -35,6 +35,25 @@
 
 namespace mcpt {
 
+// math inside the BVH walk loop (primitive tests): the short exact sequences of mcpt_math.h or
+// the generic IEEE expansions (same results).  Generic: the short sequences' fallback
+// branches inside the walk loop cost the deep-BVH kernels registers (-6..-9 % on scenes
+// 3/7/8) and buy nothing measurable on scene 6 (profiles/r01_ab19_fast_math.jsonl)
+#ifndef MCPT_WALK_FAST_MATH
+#define MCPT_WALK_FAST_MATH 0
+#endif
+#if MCPT_WALK_FAST_MATH
+__device__ __forceinline__ f3 wnormalize3(f3 a) { return normalize3(a); }
+__device__ __forceinline__ float wlength3(f3 a) { return length3(a); }
+__device__ __forceinline__ float wsqrt(float x) { return sqrt_rn(x); }
+__device__ __forceinline__ float wrcp(float x) { return rcp_rn(x); }
+#else
+__device__ __forceinline__ f3 wnormalize3(f3 a) { return normalize3_g(a); }
+__device__ __forceinline__ float wlength3(f3 a) { return length3_g(a); }
+__device__ __forceinline__ float wsqrt(float x) { return __builtin_sqrtf(x); }
+__device__ __forceinline__ float wrcp(float x) { return 1.0f / x; }
+#endif
+
 struct Hit {
   f3 pl, pg;
   float dist;
@@ -200,7 +219,7 @@ __device__ __forceinline__ void accept_cand(const SR& s, int index, int shape, i
   const size_t b = (size_t)index * 8;
   constexpr bool U = UNI && !SR::kLds;
   f3 Pg = xpoint(ld4<U>(s.prims, b + 3), ld4<U>(s.prims, b + 4), ld4<U>(s.prims, b + 5), Pl);
-  float dist = length3(sub(Ol, Pg));
+  float dist = wlength3(sub(Ol, Pg));
   if (dist < h.dist) {
     h.dist = dist; h.pl = Pl; h.pg = Pg; h.index = index; h.shape = shape; h.dir = dir;
     h.cull2 = cull_bound_sq(dist);
@@ -220,7 +239,7 @@ __device__ __forceinline__ void tri_test(const SR& s, int tri_base, int t, int i
   const f3 hv = cross3(D, edge2);
   const float det = dot3(edge1, hv);
   if (__builtin_fabsf(det) < kEPS) return;
-  const float invdet = 1.0f / det;
+  const float invdet = wrcp(det);
   const f3 sv = sub(O, vA);
   const float u = dot3(sv, hv) * invdet;
   if (u < 0.0f || u > 1.0f) return;
@@ -231,7 +250,7 @@ __device__ __forceinline__ void tri_test(const SR& s, int tri_base, int t, int i
   if (a > kEPS) {
     const f3 Pl = add(O, muls(D, a));
     const f3 Pg = xpoint(t0, t1, t2, Pl);
-    const float dist = length3(sub(Ol, Pg));
+    const float dist = wlength3(sub(Ol, Pg));
     if (dist < h.dist) {
       h.dist = dist; h.pl = Pl; h.pg = Pg; h.index = index; h.shape = CODE_MESH; h.dir = t;
       h.cull2 = cull_bound_sq(dist);
@@ -249,7 +268,7 @@ __device__ __forceinline__ void mesh_test(const SR& s, int mesh, int index, f3 O
   const size_t b = (size_t)index * 8;
   const float4 t0 = s.prims[b + 3], t1 = s.prims[b + 4], t2 = s.prims[b + 5];   // read_mesh_transfo
   const float4* nodes = s.mnodes + (size_t)mi.x * 3;
-  const f3 invD = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);
+  const f3 invD = mk(rcp_rn(D.x), rcp_rn(D.y), rcp_rn(D.z));
   const int leaf0 = (1 << mi.z) - 1;
   int node = 0, level = 0;
   uint32_t pending = 0;
@@ -299,12 +318,12 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
   const size_t b = (size_t)i * 8;
   float4 r0 = ld4<U>(s.prims, b), r1 = ld4<U>(s.prims, b + 1), r2 = ld4<U>(s.prims, b + 2);
   f3 O = xpoint(r0, r1, r2, Ow);
-  f3 D = normalize3(xdir(r0, r1, r2, Dw));
+  f3 D = wnormalize3(xdir(r0, r1, r2, Dw));
   if (t == CODE_SPHERE) {
     float OO = dot3(O, O), OD = dot3(O, D), D2 = dot3(D, D);
     float delta4 = OD * OD - D2 * (OO - 1.0f);
     if (delta4 > 0.0f) {
-      float sq = __builtin_sqrtf(delta4);
+      float sq = wsqrt(delta4);
       float a = -(OD + sq) / D2;
       if (a > kEPS) accept_cand<COUNT, UNI>(s, i, CODE_SPHERE, 0, add(O, muls(D, a)), Ow, h, ev);
       a = -(OD - sq) / D2;
@@ -349,7 +368,7 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
     float D2 = __builtin_fmaf(D.y, D.y, D.x * D.x);
     float delta4 = OD * OD - D2 * (O2 - 1.0f);
     if (delta4 > 0.0f) {
-      float a = -(OD + __builtin_sqrtf(delta4)) / D2;
+      float a = -(OD + wsqrt(delta4)) / D2;
       if ((a > kEPS) && (a < al)) {
         float z = O.z + a * D.z;
         if (__builtin_fabsf(z) < 1.0f) { cl = 2; al = a; }
@@ -371,7 +390,7 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
     float cc = co.z * co.z - dot3(co, co) * 0.8f;
     float det = b * b - (4.0f * a) * cc;
     if (det > 0.0f) {
-      det = __builtin_sqrtf(det);
+      det = wsqrt(det);
       float t1 = (-b - det) / (2.0f * a);
       if (__builtin_fabsf(O.z + t1 * D.z) > 1.0f) t1 = kFLTMAX;
       float t2 = (-b + det) / (2.0f * a);
@@ -394,7 +413,7 @@ template <bool COUNT, bool ANY = false, class SR>
 __device__ __forceinline__ void traverse_lane(const SR& s, f3 O, f3 D, Hit& h, Ev<COUNT>& ev) {
   ev.inc(EV_TRAV);
   h.index = -1; h.dist = kFLTMAX; h.shape = -1; h.dir = -1; h.cull2 = cull_bound_sq(kFLTMAX);
-  const f3 invD = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);
+  const f3 invD = mk(rcp_rn(D.x), rcp_rn(D.y), rcp_rn(D.z));
   const int leaf0 = (1 << s.depth) - 1;
   int node = 0, level = 0;
   uint32_t pending = 0;
@@ -456,7 +475,7 @@ template <bool COUNT, class SR>
 __device__ __forceinline__ void walk_begin(const SR& s, f3 D, Hit& h, Walk& w, Ev<COUNT>& ev) {
   ev.inc(EV_TRAV);
   h.index = -1; h.dist = kFLTMAX; h.shape = -1; h.dir = -1; h.cull2 = cull_bound_sq(kFLTMAX);
-  w.invD = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);
+  w.invD = mk(rcp_rn(D.x), rcp_rn(D.y), rcp_rn(D.z));
   w.node = 0; w.level = 0; w.pending = 0;
 }
 
@@ -518,7 +537,7 @@ template <bool COUNT, class SR>
 __device__ __forceinline__ void traverse_lane_ww(const SR& s, f3 O, f3 D, Hit& h, Ev<COUNT>& ev) {
   ev.inc(EV_TRAV);
   h.index = -1; h.dist = kFLTMAX; h.shape = -1; h.dir = -1; h.cull2 = cull_bound_sq(kFLTMAX);
-  const f3 invD = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);
+  const f3 invD = mk(rcp_rn(D.x), rcp_rn(D.y), rcp_rn(D.z));
   const int leaf0 = (1 << s.depth) - 1;
   int node = 0, level = 0;
   uint32_t pending = 0;
@@ -571,7 +590,7 @@ template <bool COUNT, class SR>
 __device__ __forceinline__ void traverse_wave(const SR& s, f3 O, f3 D, Hit& h, Ev<COUNT>& ev) {
   ev.inc(EV_TRAV);
   h.index = -1; h.dist = kFLTMAX; h.shape = -1; h.dir = -1; h.cull2 = cull_bound_sq(kFLTMAX);
-  const f3 invD = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);
+  const f3 invD = mk(rcp_rn(D.x), rcp_rn(D.y), rcp_rn(D.z));
   const int leaf0 = (1 << s.depth) - 1;
   uint32_t lpend = 0;    // bit L: this lane pushed the left child at level L of the cursor path
   bool act = true;       // this lane visits the cursor node
@@ -650,7 +669,7 @@ __device__ __forceinline__ void geom_info(const SR& s, const Hit& h, f3& N, f3& 
     if (h.dir == 1) { N = mk(0.0f, 0.0f, 0.0f); return; }
     if (h.dir == 0) q = mk(h.pl.x, h.pl.y, h.pl.z - 1.0f);
     else {
-      float lxy = __builtin_sqrtf(__builtin_fmaf(h.pl.y, h.pl.y, h.pl.x * h.pl.x));
+      float lxy = sqrt_rn(__builtin_fmaf(h.pl.y, h.pl.y, h.pl.x * h.pl.x));
       q = add(h.pl, mk(h.pl.x, h.pl.y, lxy / 2.0f));
     }
   } else if (h.shape == CODE_QUAD) {
@@ -687,8 +706,8 @@ __device__ __forceinline__ f3 random_ray(Rng& rng, f3 D, float roughness) {
   float alpha = roughness * roughness;
   float beta = (2.0f * kPI) * rnd(rng);
   float tanTheta2 = ((-alpha) * alpha) * mc_log(1.0f - rnd(rng));
-  float cosTheta = 1.0f / __builtin_sqrtf(1.0f + tanTheta2);
-  float sinTheta = __builtin_sqrtf(gmax(0.0f, 1.0f - cosTheta * cosTheta));
+  float cosTheta = rcp_rn(sqrt_rn(1.0f + tanTheta2));
+  float sinTheta = sqrt_rn(gmax(0.0f, 1.0f - cosTheta * cosTheta));
   float sb, cb;
   mc_sincos(beta, sb, cb);
   f3 sm = normalize3(mk(cb * sinTheta, sb * sinTheta, cosTheta));

@@ -6,7 +6,10 @@
 //   * IEEE-754 binary32, round-to-nearest, built with -ffp-contract=off;
 //   * dot products and matrix·vector products are explicit fmaf chains in
 //     component order (x, then y, then z, then the translation column);
-//   * sqrt and '/' are the correctly-rounded HIP defaults;
+//   * sqrt and '/' are correctly rounded: '/' the HIP default expansion, sqrt and the
+//     reciprocals 1/x through sqrt_rn / rcp_rn below, shorter sequences proven equal to the
+//     correctly rounded results by an exhaustive check of all 2^32 inputs on gfx950
+//     (tools/mathcheck, tests/test_gpu_mathcheck.py);
 //   * normalize(v) = v * (1/sqrt(dot(v,v)));
 //   * sin/cos/log/exp2/pow are the fixed polynomial algorithms below (GLSL leaves
 //     their precision to the driver; ours are ≤ a few ulp and reproducible);
@@ -26,9 +29,69 @@ __device__ __forceinline__ f3 mulv(f3 a, f3 b) { return mk(a.x * b.x, a.y * b.y,
 __device__ __forceinline__ f3 muls(f3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
 __device__ __forceinline__ f3 neg(f3 a) { return mk(-a.x, -a.y, -a.z); }
 
+// generic IEEE expansions, out of line: the rare slow paths of the short sequences below stay
+// out of the register allocation of the hot code
+__device__ __attribute__((noinline)) inline float sqrt_ieee(float x) { return __builtin_sqrtf(x); }
+__device__ __attribute__((noinline)) inline float rcp_ieee(float x) { return 1.0f / x; }
+
+// Short sequences for RN(sqrt(x)) and RN(1/x), checked against the correctly rounded results
+// on all 2^32 inputs (tools/mathcheck/exhaustive.hip, tests/test_gpu_mathcheck.py):
+//  * sqrt_core: the hardware root (~1 ulp) corrected by the signs of the exact residuals
+//    x - s'·s of its two neighbours (7 VALU vs 16): exact except for 0 < |x| < 2^-96;
+//  * rcp_core: the hardware reciprocal + one Newton step on the exact residual (3 VALU vs
+//    11): exact for 2^-126 <= |x| < 2^126.
+// The *_rn wrappers route the other inputs to the generic expansions, wave-uniformly.
+__device__ __forceinline__ float sqrt_core(float x) {
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float sd = __uint_as_float(__float_as_uint(s) - 1u), su = __uint_as_float(__float_as_uint(s) + 1u);
+  float r = s;
+  if (__builtin_fmaf(-sd, s, x) <= 0.0f) r = sd;
+  if (__builtin_fmaf(-su, s, x) > 0.0f) r = su;
+  return r;
+}
+__device__ __forceinline__ float rcp_core(float x) {
+  const float y = __builtin_amdgcn_rcpf(x);
+  return __builtin_fmaf(__builtin_fmaf(-x, y, 1.0f), y, y);
+}
+__device__ __forceinline__ bool sqrt_core_ok(float x) { return !(__builtin_fabsf(x) < 0x1p-96f) || x == 0.0f; }
+__device__ __forceinline__ bool rcp_core_ok(float x) {
+  const float ax = __builtin_fabsf(x);
+  return ax >= 0x1p-126f && ax < 0x1p126f;
+}
+__device__ __forceinline__ float sqrt_rn(float x) {
+  float r = sqrt_core(x);
+  const bool ok = sqrt_core_ok(x);
+  if (__builtin_expect(__ballot(!ok) != 0, 0)) {
+    if (!ok) r = sqrt_ieee(x);
+  }
+  return r;
+}
+__device__ __forceinline__ float rcp_rn(float x) {
+  float r = rcp_core(x);
+  const bool ok = rcp_core_ok(x);
+  if (__builtin_expect(__ballot(!ok) != 0, 0)) {
+    if (!ok) r = rcp_ieee(x);
+  }
+  return r;
+}
+// RN(1/RN(sqrt(x))), the factor of normalize: for 2^-96 <= x < 2^126 both cores are exact
+// (the root lies in [2^-48, 2^63)): one range test for the pair
+__device__ __forceinline__ float rsqrt_rn(float x) {
+  float r = rcp_core(sqrt_core(x));
+  const bool ok = x >= 0x1p-96f && x < 0x1p126f;
+  if (__builtin_expect(__ballot(!ok) != 0, 0)) {
+    if (!ok) r = rcp_ieee(sqrt_ieee(x));
+  }
+  return r;
+}
+
 __device__ __forceinline__ float dot3(f3 a, f3 b) { return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x)); }
-__device__ __forceinline__ f3 normalize3(f3 a) { float r = 1.0f / __builtin_sqrtf(dot3(a, a)); return muls(a, r); }
-__device__ __forceinline__ float length3(f3 a) { return __builtin_sqrtf(dot3(a, a)); }
+__device__ __forceinline__ f3 normalize3(f3 a) { return muls(a, rsqrt_rn(dot3(a, a))); }
+__device__ __forceinline__ float length3(f3 a) { return sqrt_rn(dot3(a, a)); }
+// the same with the generic expansions inline (for code inside the BVH walk loop, where the
+// short sequences' fallback branches cost more registers than they save instructions)
+__device__ __forceinline__ f3 normalize3_g(f3 a) { float r = 1.0f / __builtin_sqrtf(dot3(a, a)); return muls(a, r); }
+__device__ __forceinline__ float length3_g(f3 a) { return __builtin_sqrtf(dot3(a, a)); }
 __device__ __forceinline__ f3 cross3(f3 a, f3 b) {
   return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
@@ -42,7 +105,7 @@ __device__ __forceinline__ f3 grefract(f3 I, f3 N, float eta) {
   float d = dot3(N, I);
   float k = 1.0f - (eta * eta) * (1.0f - d * d);
   if (k < 0.0f) return mk(0.0f, 0.0f, 0.0f);
-  return sub(muls(I, eta), muls(N, eta * d + __builtin_sqrtf(k)));
+  return sub(muls(I, eta), muls(N, eta * d + sqrt_rn(k)));
 }
 
 // 3x4 affine rows (row r = (m[r], m[4+r], m[8+r], m[12+r]) of a column-major mat4)
