@@ -142,10 +142,16 @@ int mcpt_get_traversal(mcpt_ctx* ctx, int* resolved_mode);
 
 /* Per-lane walks (MCPT_TRAVERSAL_LANE): the wave suspends its BVH walk loop once at most
  * `lanes` lanes are still walking, shades the finished lanes and resumes the rest with
- * their next rays (0 = never suspend; -1 = default: 8 for BVH depth >= 8, else 0).  Same
+ * their next rays (0 = never suspend; -1 = default: 16 for BVH depth >= 8, else 0).  Same
  * results for every value; a scheduling knob.  mcpt_get_walk_exit reports the value used. */
 int mcpt_set_walk_exit(mcpt_ctx* ctx, int lanes);
 int mcpt_get_walk_exit(mcpt_ctx* ctx, int* resolved_lanes);
+
+/* Per-lane walks: run the primitive-test block only once at least `lanes` lanes wait on a
+ * leaf (or no lane can take a node step); others wait (0 = off: node and leaf blocks every
+ * iteration; -1 = default: 8 for BVH depth >= 8, else 0).  Same results for every value. */
+int mcpt_set_leaf_batch(mcpt_ctx* ctx, int lanes);
+int mcpt_get_leaf_batch(mcpt_ctx* ctx, int* resolved_lanes);
 
 /* Ray queries on the uploaded scene — the shader library calls a TP integrator may use
  * (raytracer_func.frag:718-781, 874-907): traverse_all_bvh (any_hit = 0) or just_hit_bvh

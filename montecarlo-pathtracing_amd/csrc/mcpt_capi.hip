@@ -9,6 +9,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <vector>
@@ -65,13 +66,24 @@ struct mcpt_ctx {
   bool timed = false;
   int traversal = MCPT_TRAVERSAL_AUTO;
   int walk_exit = -1;               // mcpt_set_walk_exit; -1: by BVH depth
+  int leaf_batch = -1;              // MCPT_LEAF_BATCH env (tuning); -1: default
 };
 
-// per-lane walks leave the traversal loop at <= this many walking lanes (walk_run): pays off
-// when traversals are long (deep BVHs: +34-43 % on scenes 3/7/8), costs extra shading rounds
-// when they are short (-15-30 % on scenes 1/2/6; scene 5, depth 7: -4 %)
+static int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return v ? std::atoi(v) : dflt;
+}
+
+// Deep-BVH walk (walk_run's SUSPEND kernel): suspend the walk loop at <= walk_exit walking
+// lanes and batch leaf visits (>= leaf_batch waiting lanes).  Both pay off when traversals
+// are long (depth >= 8: scenes 3/7/8 +63-76 % over v6, profiles/r01_ab21_leaf_batch.jsonl)
+// and cost extra rounds when they are short (scenes 1/2/6: -10-30 %), so they are off there.
 static int resolve_walk_exit(const mcpt_ctx* c) {
   if (c->walk_exit >= 0) return c->walk_exit;
+  return c->depth >= 8 ? 16 : 0;
+}
+static int resolve_leaf_batch(const mcpt_ctx* c) {
+  if (c->leaf_batch >= 0) return c->leaf_batch;
   return c->depth >= 8 ? 8 : 0;
 }
 
@@ -106,6 +118,7 @@ int mcpt_create(int device_ordinal, mcpt_ctx** out) {
   HIP_OR_RETURN(hipSetDevice(device_ordinal));
   mcpt_ctx* c = new (std::nothrow) mcpt_ctx();
   if (!c) return MCPT_ERR_INVALID_ARG;
+  c->leaf_batch = env_int("MCPT_LEAF_BATCH", -1);   // tuning hook (same results for any value)
   c->device = device_ordinal;
   hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&c->ev_start);
@@ -397,6 +410,7 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   p.mverts = c->d_mverts; p.mnorms = c->d_mnorms; p.n_meshes = c->n_meshes; p.flat_face = c->flat_face;
   p.wave_traversal = (resolve_traversal(c) == MCPT_TRAVERSAL_WAVE) ? 1 : 0;
   p.walk_exit = resolve_walk_exit(c);
+  p.leaf_batch = resolve_leaf_batch(c);
   p.first_pass = first_pass; p.n_passes = n_passes; p.bounces = bounces; p.variant = variant;
   p.date = date; p.ior = refract_ind;
   p.n_local_px = (long long)c->n_local_rows * c->W;
@@ -563,6 +577,18 @@ int mcpt_set_traversal(mcpt_ctx* c, int mode) {
 int mcpt_set_walk_exit(mcpt_ctx* c, int lanes) {
   if (!c || lanes < -1 || lanes > 64) return set_err(MCPT_ERR_INVALID_ARG, "mcpt_set_walk_exit: bad lane count");
   c->walk_exit = lanes;
+  return MCPT_OK;
+}
+
+int mcpt_set_leaf_batch(mcpt_ctx* c, int lanes) {
+  if (!c || lanes < -1 || lanes > 64) return set_err(MCPT_ERR_INVALID_ARG, "mcpt_set_leaf_batch: bad lane count");
+  c->leaf_batch = lanes;
+  return MCPT_OK;
+}
+
+int mcpt_get_leaf_batch(mcpt_ctx* c, int* resolved) {
+  if (!c || !resolved) return MCPT_ERR_INVALID_ARG;
+  *resolved = resolve_leaf_batch(c);
   return MCPT_OK;
 }
 

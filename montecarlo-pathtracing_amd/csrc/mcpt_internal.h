@@ -67,6 +67,7 @@ struct RenderParams {
   int n_meshes, flat_face;
   int wave_traversal;           // 1: wave-coherent BVH walk (traverse_wave), 0: per lane
   int walk_exit;                // per-lane walks: leave the loop at <= this many walking lanes
+  int leaf_batch;               // deep-BVH walk: run the leaf block once >= this many lanes wait
   int first_pass, n_passes, bounces, variant;
   float date, ior;
 };

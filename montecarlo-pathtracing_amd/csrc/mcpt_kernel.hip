@@ -479,28 +479,42 @@ __device__ __forceinline__ void walk_begin(const SR& s, f3 D, Hit& h, Walk& w, E
   w.node = 0; w.level = 0; w.pending = 0;
 }
 
-// true: this lane's walk is complete; false: suspended (wave-level early exit)
+// true: this lane's walk is complete; false: suspended (wave-level early exit).
+// SUSPEND (deep-BVH kernel) also batches leaf visits: an iteration runs either the leaf
+// block (for the lanes sitting on a leaf) or the node block (for the others), and the leaf
+// block only once at least `leaf_batch` lanes wait on a leaf or no lane can take a node step.
+// In the if/if loop nearly every iteration of a deep walk pays for both blocks (some lane
+// is always on a leaf); here a lane waits a few node iterations instead.  Each lane's own
+// visit sequence is unchanged (the cull reads its own hit record only).
 template <bool COUNT, bool SUSPEND, class SR>
-__device__ __forceinline__ bool walk_run(const SR& s, f3 O, f3 D, Hit& h, Walk& w, Ev<COUNT>& ev, int exit) {
+__device__ __forceinline__ bool walk_run(const SR& s, f3 O, f3 D, Hit& h, Walk& w, Ev<COUNT>& ev, int exit,
+                                         int leaf_batch) {
   const int leaf0 = (1 << s.depth) - 1;
   const int n0 = SUSPEND ? __builtin_popcountll(__ballot(1)) : 0;
   for (;;) {
     bool pop = true;
-    const bool is_leaf = w.node >= leaf0;
+    bool is_leaf = w.node >= leaf0;
+    bool do_leaf = is_leaf, do_node = !is_leaf;
+    if (SUSPEND && leaf_batch > 0) {   // wave-uniform choice of the block
+      const uint64_t on_leaf = __ballot(is_leaf), act = __ballot(1);
+      const bool leaves = __builtin_popcountll(on_leaf) >= leaf_batch || on_leaf == act;
+      do_leaf = leaves && is_leaf;
+      do_node = !leaves && !is_leaf;
+    }
 #ifdef MCPT_STAMPS
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();   // wave-uniform stamps
 #endif
-    if (is_leaf) {
+    if (do_leaf) {
       ev.inc(EV_LEAF);
       int p = s.leaves[w.node - leaf0];
       if (p >= 0) prim_test<COUNT, false, false>(s, p, O, D, h, ev);
     }
 #ifdef MCPT_STAMPS
     ev.st_leaf += __builtin_amdgcn_s_memtime() - t0;
-    ev.st_lit++;
+    ev.st_lit += do_leaf || do_node;
     ev.st_wit += (int)__lane_id() == __builtin_ffsll((long long)__ballot(1)) - 1;
 #endif
-    if (!is_leaf) {
+    if (do_node) {
       ev.inc(EV_NODE);
       const size_t j = 2 * (size_t)w.node + 1;
       const float4 l0 = s.nodes[j * 3], r0 = s.nodes[j * 3 + 3];
@@ -514,7 +528,7 @@ __device__ __forceinline__ bool walk_run(const SR& s, f3 O, f3 D, Hit& h, Walk& 
         w.node = (int)j; w.level++;
       }
     }
-    if (pop) {
+    if (pop && (do_leaf || do_node)) {
       if (w.pending == 0) return true;
       int L = 31 - __builtin_clz(w.pending);
       w.pending &= ~(1u << L);
@@ -736,7 +750,8 @@ __device__ __forceinline__ int floordiv(int a, int b) { return (a >= 0) ? a / b 
 // LDSS: the scene (nodes, primitive records, leaves, type codes: RenderParams::lds_scene_bytes
 // <= kLdsSceneBytes) is copied into the workgroup's LDS first, so the traversal's dependent
 // node loads are LDS reads instead of L1/L2 gathers.
-// SUSPEND: per-lane walks may be suspended (RenderParams::walk_exit > 0; walk_run)
+// SUSPEND: the deep-BVH walk (suspendable walks, batched leaf visits: RenderParams::walk_exit,
+// leaf_batch; walk_run)
 template <bool COUNT, bool WAVE, bool MESH, bool LDSS, bool SUSPEND>
 __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParams p) {
   const int tid = threadIdx.x;
@@ -862,7 +877,7 @@ __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParam
         traverse<COUNT, WAVE>(s, O, D, h, ev);
       } else {
         if (!walking) { walk_begin<COUNT>(s, D, h, walk, ev); walking = true; }
-        walking = !walk_run<COUNT, SUSPEND>(s, O, D, h, walk, ev, p.walk_exit);
+        walking = !walk_run<COUNT, SUSPEND>(s, O, D, h, walk, ev, p.walk_exit, p.leaf_batch);
         ready = !walking;
       }
     }
@@ -1133,7 +1148,8 @@ hipError_t mcpt_launch_render(const mcpt::RenderParams& p, bool count, hipStream
   dim3 block(256), grid((unsigned)items);
   const bool wave = p.wave_traversal != 0, mesh = p.n_meshes > 0;
   const bool lds = !mesh && p.lds_scene_bytes > 0;
-  const bool susp = !count && !wave && p.walk_exit > 0;
+  // deep-BVH walk kernel: suspendable walks and/or batched leaf visits (walk_run)
+  const bool susp = !count && !wave && (p.walk_exit > 0 || p.leaf_batch > 0);
   const size_t shm = lds ? (size_t)p.lds_scene_bytes : 0;
 #define MCPT_RENDER(C, W, M, L, S) \
   hipLaunchKernelGGL((mcpt::render_kernel<C, W, M, L, S>), grid, block, shm, stream, p)

@@ -90,6 +90,8 @@ def _declare(L: ctypes.CDLL) -> None:
         "mcpt_get_traversal": (i, [_vp, ip]),
         "mcpt_set_walk_exit": (i, [_vp, i]),
         "mcpt_get_walk_exit": (i, [_vp, ip]),
+        "mcpt_set_leaf_batch": (i, [_vp, i]),
+        "mcpt_get_leaf_batch": (i, [_vp, ip]),
         "mcpt_set_stream": (i, [_vp, _vp]),
         "mcpt_synchronize": (i, [_vp]),
         "mcpt_last_render_ms": (i, [_vp, fp]),
@@ -531,6 +533,15 @@ class Renderer:
     def walk_exit(self) -> int:
         n = ctypes.c_int()
         _check(lib().mcpt_get_walk_exit(self._h, ctypes.byref(n)), "mcpt_get_walk_exit")
+        return n.value
+
+    def set_leaf_batch(self, lanes: int) -> None:
+        """mcpt_set_leaf_batch: primitive-test block once >= lanes lanes wait on a leaf (-1: default)."""
+        _check(lib().mcpt_set_leaf_batch(self._h, int(lanes)), "mcpt_set_leaf_batch")
+
+    def leaf_batch(self) -> int:
+        n = ctypes.c_int()
+        _check(lib().mcpt_get_leaf_batch(self._h, ctypes.byref(n)), "mcpt_get_leaf_batch")
         return n.value
 
     def traversal(self) -> int:

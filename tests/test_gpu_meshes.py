@@ -19,7 +19,7 @@ def renderer(mcpt_mod):
     r.close()
 
 
-@pytest.mark.parametrize("flat,walk_exit", [(False, -1), (True, -1), (False, 12)])
+@pytest.mark.parametrize("flat,walk_exit", [(False, -1), (True, -1), (False, 12), (False, 0)])
 @pytest.mark.parametrize("traversal", [1, 2])
 def test_mesh_scene_render(mcpt_mod, oracle_mod, renderer, traversal, flat, walk_exit):
     sc = mesh_scene(mcpt_mod)
@@ -27,6 +27,7 @@ def test_mesh_scene_render(mcpt_mod, oracle_mod, renderer, traversal, flat, walk
     W, H, S, B = 64, 48, 3, 8
     renderer.set_traversal(traversal)
     renderer.set_walk_exit(walk_exit)
+    renderer.set_leaf_batch(4 if walk_exit == 0 else -1)
     renderer.set_flat_face(flat)
     renderer.upload_scene(sc)
     renderer.set_target(W, H)
@@ -35,6 +36,7 @@ def test_mesh_scene_render(mcpt_mod, oracle_mod, renderer, traversal, flat, walk
     gpu, n = renderer.read_accum()
     renderer.set_traversal(0)
     renderer.set_walk_exit(-1)
+    renderer.set_leaf_batch(-1)
     renderer.set_flat_face(False)
     mv = oracle_mod.MeshView(sc.mesh_buffers(), flat_face=flat)
     ref, _ = oracle_mod.render(prims, nodes, leaves, sc.depth(), ipv, iv, W, H, 1, S, 0.0, B, 1.2, 0, meshes=mv)

@@ -213,3 +213,20 @@ def test_walk_exit_parity(mcpt_mod, oracle_mod, renderer, walk_exit, scene_id, B
     ref, _ = _oracle(oracle_mod, scene_id, W, H, 3, S, B, ior=ior, variant=variant)
     _compare(gpu, ref, f"scene {scene_id} walk_exit {walk_exit}")
 
+
+@pytest.mark.parametrize("walk_exit,leaf_batch", [(0, 8), (16, 1), (16, 64), (24, 8), (0, 0)])
+@pytest.mark.parametrize("scene_id,B,ior", [(3, 8, 1.0), (8, 6, 1.5), (6, 8, 1.5)])
+def test_leaf_batch_parity(mcpt_mod, oracle_mod, renderer, walk_exit, leaf_batch, scene_id, B, ior):
+    """Batched leaf visits (mcpt_set_leaf_batch) with and without suspension: bit-exact."""
+    W, H, S = 40, 32, 3
+    renderer.set_walk_exit(walk_exit)
+    renderer.set_leaf_batch(leaf_batch)
+    try:
+        gpu = _gpu(mcpt_mod, renderer, scene_id, W, H, 7, S, B, ior=ior, traversal=1)
+        assert renderer.leaf_batch() == leaf_batch
+    finally:
+        renderer.set_walk_exit(-1)
+        renderer.set_leaf_batch(-1)
+    ref, _ = _oracle(oracle_mod, scene_id, W, H, 7, S, B, ior=ior)
+    _compare(gpu, ref, f"scene {scene_id} walk_exit {walk_exit} leaf_batch {leaf_batch}")
+
