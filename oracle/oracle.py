@@ -41,6 +41,9 @@ def lib() -> ctypes.CDLL:
         sigs = {
             "orc_scene_build": (_vp, [i, f]),
             "orc_scene_free": (None, [_vp]),
+            "orc_scene_new": (_vp, [f]),
+            "orc_scene_add": (i, [_vp, i, _fp, _fp]),
+            "orc_scene_finalize": (i, [_vp]),
             "orc_scene_n_prims": (i, [_vp]),
             "orc_scene_depth": (i, [_vp]),
             "orc_scene_n_emissive": (i, [_vp]),
@@ -90,6 +93,28 @@ def scene(scene_id: int, light_intensity: float = 1.2) -> Tuple[np.ndarray, np.n
     finally:
         L.orc_scene_free(h)
     return prims, nodes, leaves, d, ne
+
+
+def custom_scene(ops, light_intensity: float = 1.2):
+    """Build a scene from [(type 1..5, trf16 column-major, material7)] with the oracle's own
+    producer (scene.h add_* + finalize): (prims, nodes, leaves, depth, nb_emissive)."""
+    L = lib()
+    h = L.orc_scene_new(ctypes.c_float(light_intensity))
+    try:
+        for t, trf, mat in ops:
+            a = np.ascontiguousarray(trf, np.float32).reshape(16)
+            m = np.ascontiguousarray(mat, np.float32).reshape(7)
+            if L.orc_scene_add(h, int(t), P(a), P(m)) < 0:
+                raise ValueError(f"bad primitive type {t}")
+        L.orc_scene_finalize(h)
+        n, d = L.orc_scene_n_prims(h), L.orc_scene_depth(h)
+        prims = np.zeros((n, 64), np.float32)
+        nodes = np.zeros(((2 << d) - 1) * 6, np.float32)
+        leaves = np.zeros(1 << d, np.int32)
+        L.orc_scene_export(h, P(prims), P(nodes), P(leaves, _ip))
+        return prims, nodes, leaves, d, L.orc_scene_n_emissive(h)
+    finally:
+        L.orc_scene_free(h)
 
 
 def camera(W: int, H: int) -> Tuple[np.ndarray, np.ndarray]:
