@@ -45,7 +45,8 @@ enum mcpt_variant {
 
 /* BVH traversal strategy of the kernel (same results, different speed) */
 enum mcpt_traversal {
-  MCPT_TRAVERSAL_AUTO = 0,   /* wave-coherent for shallow BVHs, per lane otherwise */
+  MCPT_TRAVERSAL_AUTO = 0,   /* measured: the first two launches of >= 2^24 samples after a scene
+                                upload try LANE and WAVE, later launches use the faster */
   MCPT_TRAVERSAL_LANE = 1,   /* each lane walks its own DFS (divergent, vector loads) */
   MCPT_TRAVERSAL_WAVE = 2,   /* the wave walks the union of its lanes' DFS orders (scalar loads) */
 };
@@ -136,7 +137,8 @@ int mcpt_accum_device_ptr(mcpt_ctx* ctx, void** dev_ptr, size_t* bytes);
 int mcpt_copy_accum_device(mcpt_ctx* ctx, void* dst_dev_ptr, size_t bytes);
 
 /* Select the traversal strategy (mcpt_traversal) for later renders; default AUTO.
- * mcpt_get_traversal reports the strategy AUTO resolves to for the uploaded scene. */
+ * mcpt_get_traversal reports the strategy the next render uses (under AUTO: the trial mode
+ * until both were timed, then the faster one).  Every strategy gives the same bits. */
 int mcpt_set_traversal(mcpt_ctx* ctx, int mode);
 int mcpt_get_traversal(mcpt_ctx* ctx, int* resolved_mode);
 

@@ -65,6 +65,13 @@ struct mcpt_ctx {
   hipEvent_t ev_start = nullptr, ev_mid = nullptr, ev_stop = nullptr;
   bool timed = false;
   int traversal = MCPT_TRAVERSAL_AUTO;
+  // AUTO traversal: the first two sizeable launches after a scene upload run the per-lane and
+  // the wave-coherent walk once each (kernel time per sample from the launch events), later
+  // launches use the faster one (results are identical either way)
+  int tune_pending = 0;             // mode of the launch whose timing is not collected yet
+  double tune_samples = 0.0;        // samples of that launch
+  double tune_ns[3] = {0.0, 0.0, 0.0};   // ns per sample measured, by mode
+  int tune_choice = 0;              // resolved mode once both are measured
   int walk_exit = -1;               // mcpt_set_walk_exit; -1: by BVH depth
   int leaf_batch = -1;              // MCPT_LEAF_BATCH env (tuning); -1: default
 };
@@ -89,8 +96,32 @@ static int resolve_leaf_batch(const mcpt_ctx* c) {
 
 static int resolve_traversal(const mcpt_ctx* c) {
   if (c->traversal != MCPT_TRAVERSAL_AUTO) return c->traversal;
-  return (c->depth <= mcpt::kWaveMaxDepth) ? MCPT_TRAVERSAL_WAVE : MCPT_TRAVERSAL_LANE;
+  if (c->tune_choice) return c->tune_choice;
+  return c->tune_ns[MCPT_TRAVERSAL_LANE] > 0.0 ? MCPT_TRAVERSAL_WAVE : MCPT_TRAVERSAL_LANE;   // next trial
 }
+
+static void reset_tuning(mcpt_ctx* c) {
+  c->tune_pending = 0;
+  c->tune_samples = 0.0;
+  c->tune_ns[0] = c->tune_ns[1] = c->tune_ns[2] = 0.0;
+  c->tune_choice = 0;
+}
+
+// collect the timing of the last trial launch (waits for it), decide once both are measured
+static hipError_t collect_tuning(mcpt_ctx* c) {
+  if (!c->tune_pending || !c->timed) return hipSuccess;
+  float ms = 0.0f;
+  hipError_t e = hipEventSynchronize(c->ev_mid);
+  if (e == hipSuccess) e = hipEventElapsedTime(&ms, c->ev_start, c->ev_mid);
+  if (e != hipSuccess) return e;
+  c->tune_ns[c->tune_pending] = (double)ms * 1e6 / c->tune_samples;
+  c->tune_pending = 0;
+  if (c->tune_ns[MCPT_TRAVERSAL_LANE] > 0.0 && c->tune_ns[MCPT_TRAVERSAL_WAVE] > 0.0)
+    c->tune_choice = c->tune_ns[MCPT_TRAVERSAL_WAVE] < c->tune_ns[MCPT_TRAVERSAL_LANE] ? MCPT_TRAVERSAL_WAVE
+                                                                                    : MCPT_TRAVERSAL_LANE;
+  return hipSuccess;
+}
+constexpr double kTuneMinSamples = 1 << 24;   // launches smaller than this are not timed
 
 extern "C" {
 
@@ -231,6 +262,7 @@ int mcpt_upload_scene(mcpt_ctx* c, const float* prims, int n_prims, const float*
   c->mesh_ids = mesh_ids;
   free_meshes(c);                 // a new scene drops the previous meshes (upload them again)
   c->has_scene = true;
+  reset_tuning(c);
   return MCPT_OK;
 }
 
@@ -408,7 +440,11 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   }
   p.minfo = c->d_minfo; p.mnodes = c->d_mnodes; p.mleaves = c->d_mleaves; p.mtris = c->d_mtris;
   p.mverts = c->d_mverts; p.mnorms = c->d_mnorms; p.n_meshes = c->n_meshes; p.flat_face = c->flat_face;
-  p.wave_traversal = (resolve_traversal(c) == MCPT_TRAVERSAL_WAVE) ? 1 : 0;
+  HIP_OR_RETURN(collect_tuning(c));
+  // (the counting build is not timed: AUTO counts with the per-lane walk)
+  const int mode = count ? (c->traversal == MCPT_TRAVERSAL_AUTO ? MCPT_TRAVERSAL_LANE : c->traversal)
+                         : resolve_traversal(c);
+  p.wave_traversal = (mode == MCPT_TRAVERSAL_WAVE) ? 1 : 0;
   p.walk_exit = resolve_walk_exit(c);
   p.leaf_batch = resolve_leaf_batch(c);
   p.first_pass = first_pass; p.n_passes = n_passes; p.bounces = bounces; p.variant = variant;
@@ -435,6 +471,11 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   }
   p.partial = c->d_partial;
   if (count) HIP_OR_RETURN(hipMemsetAsync(c->d_events, 0, sizeof(unsigned long long) * mcpt::EV_COUNT, c->stream));
+  const double samples = (double)p.n_local_px * n_passes;
+  if (!count && c->traversal == MCPT_TRAVERSAL_AUTO && !c->tune_choice && samples >= kTuneMinSamples) {
+    c->tune_pending = mode;
+    c->tune_samples = samples;
+  }
   HIP_OR_RETURN(hipEventRecord(c->ev_start, c->stream));
   HIP_OR_RETURN(mcpt_launch_render(p, count, c->stream));
   HIP_OR_RETURN(hipEventRecord(c->ev_mid, c->stream));
@@ -571,6 +612,7 @@ int mcpt_set_traversal(mcpt_ctx* c, int mode) {
   if (!c || mode < MCPT_TRAVERSAL_AUTO || mode > MCPT_TRAVERSAL_WAVE)
     return set_err(MCPT_ERR_INVALID_ARG, "mcpt_set_traversal: bad mode");
   c->traversal = mode;
+  reset_tuning(c);
   return MCPT_OK;
 }
 

@@ -35,11 +35,6 @@ constexpr int kPassChunk = 32;
 // largest scene render_kernel stages into LDS: 160 KB / 7 workgroups - 19 KB of per-pixel rows
 constexpr int kLdsSceneBytes = 3584;
 constexpr int kPrimF4 = 8;
-// MCPT_TRAVERSAL_AUTO picks the wave-coherent walk for BVHs up to this depth.  Since the
-// per-pixel state moved to LDS (7 waves/SIMD), the per-lane walk is faster on every
-// reference scene (profiles/r01_ab6.jsonl: scene 6 8.07 vs 7.72, scene 1 10.4 vs 8.9,
-// scene 8 0.26 vs 0.11 Gsamples/s), so AUTO = per lane; the wave walk stays selectable.
-constexpr int kWaveMaxDepth = -1;
 
 struct RenderParams {
   const float4* nodes;

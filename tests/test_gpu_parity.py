@@ -230,3 +230,29 @@ def test_leaf_batch_parity(mcpt_mod, oracle_mod, renderer, walk_exit, leaf_batch
     ref, _ = _oracle(oracle_mod, scene_id, W, H, 7, S, B, ior=ior)
     _compare(gpu, ref, f"scene {scene_id} walk_exit {walk_exit} leaf_batch {leaf_batch}")
 
+
+def test_auto_traversal_tuning(mcpt_mod, renderer):
+    """AUTO times LANE then WAVE on the first two sizeable launches and keeps the faster one;
+    the image is bit-identical to a fixed strategy with the same launch split."""
+    W, H = 1920, 1080
+    ipv, iv = mcpt_mod.camera_canonical(W, H)
+
+    def run(mode):
+        renderer.set_traversal(mode)          # also restarts the AUTO measurement
+        renderer.upload_scene(mcpt_mod.Scene.reference(6))
+        renderer.set_target(W, H)
+        seen = []
+        for k in range(3):                    # 1080p x 16 passes = 33 M samples >= 2^24
+            seen.append(renderer.traversal())
+            renderer.render(ipv, iv, 1 + 16 * k, 16, 0.0, 4, 1.0, 0)
+        seen.append(renderer.traversal())
+        acc, n = renderer.read_accum()
+        return acc, n, seen
+
+    auto, n_a, seen = run(0)
+    lane, n_l, _ = run(1)
+    renderer.set_traversal(0)
+    assert seen[:3] == [1, 1, 2] and seen[3] in (1, 2)
+    assert n_a == n_l == 48
+    assert np.array_equal(auto.view(np.uint32), lane.view(np.uint32))
+
