@@ -16,7 +16,12 @@
 //    inner traversal and lanes doing their next bounce run the same instructions;
 //  * BVH traversal is the reference's DFS (raytracer_func.frag:734-769, right child
 //    popped first, cull test at push time) but stackless: the implicit-heap stack is
-//    encoded as a bitmask of levels holding a pending left sibling — registers only;
+//    encoded as a bitmask of levels holding a pending left sibling — registers only.
+//    Per lane (walk_run, resumable: deep BVHs suspend the walk loop when few lanes still
+//    walk and batch leaf visits) or wave-coherent (traverse_wave, scalar loads);
+//  * the primary hit of a pixel is cached per segment (no jitter: same camera ray every
+//    pass); square roots and reciprocals outside the walk loop use short sequences proven
+//    correctly rounded on all 2^32 inputs (mcpt_math.h, tools/mathcheck);
 //  * the scene is repacked at upload into 16-byte records (node: centre / half-width /
 //    1/half-width; prim: inverse rows, transform rows, colour, material) so every fetch
 //    is a dwordx4; scenes up to kLdsSceneBytes are staged once per workgroup into LDS;
@@ -542,55 +547,6 @@ __device__ __forceinline__ bool walk_run(const SR& s, f3 O, f3 D, Hit& h, Walk& 
   }
 }
 
-// intersect_bvh per lane, "while-while" schedule (Aila & Laine, non-speculative): the wave
-// runs internal-node steps while any lane sits on an internal node (lanes on a leaf wait),
-// then one leaf step for every lane on a leaf.  Each lane's own visit sequence is the
-// reference's; only the interleaving across lanes changes.  Diagnostic variant
-// (MCPT_WHILE_WHILE); the default is the if-if loop of traverse_lane.
-template <bool COUNT, class SR>
-__device__ __forceinline__ void traverse_lane_ww(const SR& s, f3 O, f3 D, Hit& h, Ev<COUNT>& ev) {
-  ev.inc(EV_TRAV);
-  h.index = -1; h.dist = kFLTMAX; h.shape = -1; h.dir = -1; h.cull2 = cull_bound_sq(kFLTMAX);
-  const f3 invD = mk(rcp_rn(D.x), rcp_rn(D.y), rcp_rn(D.z));
-  const int leaf0 = (1 << s.depth) - 1;
-  int node = 0, level = 0;
-  uint32_t pending = 0;
-  bool done = false;
-  auto pop = [&]() {
-    if (pending == 0) { done = true; return; }
-    int L = 31 - __builtin_clz(pending);
-    pending &= ~(1u << L);
-    node = ((node + 1) >> (level - L)) - 2;
-    level = L;
-  };
-  for (;;) {
-    while (__ballot(!done && node < leaf0)) {
-      if (!done && node < leaf0) {
-        ev.inc(EV_NODE);
-        const size_t j = 2 * (size_t)node + 1;
-        const float4 l0 = s.nodes[j * 3], r0 = s.nodes[j * 3 + 3];
-        bool hl = (COUNT || l0.w != 0.0f) && box_test<false>(l0, s.nodes[j * 3 + 1], s.nodes[j * 3 + 2], O, D, invD, h.cull2);
-        bool hr = (COUNT || r0.w != 0.0f) && box_test<false>(r0, s.nodes[j * 3 + 4], s.nodes[j * 3 + 5], O, D, invD, h.cull2);
-        if (hr) {
-          if (hl) pending |= 1u << (level + 1);
-          node = (int)j + 1; level++;
-        } else if (hl) {
-          node = (int)j; level++;
-        } else {
-          pop();
-        }
-      }
-    }
-    if (!done) {   // every live lane is on a leaf
-      ev.inc(EV_LEAF);
-      int p = s.leaves[node - leaf0];
-      if (p >= 0) prim_test<COUNT, false>(s, p, O, D, h, ev);
-      pop();
-    }
-    if (__ballot(!done) == 0) break;
-  }
-}
-
 // intersect_bvh, wave-coherent.  Every lane's DFS visits a subsequence of ONE fixed order:
 // the right-child-first pre-order of the implicit heap, with the subtrees its push-time
 // box tests culled.  The wave walks that order once with a wave-uniform cursor (node,
@@ -655,11 +611,7 @@ __device__ __forceinline__ void traverse_wave(const SR& s, f3 O, f3 D, Hit& h, E
 template <bool COUNT, bool WAVE, class SR>
 __device__ __forceinline__ void traverse(const SR& s, f3 O, f3 D, Hit& h, Ev<COUNT>& ev) {
   if (WAVE) traverse_wave<COUNT>(s, O, D, h, ev);
-#ifdef MCPT_WHILE_WHILE
-  else traverse_lane_ww<COUNT>(s, O, D, h, ev);
-#else
   else traverse_lane<COUNT>(s, O, D, h, ev);
-#endif
 }
 
 // intersection_info raytracer_func.frag:812-897 (hit only; misses leave N,P untouched)
