@@ -1,0 +1,107 @@
+"""BASELINE.json configurations at their full sizes: oracle checks on row subsets
+(the oracle renders only the sampled rows) and size-independent properties over whole frames —
+determinism, launch-split invariance at chunk boundaries, row-band shard invariance."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def bits(a):
+    return np.asarray(a, np.float32).view(np.uint32)
+
+
+@pytest.fixture(scope="module")
+def renderer(mcpt_mod):
+    r = mcpt_mod.Renderer(0)
+    yield r
+    r.close()
+
+
+def render(mcpt_mod, r, sc, W, H, first, S, B, ior=1.0, band_rows=8, world=1, rank=0, split=None):
+    r.upload_scene(sc)
+    r.set_target(W, H, band_rows, world, rank)
+    ipv, iv = mcpt_mod.camera_canonical(W, H)
+    p = first
+    for n in (split or [S]):
+        r.render(ipv, iv, p, n, 0.0, B, ior, 0)
+        p += n
+    acc, n = r.read_accum()
+    assert n == S
+    return acc
+
+
+def oracle_rows(oracle_mod, sc, W, H, first, S, B, rows, ior=1.0):
+    """Oracle image restricted to `rows` (absolute frame rows)."""
+    prims, nodes, leaves = sc.buffers()
+    ipv, iv = oracle_mod.camera(W, H)
+    out = {}
+    for y in rows:
+        ref, _ = oracle_mod.render(prims, nodes, leaves, sc.depth(), ipv, iv, W, H, first, S, 0.0, B, ior, 0,
+                                   row_step=H, row_offset=int(y))
+        out[int(y)] = ref[int(y)]
+    return out
+
+
+def test_c5_4k_shard_rows(mcpt_mod, oracle_mod, renderer):
+    """C5 geometry: 3840x2160, 8-GPU row bands (rank 3), late passes of the 84,000-spp run."""
+    sc = mcpt_mod.Scene.reference(6)
+    W, H, first, S, B = 3840, 2160, 83_969, 2, 8
+    part = render(mcpt_mod, renderer, sc, W, H, first, S, B, world=8, rank=3)
+    rows = renderer.local_row_ids()
+    pick = np.arange(5, len(rows), 67)
+    ref = oracle_rows(oracle_mod, sc, W, H, first, S, B, rows[pick])
+    for i in pick:
+        assert np.array_equal(bits(part[i]), bits(ref[int(rows[i])])), f"4K row {rows[i]}"
+
+
+def test_c4_scene8_rows(mcpt_mod, oracle_mod, renderer):
+    """C4 workload: scene 8 (largest BVH), 1080p, B 12 (deep-BVH walk kernel)."""
+    sc = mcpt_mod.Scene.reference(8)
+    W, H, S, B = 1920, 1080, 2, 12
+    img = render(mcpt_mod, renderer, sc, W, H, 1, S, B)
+    rows = np.arange(11, H, 157)
+    ref = oracle_rows(oracle_mod, sc, W, H, 1, S, B, rows)
+    for y in rows:
+        assert np.array_equal(bits(img[y]), bits(ref[int(y)])), f"scene 8 row {y}"
+
+
+def test_c3_ior_roughness_rows(mcpt_mod, oracle_mod, renderer):
+    """C3 workload: scene 6, IOR 1.5, roughness 0.5 on every non-emissive primitive."""
+    sc = mcpt_mod.Scene.reference(6)
+    prims, _, _ = sc.buffers()
+    for i in range(sc.nb_prim()):
+        rec = prims[i]
+        if rec[58] <= 0:
+            sc.set_material(i, np.concatenate([rec[52:56], [rec[56], 0.5, rec[58]]]).astype(np.float32))
+    W, H, S, B = 1920, 1080, 2, 8
+    img = render(mcpt_mod, renderer, sc, W, H, 1, S, B, ior=1.5)
+    rows = np.arange(3, H, 119)
+    ref = oracle_rows(oracle_mod, sc, W, H, 1, S, B, rows, ior=1.5)
+    for y in rows:
+        assert np.array_equal(bits(img[y]), bits(ref[int(y)])), f"C3 row {y}"
+
+
+def test_c2_determinism_and_chunk_split(mcpt_mod, renderer):
+    """C2 at full size: the same 64 passes twice, and split at the 32-pass chunk boundary."""
+    sc = mcpt_mod.Scene.reference(6)
+    a = render(mcpt_mod, renderer, sc, 1920, 1080, 1, 64, 8)
+    b = render(mcpt_mod, renderer, sc, 1920, 1080, 1, 64, 8)
+    c = render(mcpt_mod, renderer, sc, 1920, 1080, 1, 64, 8, split=[32, 32])
+    assert np.array_equal(bits(a), bits(b))
+    assert np.array_equal(bits(a), bits(c))
+    assert np.isfinite(a).all() and (a >= 0).all() and a.mean() > 0
+
+
+def test_c2_shards_cover_frame(mcpt_mod, renderer):
+    """8 row-band shards of the 1080p frame are exactly the single-GPU frame's rows."""
+    sc = mcpt_mod.Scene.reference(6)
+    full = render(mcpt_mod, renderer, sc, 1920, 1080, 1, 4, 8)
+    seen = np.zeros(1080, bool)
+    for rank in range(8):
+        part = render(mcpt_mod, renderer, sc, 1920, 1080, 1, 4, 8, world=8, rank=rank)
+        rows = renderer.local_row_ids()
+        assert not seen[rows].any()
+        seen[rows] = True
+        assert np.array_equal(bits(part), bits(full[rows]))
+    assert seen.all()
