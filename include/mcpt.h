@@ -119,7 +119,9 @@ int mcpt_render_counted(mcpt_ctx* ctx, const float* invPV, const float* invV, in
                         unsigned long long* events);
 int mcpt_event_bytes(int event);
 
-/* Diagnostics: read (and optionally zero) the context's MCPT_EV_COUNT device counter slots.
+#define MCPT_DEBUG_SLOTS 16
+/* Diagnostics: read (and optionally zero) the context's MCPT_DEBUG_SLOTS device counter slots
+ * (the first MCPT_EV_COUNT are the event counters).
  * Only the counting launches and diagnostic builds (-DMCPT_STAMPS: wave-cycle section
  * totals) write them.  Synchronizes the context's stream. */
 int mcpt_debug_counters(mcpt_ctx* ctx, unsigned long long* out, int reset);

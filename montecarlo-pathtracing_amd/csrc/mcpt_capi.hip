@@ -155,7 +155,8 @@ int mcpt_create(int device_ordinal, mcpt_ctx** out) {
   if (e == hipSuccess) e = hipEventCreate(&c->ev_start);
   if (e == hipSuccess) e = hipEventCreate(&c->ev_mid);
   if (e == hipSuccess) e = hipEventCreate(&c->ev_stop);
-  if (e == hipSuccess) e = hipMalloc(&c->d_events, sizeof(unsigned long long) * mcpt::EV_COUNT);
+  if (e == hipSuccess) e = hipMalloc(&c->d_events, sizeof(unsigned long long) * MCPT_DEBUG_SLOTS);
+  if (e == hipSuccess) e = hipMemset(c->d_events, 0, sizeof(unsigned long long) * MCPT_DEBUG_SLOTS);
   if (e != hipSuccess) { mcpt_destroy(c); return set_err(MCPT_ERR_HIP, "mcpt_create", e); }
   c->stream = c->own_stream;
   *out = c;
@@ -506,9 +507,9 @@ int mcpt_render_counted(mcpt_ctx* c, const float* invPV, const float* invV, int 
 int mcpt_debug_counters(mcpt_ctx* c, unsigned long long* out, int reset) {
   if (!c || !out) return MCPT_ERR_INVALID_ARG;
   HIP_OR_RETURN(hipSetDevice(c->device));
-  HIP_OR_RETURN(hipMemcpyAsync(out, c->d_events, sizeof(unsigned long long) * mcpt::EV_COUNT,
+  HIP_OR_RETURN(hipMemcpyAsync(out, c->d_events, sizeof(unsigned long long) * MCPT_DEBUG_SLOTS,
                                hipMemcpyDeviceToHost, c->stream));
-  if (reset) HIP_OR_RETURN(hipMemsetAsync(c->d_events, 0, sizeof(unsigned long long) * mcpt::EV_COUNT, c->stream));
+  if (reset) HIP_OR_RETURN(hipMemsetAsync(c->d_events, 0, sizeof(unsigned long long) * MCPT_DEBUG_SLOTS, c->stream));
   HIP_OR_RETURN(hipStreamSynchronize(c->stream));
   return MCPT_OK;
 }

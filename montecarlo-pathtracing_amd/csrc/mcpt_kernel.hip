@@ -137,6 +137,7 @@ struct Ev {
 #ifdef MCPT_STAMPS
   unsigned long long st_leaf = 0;   // diagnostic: wave-cycles in the traversal's leaf blocks
   unsigned long long st_lit = 0, st_wit = 0;   // traversal loop: lane iterations, wave iterations
+  unsigned long long st_nl = 0, st_ll = 0, st_nw = 0, st_lw = 0;   // node / leaf block lanes, iterations
 #endif
   __device__ __forceinline__ void init() { if (COUNT) for (int i = 0; i < EV_COUNT; ++i) c.v[i] = 0; }
   __device__ __forceinline__ void inc(int e) { if (COUNT) c.v[e]++; }
@@ -517,7 +518,14 @@ __device__ __forceinline__ bool walk_run(const SR& s, f3 O, f3 D, Hit& h, Walk& 
 #ifdef MCPT_STAMPS
     ev.st_leaf += __builtin_amdgcn_s_memtime() - t0;
     ev.st_lit += do_leaf || do_node;
-    ev.st_wit += (int)__lane_id() == __builtin_ffsll((long long)__ballot(1)) - 1;
+    {
+      const bool lead = (int)__lane_id() == __builtin_ffsll((long long)__ballot(1)) - 1;
+      ev.st_wit += lead;
+      ev.st_nl += do_node;   // lanes in the node block / leaf block, and iterations running each
+      ev.st_ll += do_leaf;
+      ev.st_nw += lead && __ballot(do_node) != 0;
+      ev.st_lw += lead && __ballot(do_leaf) != 0;
+    }
 #endif
     if (do_node) {
       ev.inc(EV_NODE);
@@ -967,11 +975,16 @@ __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParam
     // wave totals = the last-finishing lane's sums (max over lanes); lane-iterations summed
     unsigned long long vals[6] = {__builtin_amdgcn_s_memtime() - st_k0, st_p, st_t, st_s, st_it, ev.st_leaf};
     unsigned long long it_sum = st_it, lit = ev.st_lit, wit = ev.st_wit;
+    unsigned long long nl = ev.st_nl, nw = ev.st_nw, ll = ev.st_ll, lw = ev.st_lw;
     for (int off = 32; off > 0; off >>= 1) {
       for (int k = 0; k < 6; ++k) { unsigned long long o = __shfl_xor(vals[k], off); vals[k] = vals[k] > o ? vals[k] : o; }
       it_sum += __shfl_xor(it_sum, off);
       lit += __shfl_xor(lit, off);
       wit += __shfl_xor(wit, off);
+      nl += __shfl_xor(nl, off);
+      nw += __shfl_xor(nw, off);
+      ll += __shfl_xor(ll, off);
+      lw += __shfl_xor(lw, off);
     }
     if (lane == 0 && p.events) {
       for (int k = 0; k < 5; ++k) atomicAdd(p.events + k, vals[k]);
@@ -980,6 +993,10 @@ __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParam
       atomicAdd(p.events + 7, vals[5]);
       atomicAdd(p.events + 9, lit);
       atomicAdd(p.events + 10, wit);
+      atomicAdd(p.events + 11, nl);
+      atomicAdd(p.events + 12, nw);
+      atomicAdd(p.events + 13, ll);
+      atomicAdd(p.events + 14, lw);
     }
   }
 #endif

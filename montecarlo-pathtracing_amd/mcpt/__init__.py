@@ -39,6 +39,9 @@ SCENE_KEYS = {1: "Q", 2: "W", 3: "E", 4: "R", 5: "T", 6: "Y", 7: "U", 8: "I"}
 _HERE = os.path.dirname(os.path.abspath(__file__))
 
 
+DEBUG_SLOTS = 16   # MCPT_DEBUG_SLOTS
+
+
 class MCPTError(RuntimeError):
     pass
 
@@ -462,8 +465,8 @@ class Renderer:
         return ev
 
     def debug_counters(self, reset: bool = True) -> np.ndarray:
-        """The context's device counter slots (diagnostic builds write section cycles there)."""
-        out = np.zeros(len(EVENT_NAMES), np.uint64)
+        """The context's MCPT_DEBUG_SLOTS device counter slots (diagnostic builds write there)."""
+        out = np.zeros(DEBUG_SLOTS, np.uint64)
         _check(lib().mcpt_debug_counters(self._h, out.ctypes.data_as(_c_u64_p), int(reset)),
                "mcpt_debug_counters")
         return out

@@ -5,7 +5,8 @@ set -e
 OUT=$1; shift
 export TMPDIR=/tmp
 mkdir -p "$OUT"
-ARGS="--steps 1 --warmup 1 --no-cpu-baseline --no-count $*"
+# two warm-up steps: AUTO traversal's timing trials; the summary reads the timed step's launch
+ARGS="--steps 1 --warmup 2 --no-cpu-baseline --no-count $*"
 run() {  # name counters...
   local name=$1; shift
   timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-trace -d "$OUT/$name" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/$name.log" 2>&1

@@ -21,22 +21,34 @@ KERNEL = "render_kernel<false"
 
 
 def load(d):
-    vals = collections.defaultdict(list)
+    """Counters of the LAST path-tracing launch of each pass (the timed step: earlier launches
+    are warm-up, including AUTO traversal's two timing trials, which run other kernels)."""
+    out = {}
     for f in glob.glob(os.path.join(d, "*", "run_counter_collection.csv")):
+        per_dispatch = collections.defaultdict(dict)
+        names = {}
         for r in csv.DictReader(open(f)):
             if KERNEL in r["Kernel_Name"]:
-                vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in vals.items()}
+                k = int(r["Dispatch_Id"])
+                per_dispatch[k][r["Counter_Name"]] = per_dispatch[k].get(r["Counter_Name"], 0.0) + \
+                    float(r["Counter_Value"])
+                names[k] = r["Kernel_Name"]
+        if per_dispatch:
+            last = max(per_dispatch)
+            out.update(per_dispatch[last])
+            out["_kernel"] = names[last]
+    return out
 
 
 def main():
     d, workload, out = sys.argv[1], sys.argv[2], sys.argv[3]
     c = load(d)
+    kernel = c.pop("_kernel", "mcpt::render_kernel<false, *>")
     fetch_b = c["FETCH_SIZE"] * 1024 * 2          # gfx950: FETCH_SIZE = half the bytes
     write_b = c["WRITE_SIZE"] * 1024
     rec = {
         "workload": workload,
-        "kernel": "mcpt::render_kernel<false, *>",
+        "kernel": kernel,
         "source": f"rocprofv3 --pmc passes of tools/pmc.sh ({os.path.basename(d.rstrip('/'))})",
         "hbm_bytes_per_launch": fetch_b + write_b,
         "fetch_bytes_per_launch_corrected": fetch_b,

@@ -18,14 +18,14 @@ W, H, S = 1920, 1080, 32
 r = mcpt.Renderer(0)
 r.set_target(W, H)
 ipv, iv = mcpt.camera_canonical(W, H)
-for sid, B in [(6, 8), (1, 3), (3, 8), (8, 12)]:
+for sid, B in [(6, 8), (3, 8), (8, 12)]:
     r.upload_scene(mcpt.Scene.reference(sid))
     for mode in (1,):
         r.set_traversal(mode)
         r.debug_counters(reset=True)
         r.render(ipv, iv, 1, S, 0.0, B, 1.0, 0)
         c = r.debug_counters(reset=True).astype(float)
-        tot, pre, trav, rest, it, lane_it, waves, leaf, lane_tr, t_lit, t_wit = c[:11]
+        tot, pre, trav, rest, it, lane_it, waves, leaf, lane_tr, t_lit, t_wit, nl, nw, ll, lw = c[:15]
         print(json.dumps({"scene": sid, "mode": mode, "waves": int(waves),
                           "share_prelude": round(pre / tot, 3), "share_traverse_rounds": round(trav / tot, 3),
                           "share_shade_rounds": round(rest / tot, 3),
@@ -35,5 +35,9 @@ for sid, B in [(6, 8), (1, 3), (3, 8), (8, 12)]:
                           "trav_lane_util": round(lane_tr / (64 * it), 3) if lane_tr else None,
                           "trav_loop_simd_util": round(t_lit / (64 * t_wit), 3) if t_wit else None,
                           "trav_loop_iters_per_wave": round(t_wit / waves, 1),
+                          "node_block_lane_util": round(nl / (64 * nw), 3) if nw else None,
+                          "leaf_block_lane_util": round(ll / (64 * lw), 3) if lw else None,
+                          "node_block_iters_per_wave": round(nw / waves, 1),
+                          "leaf_block_iters_per_wave": round(lw / waves, 1),
                           "cycles_per_round": round((trav + rest) / it, 1)}), flush=True)
 r.close()
