@@ -184,6 +184,14 @@ def main():
                         valu = {"achieved": round(ach, 2), "peak": VALU_PEAK_T, "unit": "T lane-instr/s",
                                 "frac": round(ach / VALU_PEAK_T, 4), "instructions_per_launch": n_valu,
                                 "source": rec.get("source")}
+                        if rec.get("valu_lane_utilisation") is not None:
+                            valu["lane_utilisation"] = round(rec["valu_lane_utilisation"], 4)
+                        if rec.get("f32_flop_per_launch_upper"):
+                            # fp32 ops against the 157.3 TFLOP/s vector peak (upper
+                            # bound: counts every lane of an issued instruction)
+                            tf = rec["f32_flop_per_launch_upper"] / (avg_trace_ms / 1e3) / 1e12
+                            valu["f32_tflops_upper"] = round(tf, 2)
+                            valu["f32_peak_tflops"] = 157.3
             except Exception:
                 traffic, valu = None, None
         out = {

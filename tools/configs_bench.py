@@ -8,7 +8,7 @@ wall time around synchronised launches (`wall_ms`):
   C1  scene 1, 256x256, 4 spp, B 3      GPU, and the CPU oracle on the whole config (16 threads)
   C2  scene 6, 1920x1080, 256 spp, B 8  (= bench.py's workload)
   C3  scene 6, 1920x1080, 1024 spp, B 8, IOR 1.5, roughness of every non-emissive primitive
-      swept over 0, 0.25, 0.5, 0.75, 1
+      swept over 0, 0.5, 0.9, 0.99, 1
   C4  scene 8, 1920x1080, 512 spp, B 12, 8-GPU row bands: each of the 8 shards measured in
       turn on this GPU (world 8, rank r); projected 8-GPU rate = all samples / slowest shard
   C5  scene 6, 3840x2160, 8-GPU row bands, progressive: 1024 spp per shard measured (of the
@@ -93,7 +93,7 @@ def main():
 
     # C3: IOR 1.5, roughness sweep over the non-emissive primitives
     S = 1024 // q
-    for rough in (0.0, 0.25, 0.5, 0.75, 1.0):
+    for rough in (0.0, 0.5, 0.9, 0.99, 1.0):
         sc = mcpt.Scene.reference(6)
         prims, _, _ = sc.buffers()
         for i in range(sc.nb_prim()):
