@@ -45,8 +45,9 @@ enum mcpt_variant {
 
 /* BVH traversal strategy of the kernel (same results, different speed) */
 enum mcpt_traversal {
-  MCPT_TRAVERSAL_AUTO = 0,   /* measured: the first two launches of >= 2^24 samples after a scene
-                                upload try LANE and WAVE, later launches use the faster */
+  MCPT_TRAVERSAL_AUTO = 0,   /* measured: after a scene upload, launches of >= 2^24 samples try
+                                LANE and WAVE once each on launches of the same shape (pixels,
+                                passes); later launches use the faster */
   MCPT_TRAVERSAL_LANE = 1,   /* each lane walks its own DFS (divergent, vector loads) */
   MCPT_TRAVERSAL_WAVE = 2,   /* the wave walks the union of its lanes' DFS orders (scalar loads) */
 };

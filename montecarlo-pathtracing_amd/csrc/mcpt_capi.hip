@@ -70,7 +70,9 @@ struct mcpt_ctx {
   // launches use the faster one (results are identical either way)
   int tune_pending = 0;             // mode of the launch whose timing is not collected yet
   double tune_samples = 0.0;        // samples of that launch
-  double tune_ns[3] = {0.0, 0.0, 0.0};   // ns per sample measured, by mode
+  long long tune_shape[2] = {0, 0};      // (local pixels, passes) of that launch
+  long long meas_shape[2] = {0, 0};      // shape the measurements below were taken on
+  double tune_ns[3] = {0.0, 0.0, 0.0};   // ns per sample measured, by mode (same shape)
   int tune_choice = 0;              // resolved mode once both are measured
   int walk_exit = -1;               // mcpt_set_walk_exit; -1: by BVH depth
   int leaf_batch = -1;              // MCPT_LEAF_BATCH env (tuning); -1: default
@@ -97,12 +99,14 @@ static int resolve_leaf_batch(const mcpt_ctx* c) {
 static int resolve_traversal(const mcpt_ctx* c) {
   if (c->traversal != MCPT_TRAVERSAL_AUTO) return c->traversal;
   if (c->tune_choice) return c->tune_choice;
-  return c->tune_ns[MCPT_TRAVERSAL_LANE] > 0.0 ? MCPT_TRAVERSAL_WAVE : MCPT_TRAVERSAL_LANE;   // next trial
+  // next trial: the walk not yet timed on the measured launch shape
+  return c->tune_ns[MCPT_TRAVERSAL_LANE] > 0.0 ? MCPT_TRAVERSAL_WAVE : MCPT_TRAVERSAL_LANE;
 }
 
 static void reset_tuning(mcpt_ctx* c) {
   c->tune_pending = 0;
   c->tune_samples = 0.0;
+  c->tune_shape[0] = c->tune_shape[1] = c->meas_shape[0] = c->meas_shape[1] = 0;
   c->tune_ns[0] = c->tune_ns[1] = c->tune_ns[2] = 0.0;
   c->tune_choice = 0;
 }
@@ -114,6 +118,13 @@ static hipError_t collect_tuning(mcpt_ctx* c) {
   hipError_t e = hipEventSynchronize(c->ev_mid);
   if (e == hipSuccess) e = hipEventElapsedTime(&ms, c->ev_start, c->ev_mid);
   if (e != hipSuccess) return e;
+  // per-sample times are compared only between launches of the same shape (pixels, passes):
+  // a launch of another shape restarts the comparison
+  if (c->tune_shape[0] != c->meas_shape[0] || c->tune_shape[1] != c->meas_shape[1]) {
+    c->tune_ns[0] = c->tune_ns[1] = c->tune_ns[2] = 0.0;
+    c->meas_shape[0] = c->tune_shape[0];
+    c->meas_shape[1] = c->tune_shape[1];
+  }
   c->tune_ns[c->tune_pending] = (double)ms * 1e6 / c->tune_samples;
   c->tune_pending = 0;
   if (c->tune_ns[MCPT_TRAVERSAL_LANE] > 0.0 && c->tune_ns[MCPT_TRAVERSAL_WAVE] > 0.0)
@@ -476,6 +487,8 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   if (!count && c->traversal == MCPT_TRAVERSAL_AUTO && !c->tune_choice && samples >= kTuneMinSamples) {
     c->tune_pending = mode;
     c->tune_samples = samples;
+    c->tune_shape[0] = p.n_local_px;
+    c->tune_shape[1] = n_passes;
   }
   HIP_OR_RETURN(hipEventRecord(c->ev_start, c->stream));
   HIP_OR_RETURN(mcpt_launch_render(p, count, c->stream));
