@@ -46,10 +46,11 @@ def timed_render(r, ipv, iv, first, spp, B, ior, chunk=256):
     return kms, (time.perf_counter() - t0) * 1e3
 
 
-def tune(r, ipv, iv, B, ior):
-    """AUTO traversal's two timing trials (after each scene upload), outside the measurements."""
+def tune(r, ipv, iv, B, ior, chunk=256):
+    """AUTO traversal's two timing trials (after each scene upload), outside the measurements,
+    on launches of the measured shape (timed_render's chunk)."""
     for _ in range(2):
-        r.render(ipv, iv, 1, 32, 0.0, B, ior, mcpt.MONTECARLO)
+        r.render(ipv, iv, 1, chunk, 0.0, B, ior, mcpt.MONTECARLO)
     r.clear_accum()
 
 

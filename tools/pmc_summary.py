@@ -61,9 +61,10 @@ def main():
         rec["valu_issue_busy_frac"] = c["SQ_INSTS_VALU"] * 2.0 / (simds * cycles)   # ≥2 cycles per wave64 VALU
         rec["wave_cycle_split"] = {k: c[k] / c["SQ_WAVE_CYCLES"] for k in
                                    ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY") if k in c}
-    if "SQ_THREAD_CYCLES_VALU" in c and c.get("SQ_INST_CYCLES_VALU"):
-        # lanes doing work per issued VALU instruction (rocprof's VALUUtilization)
-        rec["valu_lane_utilisation"] = c["SQ_THREAD_CYCLES_VALU"] / (c["SQ_INST_CYCLES_VALU"] * 64.0)
+    if "SQ_THREAD_CYCLES_VALU" in c and c.get("SQ_ACTIVE_INST_VALU"):
+        # active lanes per issued VALU instruction: rocprof's VALUUtilization expression,
+        # 100 * SQ_THREAD_CYCLES_VALU / (SQ_ACTIVE_INST_VALU * 64)
+        rec["valu_lane_utilisation"] = c["SQ_THREAD_CYCLES_VALU"] / (c["SQ_ACTIVE_INST_VALU"] * 64.0)
     if "SQ_INSTS_VALU_FMA_F32" in c:
         # fp32 flop upper bound (every lane active): FMA = 2, MUL / ADD = 1
         rec["f32_flop_per_launch_upper"] = 64.0 * (2 * c["SQ_INSTS_VALU_FMA_F32"] + c["SQ_INSTS_VALU_MUL_F32"] +
