@@ -7,6 +7,7 @@
 // shader (shaders/raytracer.vert:9-22, evaluated here once per launch on the host).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -32,6 +33,10 @@ static int set_err(int status, const char* what, hipError_t e = hipSuccess) {
     hipError_t e_ = (call);                                         \
     if (e_ != hipSuccess) return set_err(MCPT_ERR_HIP, #call, e_);  \
   } while (0)
+
+// default bound of the segment-sum buffer of one sub-launch (1 GiB: 42 segments = 1,344
+// passes per launch at 1080p, 10 at 4K; mcpt_set_partial_budget / MCPT_PARTIAL_BYTES)
+constexpr size_t kDefaultPartialBudget = size_t(1) << 30;
 
 struct mcpt_ctx {
   int device = 0;
@@ -62,8 +67,12 @@ struct mcpt_ctx {
   unsigned long long* d_events = nullptr;
   float* d_partial = nullptr;       // pass-segment sums (launches spanning > 1 chunk)
   size_t partial_bytes = 0;
-  hipEvent_t ev_start = nullptr, ev_mid = nullptr, ev_stop = nullptr;
+  // per sub-launch of the last render call: (start, after the path-tracing kernel, after the
+  // combine kernel); a call is split into sub-launches at chunk boundaries (partial_budget)
+  std::vector<hipEvent_t> evs;
+  int n_sub = 0;                    // sub-launches of the last render call
   bool timed = false;
+  size_t partial_budget = kDefaultPartialBudget;
   int traversal = MCPT_TRAVERSAL_AUTO;
   // AUTO traversal: the first two sizeable launches after a scene upload run the per-lane and
   // the wave-coherent walk once each (kernel time per sample from the launch events), later
@@ -77,6 +86,33 @@ struct mcpt_ctx {
   int walk_exit = -1;               // mcpt_set_walk_exit; -1: by BVH depth
   int leaf_batch = -1;              // MCPT_LEAF_BATCH env (tuning); -1: default
 };
+
+// events of sub-launch k: start / mid / stop
+static hipEvent_t ev_start(const mcpt_ctx* c, int k) { return c->evs[3 * k]; }
+static hipEvent_t ev_mid(const mcpt_ctx* c, int k) { return c->evs[3 * k + 1]; }
+static hipEvent_t ev_stop(const mcpt_ctx* c, int k) { return c->evs[3 * k + 2]; }
+static hipError_t ensure_events(mcpt_ctx* c, int n_sub) {
+  while ((int)c->evs.size() < 3 * n_sub) {
+    hipEvent_t e = nullptr;
+    hipError_t r = hipEventCreate(&e);
+    if (r != hipSuccess) return r;
+    c->evs.push_back(e);
+  }
+  return hipSuccess;
+}
+// (path-tracing kernel ms, combine kernel ms) summed over the sub-launches of the last call
+static hipError_t sub_launch_ms(const mcpt_ctx* c, float* trace_ms, float* combine_ms) {
+  *trace_ms = 0.0f; *combine_ms = 0.0f;
+  for (int k = 0; k < c->n_sub; ++k) {
+    float a = 0.0f, b = 0.0f;
+    hipError_t e = hipEventSynchronize(ev_stop(c, k));
+    if (e == hipSuccess) e = hipEventElapsedTime(&a, ev_start(c, k), ev_mid(c, k));
+    if (e == hipSuccess) e = hipEventElapsedTime(&b, ev_mid(c, k), ev_stop(c, k));
+    if (e != hipSuccess) return e;
+    *trace_ms += a; *combine_ms += b;
+  }
+  return hipSuccess;
+}
 
 static int env_int(const char* name, int dflt) {
   const char* v = std::getenv(name);
@@ -114,9 +150,8 @@ static void reset_tuning(mcpt_ctx* c) {
 // collect the timing of the last trial launch (waits for it), decide once both are measured
 static hipError_t collect_tuning(mcpt_ctx* c) {
   if (!c->tune_pending || !c->timed) return hipSuccess;
-  float ms = 0.0f;
-  hipError_t e = hipEventSynchronize(c->ev_mid);
-  if (e == hipSuccess) e = hipEventElapsedTime(&ms, c->ev_start, c->ev_mid);
+  float ms = 0.0f, ms_combine = 0.0f;
+  hipError_t e = sub_launch_ms(c, &ms, &ms_combine);
   if (e != hipSuccess) return e;
   // per-sample times are compared only between launches of the same shape (pixels, passes):
   // a launch of another shape restarts the comparison
@@ -163,9 +198,8 @@ int mcpt_create(int device_ordinal, mcpt_ctx** out) {
   c->leaf_batch = env_int("MCPT_LEAF_BATCH", -1);   // tuning hook (same results for any value)
   c->device = device_ordinal;
   hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipEventCreate(&c->ev_start);
-  if (e == hipSuccess) e = hipEventCreate(&c->ev_mid);
-  if (e == hipSuccess) e = hipEventCreate(&c->ev_stop);
+  if (e == hipSuccess) e = ensure_events(c, 1);
+  if (const char* pb = std::getenv("MCPT_PARTIAL_BYTES")) c->partial_budget = (size_t)std::strtoull(pb, nullptr, 10);
   if (e == hipSuccess) e = hipMalloc(&c->d_events, sizeof(unsigned long long) * MCPT_DEBUG_SLOTS);
   if (e == hipSuccess) e = hipMemset(c->d_events, 0, sizeof(unsigned long long) * MCPT_DEBUG_SLOTS);
   if (e != hipSuccess) { mcpt_destroy(c); return set_err(MCPT_ERR_HIP, "mcpt_create", e); }
@@ -197,9 +231,7 @@ int mcpt_destroy(mcpt_ctx* c) {
   (void)hipFree(c->d_accum);
   (void)hipFree(c->d_events);
   (void)hipFree(c->d_partial);
-  if (c->ev_start) (void)hipEventDestroy(c->ev_start);
-  if (c->ev_mid) (void)hipEventDestroy(c->ev_mid);
-  if (c->ev_stop) (void)hipEventDestroy(c->ev_stop);
+  for (hipEvent_t e : c->evs) (void)hipEventDestroy(e);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
   return MCPT_OK;
@@ -463,23 +495,35 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   p.date = date; p.ior = refract_ind;
   p.n_local_px = (long long)c->n_local_rows * c->W;
   p.n_tiles = ((c->W + 15) / 16) * ((c->n_local_rows + 15) / 16);
-  p.n_segments = 0;
-  if (n_passes > 0) {
-    auto fdiv = [](int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); };
-    int c_first = fdiv(first_pass - 1, mcpt::kPassChunk);
-    int c_last = fdiv(first_pass + n_passes - 2, mcpt::kPassChunk);
-    p.n_segments = c_last - c_first + 1;
+  // The call's pass range is cut at accumulation-chunk boundaries into sub-launches of at
+  // most max_seg segments, so that the segment-sum buffer stays within partial_budget and
+  // the grid within 2^32 work-items (an 84,000-pass 4K call is ~2,600 segments: 261 GB of
+  // segment sums in one launch).  Chunk sums still reach the accumulator in chunk order, so
+  // the result is bit-identical to one launch.
+  auto fdiv = [](int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); };
+  const long long seg_bytes = p.n_local_px * 3 * (long long)sizeof(float);
+  const long long max_items = (1LL << 32) / 256 - 1;
+  if (p.n_tiles > max_items) return set_err(MCPT_ERR_INVALID_ARG, "render target too large for one launch");
+  long long max_seg = seg_bytes > 0 ? (long long)(c->partial_budget / (size_t)seg_bytes) : (1LL << 30);
+  max_seg = std::max(1LL, std::min(max_seg, p.n_tiles > 0 ? max_items / p.n_tiles : max_items));
+  int n_sub = 0;
+  for (long long lo = first_pass, end = (long long)first_pass + n_passes; lo < end; ++n_sub) {
+    const long long c0 = fdiv((int)(lo - 1), mcpt::kPassChunk);
+    lo = std::min(end, (c0 + max_seg) * mcpt::kPassChunk + 1);
   }
-  if (p.n_segments > 1) {
-    size_t need = (size_t)p.n_segments * (size_t)p.n_local_px * 3 * sizeof(float);
-    if (need > c->partial_bytes) {
-      HIP_OR_RETURN(hipStreamSynchronize(c->stream));
-      (void)hipFree(c->d_partial);
-      c->d_partial = nullptr;
-      c->partial_bytes = 0;
-      HIP_OR_RETURN(hipMalloc(&c->d_partial, need));
-      c->partial_bytes = need;
-    }
+  HIP_OR_RETURN(ensure_events(c, std::max(n_sub, 1)));
+  const long long total_seg = n_passes > 0 ? fdiv(first_pass + n_passes - 2, mcpt::kPassChunk) -
+                                                 fdiv(first_pass - 1, mcpt::kPassChunk) + 1
+                                           : 0;
+  const long long segs = std::min(max_seg, total_seg);   // most segments of one sub-launch
+  if (segs > 1 && (size_t)segs * (size_t)seg_bytes > c->partial_bytes) {
+    const size_t need = (size_t)segs * (size_t)seg_bytes;
+    HIP_OR_RETURN(hipStreamSynchronize(c->stream));
+    (void)hipFree(c->d_partial);
+    c->d_partial = nullptr;
+    c->partial_bytes = 0;
+    HIP_OR_RETURN(hipMalloc(&c->d_partial, need));
+    c->partial_bytes = need;
   }
   p.partial = c->d_partial;
   if (count) HIP_OR_RETURN(hipMemsetAsync(c->d_events, 0, sizeof(unsigned long long) * mcpt::EV_COUNT, c->stream));
@@ -490,11 +534,25 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
     c->tune_shape[0] = p.n_local_px;
     c->tune_shape[1] = n_passes;
   }
-  HIP_OR_RETURN(hipEventRecord(c->ev_start, c->stream));
-  HIP_OR_RETURN(mcpt_launch_render(p, count, c->stream));
-  HIP_OR_RETURN(hipEventRecord(c->ev_mid, c->stream));
-  HIP_OR_RETURN(mcpt_launch_combine(p, c->stream));
-  HIP_OR_RETURN(hipEventRecord(c->ev_stop, c->stream));
+  c->n_sub = std::max(n_sub, 1);
+  if (n_sub == 0) {   // no passes: an empty timed interval
+    HIP_OR_RETURN(hipEventRecord(ev_start(c, 0), c->stream));
+    HIP_OR_RETURN(hipEventRecord(ev_mid(c, 0), c->stream));
+    HIP_OR_RETURN(hipEventRecord(ev_stop(c, 0), c->stream));
+  }
+  for (long long lo = first_pass, end = (long long)first_pass + n_passes, k = 0; lo < end; ++k) {
+    const long long c0 = fdiv((int)(lo - 1), mcpt::kPassChunk);
+    const long long hi = std::min(end, (c0 + max_seg) * mcpt::kPassChunk + 1);
+    p.first_pass = (int)lo;
+    p.n_passes = (int)(hi - lo);
+    p.n_segments = fdiv((int)(hi - 2), mcpt::kPassChunk) - (int)c0 + 1;
+    HIP_OR_RETURN(hipEventRecord(ev_start(c, (int)k), c->stream));
+    HIP_OR_RETURN(mcpt_launch_render(p, count, c->stream));
+    HIP_OR_RETURN(hipEventRecord(ev_mid(c, (int)k), c->stream));
+    HIP_OR_RETURN(mcpt_launch_combine(p, c->stream));
+    HIP_OR_RETURN(hipEventRecord(ev_stop(c, (int)k), c->stream));
+    lo = hi;
+  }
   c->timed = true;
   c->pass_count += n_passes;
   if (count) {
@@ -636,6 +694,18 @@ int mcpt_set_walk_exit(mcpt_ctx* c, int lanes) {
   return MCPT_OK;
 }
 
+int mcpt_set_partial_budget(mcpt_ctx* c, size_t bytes) {
+  if (!c) return MCPT_ERR_INVALID_ARG;
+  c->partial_budget = bytes;
+  return MCPT_OK;
+}
+
+int mcpt_last_launch_count(mcpt_ctx* c, int* n_launches) {
+  if (!c || !n_launches) return MCPT_ERR_INVALID_ARG;
+  *n_launches = c->timed ? c->n_sub : 0;
+  return MCPT_OK;
+}
+
 int mcpt_set_leaf_batch(mcpt_ctx* c, int lanes) {
   if (!c || lanes < -1 || lanes > 64) return set_err(MCPT_ERR_INVALID_ARG, "mcpt_set_leaf_batch: bad lane count");
   c->leaf_batch = lanes;
@@ -679,8 +749,8 @@ int mcpt_last_render_ms(mcpt_ctx* c, float* ms) {
   if (!c || !ms) return MCPT_ERR_INVALID_ARG;
   if (!c->timed) return set_err(MCPT_ERR_INVALID_ARG, "no render timed yet");
   HIP_OR_RETURN(hipSetDevice(c->device));
-  HIP_OR_RETURN(hipEventSynchronize(c->ev_stop));
-  HIP_OR_RETURN(hipEventElapsedTime(ms, c->ev_start, c->ev_stop));
+  HIP_OR_RETURN(hipEventSynchronize(ev_stop(c, c->n_sub - 1)));
+  HIP_OR_RETURN(hipEventElapsedTime(ms, ev_start(c, 0), ev_stop(c, c->n_sub - 1)));
   return MCPT_OK;
 }
 
@@ -688,9 +758,7 @@ int mcpt_last_kernel_ms(mcpt_ctx* c, float* trace_ms, float* combine_ms) {
   if (!c || !trace_ms || !combine_ms) return MCPT_ERR_INVALID_ARG;
   if (!c->timed) return set_err(MCPT_ERR_INVALID_ARG, "no render timed yet");
   HIP_OR_RETURN(hipSetDevice(c->device));
-  HIP_OR_RETURN(hipEventSynchronize(c->ev_stop));
-  HIP_OR_RETURN(hipEventElapsedTime(trace_ms, c->ev_start, c->ev_mid));
-  HIP_OR_RETURN(hipEventElapsedTime(combine_ms, c->ev_mid, c->ev_stop));
+  HIP_OR_RETURN(sub_launch_ms(c, trace_ms, combine_ms));
   return MCPT_OK;
 }
 

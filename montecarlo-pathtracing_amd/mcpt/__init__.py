@@ -95,6 +95,8 @@ def _declare(L: ctypes.CDLL) -> None:
         "mcpt_get_walk_exit": (i, [_vp, ip]),
         "mcpt_set_leaf_batch": (i, [_vp, i]),
         "mcpt_get_leaf_batch": (i, [_vp, ip]),
+        "mcpt_set_partial_budget": (i, [_vp, ctypes.c_size_t]),
+        "mcpt_last_launch_count": (i, [_vp, ip]),
         "mcpt_set_stream": (i, [_vp, _vp]),
         "mcpt_synchronize": (i, [_vp]),
         "mcpt_last_render_ms": (i, [_vp, fp]),
@@ -545,6 +547,17 @@ class Renderer:
     def leaf_batch(self) -> int:
         n = ctypes.c_int()
         _check(lib().mcpt_get_leaf_batch(self._h, ctypes.byref(n)), "mcpt_get_leaf_batch")
+        return n.value
+
+    def set_partial_budget(self, nbytes: int) -> None:
+        """mcpt_set_partial_budget: bound of one launch's segment-sum buffer (calls spanning more
+        32-pass chunks are split into launches at chunk boundaries; same bits)."""
+        _check(lib().mcpt_set_partial_budget(self._h, int(nbytes)), "mcpt_set_partial_budget")
+
+    def last_launch_count(self) -> int:
+        """Sub-launches the last render call was split into."""
+        n = ctypes.c_int()
+        _check(lib().mcpt_last_launch_count(self._h, ctypes.byref(n)), "mcpt_last_launch_count")
         return n.value
 
     def traversal(self) -> int:

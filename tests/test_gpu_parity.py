@@ -125,6 +125,31 @@ def test_multi_launch_equals_single(mcpt_mod, renderer):
     assert np.array_equal(one.view(np.uint32), split.view(np.uint32))
 
 
+@pytest.mark.parametrize("budget_segments", [1, 2, 3])
+@pytest.mark.parametrize("first,S", [(1, 200), (20, 150), (7, 33)])
+def test_partial_budget_split_bit_equal(mcpt_mod, oracle_mod, renderer, budget_segments, first, S):
+    """A call spanning more chunks than the segment-sum budget holds runs as several launches
+    cut at chunk boundaries: same bits as one launch and as the oracle, same event counts."""
+    W, H, B = 24, 16, 4
+    ref, ev_ref = _oracle(oracle_mod, 6, W, H, first, S, B)
+    one = _gpu(mcpt_mod, renderer, 6, W, H, first, S, B)
+    assert renderer.last_launch_count() == 1
+    renderer.set_partial_budget(budget_segments * W * H * 12)
+    try:
+        split = _gpu(mcpt_mod, renderer, 6, W, H, first, S, B)
+        chunks = (first + S - 2) // 32 - (first - 1) // 32 + 1
+        assert renderer.last_launch_count() == -(-chunks // budget_segments)
+        tr, cb = renderer.last_kernel_ms()
+        assert tr > 0.0 and cb >= 0.0
+        ipv, iv = mcpt_mod.camera_canonical(W, H)
+        ev = renderer.render_counted(ipv, iv, first, S, 0.0, B, 1.0, 0)
+    finally:
+        renderer.set_partial_budget(1 << 30)
+    assert np.array_equal(one.view(np.uint32), split.view(np.uint32))
+    _compare(split, ref, f"split passes {first}..{first + S - 1}")
+    assert np.array_equal(ev, ev_ref), (ev, ev_ref)
+
+
 @pytest.mark.parametrize("first,S", [(20, 50), (1, 64), (33, 1), (7, 100)])
 def test_pass_segments_vs_oracle(mcpt_mod, oracle_mod, renderer, first, S):
     """Launches spanning several accumulation chunks (segment sums + combine kernel)."""
