@@ -494,7 +494,7 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   p.first_pass = first_pass; p.n_passes = n_passes; p.bounces = bounces; p.variant = variant;
   p.date = date; p.ior = refract_ind;
   p.n_local_px = (long long)c->n_local_rows * c->W;
-  p.n_tiles = ((c->W + 15) / 16) * ((c->n_local_rows + 15) / 16);
+  p.n_tiles = ((c->W + mcpt::kTile - 1) / mcpt::kTile) * ((c->n_local_rows + mcpt::kTile - 1) / mcpt::kTile);
   // The call's pass range is cut at accumulation-chunk boundaries into sub-launches of at
   // most max_seg segments, so that the segment-sum buffer stays within partial_budget and
   // the grid within 2^32 work-items (an 84,000-pass 4K call is ~2,600 segments: 261 GB of
@@ -502,7 +502,7 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   // the result is bit-identical to one launch.
   auto fdiv = [](int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); };
   const long long seg_bytes = p.n_local_px * 3 * (long long)sizeof(float);
-  const long long max_items = (1LL << 32) / 256 - 1;
+  const long long max_items = (1LL << 32) / mcpt::kTileThreads - 1;
   if (p.n_tiles > max_items) return set_err(MCPT_ERR_INVALID_ARG, "render target too large for one launch");
   long long max_seg = seg_bytes > 0 ? (long long)(c->partial_budget / (size_t)seg_bytes) : (1LL << 30);
   max_seg = std::max(1LL, std::min(max_seg, p.n_tiles > 0 ? max_items / p.n_tiles : max_items));

@@ -35,6 +35,13 @@ constexpr int kPassChunk = 32;
 // largest scene render_kernel stages into LDS: 160 KB / 7 workgroups - 19 KB of per-pixel rows
 constexpr int kLdsSceneBytes = 3584;
 constexpr int kPrimF4 = 8;
+// work-item tile edge (pixels): a work item is a kTile x kTile pixel tile for one pass chunk,
+// one lane per pixel, kTile^2 threads per workgroup (16: four 8x8 waves; 8: one wave)
+#ifndef MCPT_TILE
+#define MCPT_TILE 16
+#endif
+constexpr int kTile = MCPT_TILE;
+constexpr int kTileThreads = kTile * kTile;
 
 struct RenderParams {
   const float4* nodes;

@@ -713,14 +713,14 @@ __device__ __forceinline__ int floordiv(int a, int b) { return (a >= 0) ? a / b 
 // SUSPEND: the deep-BVH walk (suspendable walks, batched leaf visits: RenderParams::walk_exit,
 // leaf_batch; walk_run)
 template <bool COUNT, bool WAVE, bool MESH, bool LDSS, bool SUSPEND>
-__global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParams p) {
+__global__ __launch_bounds__(kTileThreads, MCPT_MIN_WAVES) void render_kernel(RenderParams p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int item = blockIdx.x;
   const int tile = item % p.n_tiles, seg = item / p.n_tiles;
-  const int tiles_x = (p.W + 15) >> 4;
-  const int x = (tile % tiles_x) * 16 + (wave & 1) * 8 + (lane & 7);
-  const int lr = (tile / tiles_x) * 16 + (wave >> 1) * 8 + (lane >> 3);
+  const int tiles_x = (p.W + kTile - 1) / kTile;
+  const int x = (tile % tiles_x) * kTile + (wave & 1) * 8 + (lane & 7);
+  const int lr = (tile / tiles_x) * kTile + (wave >> 1) * 8 + (lane >> 3);
   const bool live = x < p.W && lr < p.n_local_rows;   // (no early return: LDS staging barrier)
   const int c0 = floordiv(p.first_pass - 1, kPassChunk) + seg;
   const int pass_begin = max(p.first_pass, c0 * kPassChunk + 1);
@@ -734,9 +734,9 @@ __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParam
     extern __shared__ float4 s_scene[];
     const int n_nodes = (2 << p.depth) - 1, n_leaves = 1 << p.depth;
     const int n4 = 3 * n_nodes + 8 * p.n_prims;
-    for (int i = tid; i < n4; i += 256) s_scene[i] = i < 3 * n_nodes ? p.nodes[i] : p.prims[i - 3 * n_nodes];
+    for (int i = tid; i < n4; i += kTileThreads) s_scene[i] = i < 3 * n_nodes ? p.nodes[i] : p.prims[i - 3 * n_nodes];
     int* s_int = (int*)(s_scene + n4);
-    for (int i = tid; i < n_leaves + p.n_prims; i += 256)
+    for (int i = tid; i < n_leaves + p.n_prims; i += kTileThreads)
       s_int[i] = i < n_leaves ? p.leaves[i] : p.ptype[i - n_leaves];
     __syncthreads();
     s.nodes = s_scene;
@@ -769,8 +769,8 @@ __global__ __launch_bounds__(256, MCPT_MIN_WAVES) void render_kernel(RenderParam
   // (primary hit), 9-11 N / 15-17 P saved across the inner traversal, 12-14 this segment's
   // sum (from 0 in pass order); s_hit0 = primary hit shape << 28 | index (-1: miss).
   // 19 KB per workgroup, + the staged scene (LDSS, <= kLdsSceneBytes): 7 workgroups/CU.
-  __shared__ float s_pix[18][256];
-  __shared__ int s_hit0[256];
+  __shared__ float s_pix[18][kTileThreads];
+  __shared__ int s_hit0[kTileThreads];
   const f3 Dcam0 = normalize3(dir);
   s_pix[0][tid] = Dcam0.x; s_pix[1][tid] = Dcam0.y; s_pix[2][tid] = Dcam0.z;
   s_pix[12][tid] = 0.0f; s_pix[13][tid] = 0.0f; s_pix[14][tid] = 0.0f;   // this segment's sum
@@ -1114,7 +1114,7 @@ hipError_t mcpt_launch_sample(const mcpt::SampleParams& q, hipStream_t stream) {
 hipError_t mcpt_launch_render(const mcpt::RenderParams& p, bool count, hipStream_t stream) {
   const long long items = (long long)p.n_tiles * p.n_segments;
   if (items <= 0) return hipSuccess;
-  dim3 block(256), grid((unsigned)items);
+  dim3 block(mcpt::kTileThreads), grid((unsigned)items);
   const bool wave = p.wave_traversal != 0, mesh = p.n_meshes > 0;
   const bool lds = !mesh && p.lds_scene_bytes > 0;
   // deep-BVH walk kernel: suspendable walks and/or batched leaf visits (walk_run)
