@@ -475,6 +475,13 @@ struct Walk {
   f3 invD;
   int node, level;
   uint32_t pending;
+  // mesh kernels (walk_run_mesh): the instance whose mesh BVH this lane is walking (-1: none),
+  // its mesh id, the mesh walk's node / level / pending mask, and the ray in mesh space
+  int mprim, mnode, mlevel;
+  uint32_t mpending;
+  f3 Om, Dm, invDm;
+  int4 mi;                 // the mesh's (first node, first leaf, depth, first triangle)
+  float4 t0, t1, t2;       // the instance's mesh transform rows
 };
 
 template <bool COUNT, class SR>
@@ -483,6 +490,7 @@ __device__ __forceinline__ void walk_begin(const SR& s, f3 D, Hit& h, Walk& w, E
   h.index = -1; h.dist = kFLTMAX; h.shape = -1; h.dir = -1; h.cull2 = cull_bound_sq(kFLTMAX);
   w.invD = mk(rcp_rn(D.x), rcp_rn(D.y), rcp_rn(D.z));
   w.node = 0; w.level = 0; w.pending = 0;
+  if constexpr (SR::kMesh) w.mprim = -1;
 }
 
 // true: this lane's walk is complete; false: suspended (wave-level early exit).
@@ -544,6 +552,112 @@ __device__ __forceinline__ bool walk_run(const SR& s, f3 O, f3 D, Hit& h, Walk& 
     if (pop && (do_leaf || do_node)) {
       if (w.pending == 0) return true;
       int L = 31 - __builtin_clz(w.pending);
+      w.pending &= ~(1u << L);
+      w.node = ((w.node + 1) >> (w.level - L)) - 2;
+      w.level = L;
+    }
+    if (SUSPEND) {   // wave-uniform
+      const int n = __builtin_popcountll(__ballot(1));
+      if (n <= exit && n < n0) return false;
+    }
+  }
+}
+
+// walk_run for scenes with mesh instances.  The reference runs an instance's whole mesh DFS
+// (Mesh_intersect raytracer_func.frag:642-678) inside the scene DFS's leaf visit; nested that
+// way on the GPU, only the lanes sitting on a mesh leaf walk their (long, divergent) mesh
+// BVHs while the rest of the wave waits (5 % VALU lane utilisation on a 1 M-triangle scene).
+// Here a lane's mesh walk is part of the same loop: each iteration is one scene node, scene
+// leaf, mesh node or mesh leaf step of that lane; a lane reaching a mesh leaf sets up its
+// mesh-space ray (intersect_prim :681-705) and continues in the mesh until its pending mask
+// is empty, then pops the scene stack.  Each lane's sequence of box / primitive / triangle
+// tests is the reference's, in the reference's order (same bits, same event counts).
+template <bool COUNT, bool SUSPEND, class SR>
+__device__ __forceinline__ bool walk_run_mesh(const SR& s, f3 O, f3 D, Hit& h, Walk& w, Ev<COUNT>& ev, int exit) {
+  const int leaf0 = (1 << s.depth) - 1;
+  const int n0 = SUSPEND ? __builtin_popcountll(__ballot(1)) : 0;
+  for (;;) {
+    bool pop = false;   // the scene walk pops its stack this iteration
+    if (w.mprim >= 0) {
+      // one step of the instance's mesh walk (mesh_test's loop body)
+      const int4 mi = w.mi;
+      const float4 t0 = w.t0, t1 = w.t1, t2 = w.t2;
+      const int mleaf0 = (1 << mi.z) - 1;
+      bool mpop = true;
+      if (w.mnode >= mleaf0) {
+        ev.inc(EV_LEAF);
+        const int t = s.mleaves[mi.y + w.mnode - mleaf0];
+        if (t >= 0) tri_test<COUNT>(s, mi.w, t, w.mprim, w.Om, w.Dm, O, t0, t1, t2, h, ev);
+      } else {
+        ev.inc(EV_NODE);
+        const float4* nodes = s.mnodes + (size_t)mi.x * 3;
+        const size_t j = 2 * (size_t)w.mnode + 1;
+        const float4 l0 = nodes[j * 3], r0 = nodes[j * 3 + 3];
+        const bool hl = (COUNT || l0.w != 0.0f) &&
+                        box_test_mesh(l0, nodes[j * 3 + 1], nodes[j * 3 + 2], w.Om, w.Dm, w.invDm, O, t0, t1, t2, h.cull2);
+        const bool hr = (COUNT || r0.w != 0.0f) &&
+                        box_test_mesh(r0, nodes[j * 3 + 4], nodes[j * 3 + 5], w.Om, w.Dm, w.invDm, O, t0, t1, t2, h.cull2);
+        mpop = !(hl || hr);
+        if (hr) {
+          if (hl) w.mpending |= 1u << (w.mlevel + 1);
+          w.mnode = (int)j + 1; w.mlevel++;
+        } else if (hl) {
+          w.mnode = (int)j; w.mlevel++;
+        }
+      }
+      if (mpop) {
+        if (w.mpending == 0) {
+          w.mprim = -1;   // Mesh_intersect done: back to the scene DFS
+          pop = true;
+        } else {
+          const int L = 31 - __builtin_clz(w.mpending);
+          w.mpending &= ~(1u << L);
+          w.mnode = ((w.mnode + 1) >> (w.mlevel - L)) - 2;
+          w.mlevel = L;
+        }
+      }
+    } else if (w.node >= leaf0) {
+      ev.inc(EV_LEAF);
+      pop = true;
+      const int p = s.leaves[w.node - leaf0];
+      if (p >= 0) {
+        const int pt = s.ptype[p];
+        if (pt >= 0 && (pt & 15) == CODE_MESH) {
+          // intersect_prim's transforms, then the mesh walk starts with the next iteration
+          ev.inc(EV_PRIM);
+          ev.inc(EV_MESH);
+          const size_t b = (size_t)p * 8;
+          const float4 r0 = s.prims[b], r1 = s.prims[b + 1], r2 = s.prims[b + 2];
+          w.Om = xpoint(r0, r1, r2, O);
+          w.Dm = wnormalize3(xdir(r0, r1, r2, D));
+          w.invDm = mk(rcp_rn(w.Dm.x), rcp_rn(w.Dm.y), rcp_rn(w.Dm.z));
+          w.mprim = p; w.mi = s.minfo[pt >> 4];
+          w.t0 = s.prims[b + 3]; w.t1 = s.prims[b + 4]; w.t2 = s.prims[b + 5];
+          w.mnode = 0; w.mlevel = 0; w.mpending = 0;
+          pop = false;
+        } else {
+          prim_test<COUNT, false, false>(s, p, O, D, h, ev);
+        }
+      }
+    } else {
+      ev.inc(EV_NODE);
+      const size_t j = 2 * (size_t)w.node + 1;
+      const float4 l0 = s.nodes[j * 3], r0 = s.nodes[j * 3 + 3];
+      const bool hl = (COUNT || l0.w != 0.0f) &&
+                      box_test<false>(l0, s.nodes[j * 3 + 1], s.nodes[j * 3 + 2], O, D, w.invD, h.cull2);
+      const bool hr = (COUNT || r0.w != 0.0f) &&
+                      box_test<false>(r0, s.nodes[j * 3 + 4], s.nodes[j * 3 + 5], O, D, w.invD, h.cull2);
+      pop = !(hl || hr);
+      if (hr) {
+        if (hl) w.pending |= 1u << (w.level + 1);
+        w.node = (int)j + 1; w.level++;
+      } else if (hl) {
+        w.node = (int)j; w.level++;
+      }
+    }
+    if (pop) {
+      if (w.pending == 0) return true;
+      const int L = 31 - __builtin_clz(w.pending);
       w.pending &= ~(1u << L);
       w.node = ((w.node + 1) >> (w.level - L)) - 2;
       w.level = L;
@@ -713,7 +827,14 @@ __device__ __forceinline__ int floordiv(int a, int b) { return (a >= 0) ? a / b 
 // SUSPEND: the deep-BVH walk (suspendable walks, batched leaf visits: RenderParams::walk_exit,
 // leaf_batch; walk_run)
 template <bool COUNT, bool WAVE, bool MESH, bool LDSS, bool SUSPEND>
-__global__ __launch_bounds__(kTileThreads, MCPT_MIN_WAVES) void render_kernel(RenderParams p) {
+// per-lane walks of mesh scenes (walk_run_mesh keeps the mesh walk state, ray in mesh space
+// and instance transform in registers): 4 waves/SIMD, 128 VGPRs (tools/big_mesh_bench.py:
+// 7 waves with that state spills and runs at a third of the speed)
+#ifndef MCPT_MIN_WAVES_MESH
+#define MCPT_MIN_WAVES_MESH 4
+#endif
+__global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH : MCPT_MIN_WAVES) void render_kernel(
+    RenderParams p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int item = blockIdx.x;
@@ -837,7 +958,8 @@ __global__ __launch_bounds__(kTileThreads, MCPT_MIN_WAVES) void render_kernel(Re
         traverse<COUNT, WAVE>(s, O, D, h, ev);
       } else {
         if (!walking) { walk_begin<COUNT>(s, D, h, walk, ev); walking = true; }
-        walking = !walk_run<COUNT, SUSPEND>(s, O, D, h, walk, ev, p.walk_exit, p.leaf_batch);
+        if constexpr (MESH) walking = !walk_run_mesh<COUNT, SUSPEND>(s, O, D, h, walk, ev, p.walk_exit);
+        else walking = !walk_run<COUNT, SUSPEND>(s, O, D, h, walk, ev, p.walk_exit, p.leaf_batch);
         ready = !walking;
       }
     }

@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""Large triangle-mesh scenes ("the only route to HBM-sized scenes").
+
+The mesh test scene of tests/test_meshes.py with its sphere instance replaced by a UV sphere of
+N triangles (10 K ... 1 M: mesh BVH depth 14 ... 20, up to 100 MB of mesh nodes + 24 MB of
+triangles / vertices / normals in HBM), 1920x1080, B 8, per-lane and wave-coherent walks.
+Per size: Msamples/s (kernel time, HIP events), the counting build's algorithmic bytes per
+sample (SURVEY §8d model incl. the mesh events) and the achieved algorithmic GB/s.
+
+    python tools/big_mesh_bench.py [--sizes 10000 100000 1000000] [--spp 32]
+"""
+import argparse
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "montecarlo-pathtracing_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402,F401  (HIP runtime first)
+
+import mcpt  # noqa: E402
+from mcpt import meshes  # noqa: E402
+
+
+def big_mesh_scene(n_tris: int):
+    # uv_sphere(n_lon, n_lat) has 2 n_lon (n_lat - 1) triangles; n_lon = 2 n_lat
+    n_lat = max(3, int(round((n_tris / 4.0) ** 0.5)))
+    v, n, t, bb = meshes.uv_sphere(2 * n_lat, n_lat)
+    T, M = mcpt.Transfo, mcpt.material
+    s = mcpt.Scene()
+    s.add_cube(T.mul(T.translate(0, 0, -51), T.scale(500, 500, 1)), M([0.9, 0.9, 0.9, 1], 0.3, 0.95))
+    mid = s.add_mesh(v, n, t, bb)
+    s.place_mesh(mid, T.mul(T.translate(60, -20, 0), T.scale(45)), M([0.1, 0.9, 0.9, 0.4], 0.7, 0.9))
+    s.place_mesh(mid, T.mul(T.translate(-70, 40, 10), T.scale(35)), M([0.9, 0.3, 0.1, 1], 0.5, 0.8))
+    s.add_sphere(T.mul(T.translate(0, 0, 20), T.scale(20)), M([0.9, 0, 0.9, 0.2], 0.6, 0.7))
+    s.add_oriented_quad(T.mul(T.translate(0, 0, 160), T.rotateX(180), T.scale(70, 70, 1)),
+                        mcpt.light([0.9, 0.9, 0.9, 1], 24))
+    s.finalize()
+    return s, len(t)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sizes", type=int, nargs="+", default=[10_000, 100_000, 1_000_000])
+    ap.add_argument("--spp", type=int, default=32)
+    ap.add_argument("--bounces", type=int, default=8)
+    a = ap.parse_args()
+    W, H, B, S = 1920, 1080, a.bounces, a.spp
+    r = mcpt.Renderer(0)
+    r.set_target(W, H)
+    ipv, iv = mcpt.camera_canonical(W, H)
+    eb = mcpt.Renderer.event_bytes()
+    for n in a.sizes:
+        sc, n_tris = big_mesh_scene(n)
+        r.upload_scene(sc)
+        mb = sc.mesh_buffers()
+        mesh_mb = sum(x.nbytes for x in mb.values()) / 1e6
+        ev = r.render_counted(ipv, iv, 1, S, 0.0, B, 1.0, 0)
+        bps = float((ev.astype(np.float64) * eb).sum() / max(float(ev[6]), 1.0))
+        for mode in (1, 2):
+            r.set_traversal(mode)
+            r.render(ipv, iv, 1, S, 0.0, B, 1.0, 0)   # warm-up
+            ms = []
+            for k in range(2):
+                r.render(ipv, iv, 1 + (k + 1) * S, S, 0.0, B, 1.0, 0)
+                ms.append(r.last_kernel_ms()[0])
+            t = float(np.mean(ms))
+            sps = W * H * S / (t / 1e3)
+            print(json.dumps({"triangles_per_instance": n_tris, "instances": 2, "mesh_buffers_mb": round(mesh_mb, 1),
+                              "traversal": "lane" if mode == 1 else "wave", "spp": S, "bounces": B,
+                              "kernel_ms": round(t, 2), "msamples_s": round(sps / 1e6, 1),
+                              "algorithmic_bytes_per_sample": round(bps, 1),
+                              "algorithmic_gb_s": round(bps * sps / 1e9, 1),
+                              "events_per_sample": {k: round(float(v) / max(float(ev[6]), 1.0), 2)
+                                                    for k, v in zip(mcpt.EVENT_NAMES, ev)}}), flush=True)
+        r.set_traversal(0)
+    r.close()
+
+
+if __name__ == "__main__":
+    main()
