@@ -147,7 +147,8 @@ int mcpt_get_traversal(mcpt_ctx* ctx, int* resolved_mode);
 
 /* Per-lane walks (MCPT_TRAVERSAL_LANE): the wave suspends its BVH walk loop once at most
  * `lanes` lanes are still walking, shades the finished lanes and resumes the rest with
- * their next rays (0 = never suspend; -1 = default: 16 for BVH depth >= 8, else 0).  Same
+ * their next rays (0 = never suspend; -1 = default: 40 with mesh instances, 16 for BVH
+ * depth >= 8, else 0).  Same
  * results for every value; a scheduling knob.  mcpt_get_walk_exit reports the value used. */
 int mcpt_set_walk_exit(mcpt_ctx* ctx, int lanes);
 int mcpt_get_walk_exit(mcpt_ctx* ctx, int* resolved_lanes);

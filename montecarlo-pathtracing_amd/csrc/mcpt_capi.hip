@@ -125,6 +125,10 @@ static int env_int(const char* name, int dflt) {
 // and cost extra rounds when they are short (scenes 1/2/6: -10-30 %), so they are off there.
 static int resolve_walk_exit(const mcpt_ctx* c) {
   if (c->walk_exit >= 0) return c->walk_exit;
+  // mesh scenes: a lane's walk includes its instances' mesh DFSs (walk_run_mesh), long and
+  // very unequal across lanes: leaving the loop once 24 lanes are done more than doubles
+  // throughput (1 M-triangle meshes 173 -> 381 Msamples/s, tools/big_mesh_bench.py)
+  if (c->n_meshes > 0) return 40;
   return c->depth >= 8 ? 16 : 0;
 }
 static int resolve_leaf_batch(const mcpt_ctx* c) {

@@ -46,6 +46,7 @@ def main():
     ap.add_argument("--sizes", type=int, nargs="+", default=[10_000, 100_000, 1_000_000])
     ap.add_argument("--spp", type=int, default=32)
     ap.add_argument("--bounces", type=int, default=8)
+    ap.add_argument("--walk-exit", type=int, nargs="+", default=[-1], help="per-lane walk suspension (mcpt_set_walk_exit)")
     a = ap.parse_args()
     W, H, B, S = 1920, 1080, a.bounces, a.spp
     r = mcpt.Renderer(0)
@@ -59,8 +60,9 @@ def main():
         mesh_mb = sum(x.nbytes for x in mb.values()) / 1e6
         ev = r.render_counted(ipv, iv, 1, S, 0.0, B, 1.0, 0)
         bps = float((ev.astype(np.float64) * eb).sum() / max(float(ev[6]), 1.0))
-        for mode in (1, 2):
+        for mode, wx in [(1, x) for x in a.walk_exit] + [(2, -1)]:
             r.set_traversal(mode)
+            r.set_walk_exit(wx)
             r.render(ipv, iv, 1, S, 0.0, B, 1.0, 0)   # warm-up
             ms = []
             for k in range(2):
@@ -69,13 +71,14 @@ def main():
             t = float(np.mean(ms))
             sps = W * H * S / (t / 1e3)
             print(json.dumps({"triangles_per_instance": n_tris, "instances": 2, "mesh_buffers_mb": round(mesh_mb, 1),
-                              "traversal": "lane" if mode == 1 else "wave", "spp": S, "bounces": B,
+                              "traversal": "lane" if mode == 1 else "wave", "walk_exit": wx, "spp": S, "bounces": B,
                               "kernel_ms": round(t, 2), "msamples_s": round(sps / 1e6, 1),
                               "algorithmic_bytes_per_sample": round(bps, 1),
                               "algorithmic_gb_s": round(bps * sps / 1e9, 1),
                               "events_per_sample": {k: round(float(v) / max(float(ev[6]), 1.0), 2)
                                                     for k, v in zip(mcpt.EVENT_NAMES, ev)}}), flush=True)
         r.set_traversal(0)
+        r.set_walk_exit(-1)
     r.close()
 
 
