@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--spp", type=int, default=32)
     ap.add_argument("--bounces", type=int, default=8)
     ap.add_argument("--walk-exit", type=int, nargs="+", default=[-1], help="per-lane walk suspension (mcpt_set_walk_exit)")
+    ap.add_argument("--leaf-batch", type=int, nargs="+", default=[-1], help="batched leaf visits (mcpt_set_leaf_batch)")
     a = ap.parse_args()
     W, H, B, S = 1920, 1080, a.bounces, a.spp
     r = mcpt.Renderer(0)
@@ -60,9 +61,10 @@ def main():
         mesh_mb = sum(x.nbytes for x in mb.values()) / 1e6
         ev = r.render_counted(ipv, iv, 1, S, 0.0, B, 1.0, 0)
         bps = float((ev.astype(np.float64) * eb).sum() / max(float(ev[6]), 1.0))
-        for mode, wx in [(1, x) for x in a.walk_exit] + [(2, -1)]:
+        for mode, wx, lb in [(1, x, b) for x in a.walk_exit for b in a.leaf_batch] + [(2, -1, -1)]:
             r.set_traversal(mode)
             r.set_walk_exit(wx)
+            r.set_leaf_batch(lb)
             r.render(ipv, iv, 1, S, 0.0, B, 1.0, 0)   # warm-up
             ms = []
             for k in range(2):
@@ -71,7 +73,7 @@ def main():
             t = float(np.mean(ms))
             sps = W * H * S / (t / 1e3)
             print(json.dumps({"triangles_per_instance": n_tris, "instances": 2, "mesh_buffers_mb": round(mesh_mb, 1),
-                              "traversal": "lane" if mode == 1 else "wave", "walk_exit": wx, "spp": S, "bounces": B,
+                              "traversal": "lane" if mode == 1 else "wave", "walk_exit": wx, "leaf_batch": lb, "spp": S, "bounces": B,
                               "kernel_ms": round(t, 2), "msamples_s": round(sps / 1e6, 1),
                               "algorithmic_bytes_per_sample": round(bps, 1),
                               "algorithmic_gb_s": round(bps * sps / 1e9, 1),
@@ -79,6 +81,7 @@ def main():
                                                     for k, v in zip(mcpt.EVENT_NAMES, ev)}}), flush=True)
         r.set_traversal(0)
         r.set_walk_exit(-1)
+        r.set_leaf_batch(-1)
     r.close()
 
 
