@@ -498,7 +498,7 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   p.first_pass = first_pass; p.n_passes = n_passes; p.bounces = bounces; p.variant = variant;
   p.date = date; p.ior = refract_ind;
   p.n_local_px = (long long)c->n_local_rows * c->W;
-  p.n_tiles = ((c->W + mcpt::kTile - 1) / mcpt::kTile) * ((c->n_local_rows + mcpt::kTile - 1) / mcpt::kTile);
+  p.n_tiles = ((c->W + mcpt::kTileW - 1) / mcpt::kTileW) * ((c->n_local_rows + mcpt::kTileH - 1) / mcpt::kTileH);
   // The call's pass range is cut at accumulation-chunk boundaries into sub-launches of at
   // most max_seg segments, so that the segment-sum buffer stays within partial_budget and
   // the grid within 2^32 work-items (an 84,000-pass 4K call is ~2,600 segments: 261 GB of

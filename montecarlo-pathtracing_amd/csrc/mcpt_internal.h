@@ -35,13 +35,21 @@ constexpr int kPassChunk = 32;
 // largest scene render_kernel stages into LDS: 160 KB / 7 workgroups - 19 KB of per-pixel rows
 constexpr int kLdsSceneBytes = 3584;
 constexpr int kPrimF4 = 8;
-// work-item tile edge (pixels): a work item is a kTile x kTile pixel tile for one pass chunk,
-// one lane per pixel, kTile^2 threads per workgroup (16: four 8x8 waves; 8: one wave)
-#ifndef MCPT_TILE
-#define MCPT_TILE 16
+// work-item tile (pixels): a work item is a kTileW x kTileH pixel tile for one pass chunk, one
+// lane per pixel, made of 8x8-pixel waves side by side (kTileW/8 x kTileH/8 of them).
+//   16x16 (MCPT_TILE_W=16 MCPT_TILE_H=16): four waves in a square;
+//   32x8 (default): four waves in one 8-row strip, so in a row-band shard (8-row bands,
+//   mcpt_set_target) all waves of a workgroup lie in one band of the image.
+//   8x8: one wave per workgroup.
+#ifndef MCPT_TILE_W
+#define MCPT_TILE_W 32
 #endif
-constexpr int kTile = MCPT_TILE;
-constexpr int kTileThreads = kTile * kTile;
+#ifndef MCPT_TILE_H
+#define MCPT_TILE_H 8
+#endif
+constexpr int kTileW = MCPT_TILE_W, kTileH = MCPT_TILE_H;
+constexpr int kTileThreads = kTileW * kTileH;
+static_assert(kTileW % 8 == 0 && kTileH % 8 == 0 && kTileThreads <= 1024, "tiles are made of 8x8 waves");
 
 struct RenderParams {
   const float4* nodes;

@@ -9,7 +9,7 @@
 //    a lane whose path terminates immediately regenerates the next pass's path
 //    (persistent-lane regeneration), so a wave runs until its lanes' *sums* of path
 //    lengths are exhausted, not the max path per pass — the 4 material branches and
-//    the 0..B bounce lengths average out.  Work items = (16x16 tile, pass segment), so
+//    the 0..B bounce lengths average out.  Work items = (32x8 tile, pass segment), so
 //    a shard has enough items to fill the chip even at 8-way row-band sharding;
 //  * the bounce loop and the mixed/refraction branch's inner traversal are folded into
 //    ONE traversal site per loop iteration (a 2-phase state machine), so lanes doing an
@@ -817,7 +817,7 @@ __device__ __forceinline__ float schlick(float ior, f3 I, f3 N) {   // :91-98
 // ------------------------------------------------------------------------------------
 __device__ __forceinline__ int floordiv(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
 
-// Work item = (16x16 pixel tile, pass segment).  A segment is the part of the launch's
+// Work item = (32x8 pixel tile of four 8x8 waves, pass segment).  A segment is the part of the launch's
 // pass range inside one accumulation chunk of kPassChunk absolute passes:
 // segments of one pixel are independent items (strong-scaling parallelism beyond one
 // lane per pixel); their sums are combined in chunk order by combine_kernel.
@@ -839,9 +839,9 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH :
   const int lane = tid & 63, wave = tid >> 6;
   const int item = blockIdx.x;
   const int tile = item % p.n_tiles, seg = item / p.n_tiles;
-  const int tiles_x = (p.W + kTile - 1) / kTile;
-  const int x = (tile % tiles_x) * kTile + (wave & 1) * 8 + (lane & 7);
-  const int lr = (tile / tiles_x) * kTile + (wave >> 1) * 8 + (lane >> 3);
+  const int tiles_x = (p.W + kTileW - 1) / kTileW;
+  const int x = (tile % tiles_x) * kTileW + (wave % (kTileW / 8)) * 8 + (lane & 7);
+  const int lr = (tile / tiles_x) * kTileH + (wave / (kTileW / 8)) * 8 + (lane >> 3);
   const bool live = x < p.W && lr < p.n_local_rows;   // (no early return: LDS staging barrier)
   const int c0 = floordiv(p.first_pass - 1, kPassChunk) + seg;
   const int pass_begin = max(p.first_pass, c0 * kPassChunk + 1);
