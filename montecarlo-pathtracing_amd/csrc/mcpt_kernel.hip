@@ -36,6 +36,11 @@
 #ifndef MCPT_MIN_WAVES
 #define MCPT_MIN_WAVES 7
 #endif
+// sky fold (render_kernel): a bounce ray that misses the scene starts the lane's next pass in
+// the same round
+#ifndef MCPT_FOLD_SKY
+#define MCPT_FOLD_SKY 1
+#endif
 
 
 namespace mcpt {
@@ -945,7 +950,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH :
 #endif
     bool done = false;
     f3 res = mk(0.0f, 0.0f, 0.0f);
-    const bool first = !COUNT && bounce == 0 && phase == 0;   // camera ray of this pass
+    bool first = !COUNT && bounce == 0 && phase == 0;   // camera ray of this pass
     bool ready = true;   // this lane's hit record is complete
     if (!run) {
       done = true;   // for(i=0; i<NB_BOUNCES ...) never runs: black
@@ -967,6 +972,35 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH :
     const unsigned long long st_b = __builtin_amdgcn_s_memtime();
     st_t += st_b - st_a;
     st_s -= st_b;
+#endif
+#if MCPT_FOLD_SKY
+    // Sky fold: a bounce ray that left the scene ends its pass here, before the shading
+    // block, and the lane starts its next pass at once with the cached primary hit, so
+    // that one shading block serves both (the pass's camera-ray round, in which this
+    // lane would otherwise only shade while the others traverse, disappears).  Same
+    // per-lane sequence of values: the sky term, the segment sum in pass order, then the
+    // next pass from its seed.
+    if (!COUNT && ready && run && p.variant == 0 && phase == 0 && !first && h.shape < 0) {
+      const float a = gmax(0.0f, D.z);
+      const f3 sky = add(total, mulv(att, gmix3(mk(0.5f, 0.5f, 0.9f), mk(1.0f, 1.0f, 0.8f), a)));
+      s_pix[12][tid] = s_pix[12][tid] + sky.x;
+      s_pix[13][tid] = s_pix[13][tid] + sky.y;
+      s_pix[14][tid] = s_pix[14][tid] + sky.z;
+      ev.inc(EV_SAMPLE);
+      pass++;
+      if (pass < pass_end) {
+        rng = seed_for(((float)x + 0.5f) / (float)p.W, ((float)y + 0.5f) / (float)p.H, pass, p.date);
+        O = Ocam; D = mk(s_pix[0][tid], s_pix[1][tid], s_pix[2][tid]);
+        att = mk(0.8f, 0.8f, 0.8f); total = mk(0.0f, 0.0f, 0.0f);
+        bounce = 0;
+        const int hv = s_hit0[tid];
+        h.shape = hv < 0 ? -1 : hv >> 28;
+        h.index = hv < 0 ? -1 : hv & 0x0FFFFFFF;
+        first = true;
+      } else {
+        ready = false;   // segment finished: the loop ends for this lane
+      }
+    }
 #endif
     if (ready && run) {
       if (p.variant != 0) {
