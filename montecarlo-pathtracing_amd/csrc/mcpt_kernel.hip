@@ -838,7 +838,13 @@ template <bool COUNT, bool WAVE, bool MESH, bool LDSS, bool SUSPEND>
 #ifndef MCPT_MIN_WAVES_MESH
 #define MCPT_MIN_WAVES_MESH 4
 #endif
-__global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH : MCPT_MIN_WAVES) void render_kernel(
+// per-lane walks over scenes read through L1/L2 (not LDS-staged: scenes 3, 5, 7, 8): 6 waves/SIMD
+// leave the walk more registers (profiles/r01_ab35_occupancy_v12.jsonl)
+#ifndef MCPT_MIN_WAVES_L2
+#define MCPT_MIN_WAVES_L2 6
+#endif
+__global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
+                                           : (!WAVE && !LDSS ? MCPT_MIN_WAVES_L2 : MCPT_MIN_WAVES)) void render_kernel(
     RenderParams p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
