@@ -41,6 +41,10 @@
 #ifndef MCPT_FOLD_SKY
 #define MCPT_FOLD_SKY 1
 #endif
+// end fold: emissive hits and hits at bounce B-1 (black) end the pass before the shading block
+#ifndef MCPT_FOLD_END
+#define MCPT_FOLD_END 1
+#endif
 
 
 namespace mcpt {
@@ -986,12 +990,37 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
     // lane would otherwise only shade while the others traverse, disappears).  Same
     // per-lane sequence of values: the sky term, the segment sum in pass order, then the
     // next pass from its seed.
-    if (!COUNT && ready && run && p.variant == 0 && phase == 0 && !first && h.shape < 0) {
-      const float a = gmax(0.0f, D.z);
-      const f3 sky = add(total, mulv(att, gmix3(mk(0.5f, 0.5f, 0.9f), mk(1.0f, 1.0f, 0.8f), a)));
-      s_pix[12][tid] = s_pix[12][tid] + sky.x;
-      s_pix[13][tid] = s_pix[13][tid] + sky.y;
-      s_pix[14][tid] = s_pix[14][tid] + sky.z;
+    //
+    // End fold (MCPT_FOLD_END): the other two path ends known before shading fold the same
+    // way.  An emissive hit (material .z > 0.5) ends the pass with total + its emission
+    // term (montecarlo.frag's `else` branch: no RNG draw, no new ray), and a non-emissive
+    // hit at bounce B-1 ends it black whatever the branch (reflect / diffuse reach bounce
+    // B in this shading, the refraction branch after its inner walk), so neither needs
+    // the shading block.
+    bool fold_end = !COUNT && ready && run && p.variant == 0 && phase == 0 && !first;
+    f3 fres = mk(0.0f, 0.0f, 0.0f);
+    if (fold_end) {
+      if (h.shape < 0) {
+        const float a = gmax(0.0f, D.z);
+        fres = add(total, mulv(att, gmix3(mk(0.5f, 0.5f, 0.9f), mk(1.0f, 1.0f, 0.8f), a)));
+      } else {
+#if MCPT_FOLD_END
+        const float4 m4 = s.prims[(size_t)h.index * 8 + 7];
+        if (!(m4.z <= 0.5f)) {   // the shading block's emissive `else`, NaN included
+          const float4 c4 = s.prims[(size_t)h.index * 8 + 6];
+          fres = add(total, add(muls(mk(c4.x, c4.y, c4.z), 0.1f), muls(muls(muls(att, m4.z), 1.0f - m4.x), c4.w)));
+        } else if (bounce < B - 1) {
+          fold_end = false;
+        }
+#else
+        fold_end = false;
+#endif
+      }
+    }
+    if (fold_end) {
+      s_pix[12][tid] = s_pix[12][tid] + fres.x;
+      s_pix[13][tid] = s_pix[13][tid] + fres.y;
+      s_pix[14][tid] = s_pix[14][tid] + fres.z;
       ev.inc(EV_SAMPLE);
       pass++;
       if (pass < pass_end) {
