@@ -101,6 +101,18 @@ int mcpt_set_flat_face(mcpt_ctx* ctx, int flat_face);
  * Allocates and zeroes the accumulator; pass count reset to 0. */
 int mcpt_set_target(mcpt_ctx* ctx, int W, int H, int band_rows, int world, int rank);
 int mcpt_local_rows(mcpt_ctx* ctx, int* n_local_rows);
+/* Explicit shard: this context renders the n_rows global rows rows[0..n_rows) (distinct, in
+ * [0, H)), local row i = global row rows[i]; the accumulator holds n_rows × W pixels.
+ * Results per pixel do not depend on the partition. */
+int mcpt_set_target_rows(mcpt_ctx* ctx, int W, int H, const int* rows, int n_rows);
+/* The balanced multi-GPU partition: bands of band_rows rows dealt to ranks
+ * period by period with a rotation (period j: rank r takes band j·world + (r+j) mod world),
+ * the rows after the last whole period dealt singly; every rank gets floor(H/world) or
+ * ceil(H/world) rows.  Writes rank's rows (increasing; rows_out may be NULL to query the
+ * count) and their number.  Host-only (no device). */
+int mcpt_balanced_rows(int H, int world, int rank, int band_rows, int* rows_out, int* n_out);
+/* The context's global row ids of its local rows (n_local_rows ints). */
+int mcpt_local_row_ids(mcpt_ctx* ctx, int* rows_out);
 
 /* Accumulate passes first_pass .. first_pass+n_passes-1 into the accumulator (the
  * glDrawArrays loop of montecarlo.cpp:454-466 with blend ONE/ONE).  Summation order

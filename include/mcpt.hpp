@@ -171,6 +171,25 @@ class Renderer {
     W_ = W; H_ = H;
     check(mcpt_local_rows(c_, &rows_), "mcpt_local_rows");
   }
+  // explicit shard: local row i renders global row rows[i]
+  void set_target_rows(int W, int H, const std::vector<int>& rows) {
+    check(mcpt_set_target_rows(c_, W, H, rows.data(), (int)rows.size()), "mcpt_set_target_rows");
+    W_ = W; H_ = H; rows_ = (int)rows.size();
+  }
+  // this rank's rows of the balanced multi-GPU partition (mcpt_balanced_rows)
+  static std::vector<int> balanced_rows(int H, int world, int rank, int band_rows = 8) {
+    int n = 0;
+    check(mcpt_balanced_rows(H, world, rank, band_rows, nullptr, &n), "mcpt_balanced_rows");
+    std::vector<int> rows((size_t)n);
+    check(mcpt_balanced_rows(H, world, rank, band_rows, rows.data(), &n), "mcpt_balanced_rows");
+    return rows;
+  }
+  // global row ids of the local rows
+  std::vector<int> local_row_ids() const {
+    std::vector<int> rows((size_t)rows_);
+    if (rows_) check(mcpt_local_row_ids(c_, rows.data()), "mcpt_local_row_ids");
+    return rows;
+  }
   // numero_pass = first_pass .. first_pass + n_passes - 1, accumulated (blend ONE/ONE)
   void render(const Camera& cam, int first_pass, int n_passes, float date, int bounces, float refract_ind,
               int variant = MCPT_MONTECARLO) {

@@ -62,6 +62,8 @@ struct mcpt_ctx {
   float* d_accum = nullptr;
   size_t accum_bytes = 0;
   int W = 0, H = 0, band_rows = 1, world = 1, rank = 0, n_local_rows = 0;
+  int* d_rows = nullptr;            // global row of each local row (n_local_rows)
+  std::vector<int> rows;
   int pass_count = 0;
   bool has_target = false;
   unsigned long long* d_events = nullptr;
@@ -233,6 +235,7 @@ int mcpt_destroy(mcpt_ctx* c) {
   free_scene(c);
   free_meshes(c);
   (void)hipFree(c->d_accum);
+  (void)hipFree(c->d_rows);
   (void)hipFree(c->d_events);
   (void)hipFree(c->d_partial);
   for (hipEvent_t e : c->evs) (void)hipEventDestroy(e);
@@ -397,20 +400,13 @@ int mcpt_set_flat_face(mcpt_ctx* c, int flat_face) {
   return MCPT_OK;
 }
 
-static int count_local_rows(int H, int band_rows, int world, int rank) {
-  int n = 0;
-  for (int y = 0; y < H; ++y)
-    if ((y / band_rows) % world == rank) ++n;
-  return n;
-}
-
-int mcpt_set_target(mcpt_ctx* c, int W, int H, int band_rows, int world, int rank) {
-  if (!c || W <= 0 || H <= 0 || band_rows <= 0 || world <= 0 || rank < 0 || rank >= world)
-    return set_err(MCPT_ERR_INVALID_ARG, "mcpt_set_target: bad arguments");
+// Shard the frame by explicit row lists: `rows` = the global rows this context renders, in
+// local-row order.  mcpt_set_target (interleaved bands) and mcpt_balanced_rows are row lists.
+static int set_target_rows(mcpt_ctx* c, int W, int H, const int* rows, int n_rows, int band_rows, int world,
+                           int rank) {
   HIP_OR_RETURN(hipSetDevice(c->device));
   HIP_OR_RETURN(hipStreamSynchronize(c->stream));
-  int nl = count_local_rows(H, band_rows, world, rank);
-  size_t bytes = (size_t)nl * W * 3 * sizeof(float);
+  size_t bytes = (size_t)n_rows * W * 3 * sizeof(float);
   if (bytes != c->accum_bytes) {
     (void)hipFree(c->d_accum);
     c->d_accum = nullptr;
@@ -418,9 +414,70 @@ int mcpt_set_target(mcpt_ctx* c, int W, int H, int band_rows, int world, int ran
     if (bytes) HIP_OR_RETURN(hipMalloc(&c->d_accum, bytes));
     c->accum_bytes = bytes;
   }
-  c->W = W; c->H = H; c->band_rows = band_rows; c->world = world; c->rank = rank; c->n_local_rows = nl;
+  if ((size_t)n_rows != c->rows.size() || !c->d_rows) {
+    (void)hipFree(c->d_rows);
+    c->d_rows = nullptr;
+    HIP_OR_RETURN(hipMalloc(&c->d_rows, sizeof(int) * (size_t)std::max(n_rows, 1)));
+  }
+  c->rows.assign(rows, rows + n_rows);
+  if (n_rows) HIP_OR_RETURN(hipMemcpy(c->d_rows, rows, sizeof(int) * (size_t)n_rows, hipMemcpyHostToDevice));
+  c->W = W; c->H = H; c->band_rows = band_rows; c->world = world; c->rank = rank; c->n_local_rows = n_rows;
   c->has_target = true;
   return mcpt_clear_accum(c);
+}
+
+int mcpt_set_target(mcpt_ctx* c, int W, int H, int band_rows, int world, int rank) {
+  if (!c || W <= 0 || H <= 0 || band_rows <= 0 || world <= 0 || rank < 0 || rank >= world)
+    return set_err(MCPT_ERR_INVALID_ARG, "mcpt_set_target: bad arguments");
+  std::vector<int> rows;
+  for (int y = 0; y < H; ++y)
+    if ((y / band_rows) % world == rank) rows.push_back(y);
+  return set_target_rows(c, W, H, rows.data(), (int)rows.size(), band_rows, world, rank);
+}
+
+int mcpt_set_target_rows(mcpt_ctx* c, int W, int H, const int* rows, int n_rows) {
+  if (!c || W <= 0 || H <= 0 || n_rows < 0 || n_rows > H || (n_rows > 0 && !rows))
+    return set_err(MCPT_ERR_INVALID_ARG, "mcpt_set_target_rows: bad arguments");
+  std::vector<char> seen((size_t)H, 0);
+  for (int i = 0; i < n_rows; ++i) {
+    if (rows[i] < 0 || rows[i] >= H || seen[(size_t)rows[i]])
+      return set_err(MCPT_ERR_INVALID_ARG, "mcpt_set_target_rows: rows must be distinct and in [0, H)");
+    seen[(size_t)rows[i]] = 1;
+  }
+  return set_target_rows(c, W, H, rows, n_rows, 0, 0, 0);
+}
+
+int mcpt_balanced_rows(int H, int world, int rank, int band_rows, int* rows_out, int* n_out) {
+  if (H <= 0 || world <= 0 || rank < 0 || rank >= world || band_rows <= 0 || !n_out)
+    return set_err(MCPT_ERR_INVALID_ARG, "mcpt_balanced_rows: bad arguments");
+  // whole periods of `world` bands: in period j, rank r takes band j·world + (r + j) mod world
+  // (each rank gets every band position of a period equally often); the rows after the last
+  // whole period are dealt one at a time, rotated the same way
+  const int periods = (H / band_rows) / world;
+  const int rest0 = periods * world * band_rows;
+  int n = 0;
+  for (int y = 0; y < H; ++y) {
+    int owner;
+    if (y < rest0) {
+      const int b = y / band_rows, j = b / world;
+      owner = ((b % world) - j % world + world) % world;
+    } else {
+      owner = ((y - rest0) + periods) % world;
+    }
+    if (owner == rank) {
+      if (rows_out) rows_out[n] = y;
+      ++n;
+    }
+  }
+  *n_out = n;
+  return MCPT_OK;
+}
+
+int mcpt_local_row_ids(mcpt_ctx* c, int* rows_out) {
+  if (!c || !rows_out) return MCPT_ERR_INVALID_ARG;
+  if (!c->has_target) return MCPT_ERR_NO_TARGET;
+  std::copy(c->rows.begin(), c->rows.end(), rows_out);
+  return MCPT_OK;
 }
 
 int mcpt_local_rows(mcpt_ctx* c, int* n) {
@@ -476,7 +533,7 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   p.nodes = c->d_nodes; p.leaves = c->d_leaves; p.ptype = c->d_ptype; p.prims = c->d_prims;
   p.accum = c->d_accum; p.events = c->d_events;
   corner_rays(invPV, invV, p);
-  p.W = c->W; p.H = c->H; p.band_rows = c->band_rows; p.world = c->world; p.rank = c->rank;
+  p.W = c->W; p.H = c->H; p.rows = c->d_rows;
   p.n_local_rows = c->n_local_rows; p.depth = c->depth; p.n_prims = c->n_prims;
 #ifndef MCPT_LDS_SCENE
 #define MCPT_LDS_SCENE 1

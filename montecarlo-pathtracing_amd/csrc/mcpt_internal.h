@@ -62,7 +62,8 @@ struct RenderParams {
   float ox, oy, oz;             // camera origin (invV · (0,0,0,1))
   float cd[12];                 // 4 normalized corner directions (raytracer.vert:19)
   int W, H;
-  int band_rows, world, rank, n_local_rows;
+  const int* rows;               // global row of each local row (n_local_rows)
+  int n_local_rows;
   long long n_local_px;         // n_local_rows × W
   int n_tiles, n_segments;      // 16x16 tiles of the local rows; pass segments of this launch
   int depth, n_prims;

@@ -853,7 +853,10 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int item = blockIdx.x;
-  const int tile = item % p.n_tiles, seg = item / p.n_tiles;
+  // segment-fastest item order: the pass segments of one tile are consecutive workgroups
+  // (tile-fastest order was 1-12 % slower on one GPU and 7 % on a 1/8-row shard's launch:
+  // profiles/r01_ab42_item_order.jsonl)
+  const int tile = item / p.n_segments, seg = item % p.n_segments;
   const int tiles_x = (p.W + kTileW - 1) / kTileW;
   const int x = (tile % tiles_x) * kTileW + (wave % (kTileW / 8)) * 8 + (lane & 7);
   const int lr = (tile / tiles_x) * kTileH + (wave / (kTileW / 8)) * 8 + (lane >> 3);
@@ -861,7 +864,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
   const int c0 = floordiv(p.first_pass - 1, kPassChunk) + seg;
   const int pass_begin = max(p.first_pass, c0 * kPassChunk + 1);
   const int pass_end = min(p.first_pass + p.n_passes, (c0 + 1) * kPassChunk + 1);
-  const int y = ((lr / p.band_rows) * p.world + p.rank) * p.band_rows + (lr % p.band_rows);
+  const int y = live ? p.rows[lr] : 0;   // this shard's local row -> image row (mcpt_set_target*)
 
   SceneT<MESH, LDSS> s{p.nodes, p.leaves, p.ptype, p.prims, p.depth, p.minfo, p.mnodes, p.mleaves, p.mtris,
                        p.mverts, p.mnorms, p.flat_face};

@@ -79,6 +79,9 @@ def _declare(L: ctypes.CDLL) -> None:
         "mcpt_upload_scene": (i, [_vp, fp, i, fp, ip, i, i]),
         "mcpt_set_target": (i, [_vp, i, i, i, i, i]),
         "mcpt_local_rows": (i, [_vp, ip]),
+        "mcpt_set_target_rows": (i, [_vp, i, i, ip, i]),
+        "mcpt_balanced_rows": (i, [i, i, i, i, ip, ip]),
+        "mcpt_local_row_ids": (i, [_vp, ip]),
         "mcpt_render": (i, [_vp, fp, fp, i, i, f, i, f, i]),
         "mcpt_render_counted": (i, [_vp, fp, fp, i, i, f, i, f, i, _c_u64_p]),
         "mcpt_event_bytes": (i, [i]),
@@ -447,9 +450,19 @@ class Renderer:
         _check(lib().mcpt_local_rows(self._h, ctypes.byref(n)), "mcpt_local_rows")
         self.n_local_rows = n.value
 
+    def set_target_rows(self, W: int, H: int, rows) -> None:
+        """Explicit shard (mcpt_set_target_rows): local row i renders global row rows[i]."""
+        r = np.ascontiguousarray(rows, dtype=np.int32)
+        _check(lib().mcpt_set_target_rows(self._h, int(W), int(H), _ip(r), int(r.size)), "mcpt_set_target_rows")
+        self.W, self.H = int(W), int(H)
+        self.band_rows, self.world, self.rank = 0, 0, 0
+        self.n_local_rows = int(r.size)
+
     def local_row_ids(self) -> np.ndarray:
-        y = np.arange(self.H)
-        return y[(y // self.band_rows) % self.world == self.rank]
+        out = np.zeros(self.n_local_rows, np.int32)
+        if self.n_local_rows:
+            _check(lib().mcpt_local_row_ids(self._h, _ip(out)), "mcpt_local_row_ids")
+        return out.astype(np.int64)
 
     def render(self, invPV, invV, first_pass: int, n_passes: int, date: float = 0.0,
                bounces: int = 3, refract_ind: float = 1.0, variant: int = MONTECARLO) -> None:
@@ -487,7 +500,7 @@ class Renderer:
     def read_image(self) -> np.ndarray:
         """Averaged image (fs_frag: accum / nb, montecarlo.cpp:59-70); single-shard only."""
         acc, n = self.read_accum()
-        if self.world != 1:
+        if self.n_local_rows != self.H:
             raise MCPTError("read_image needs the full frame; gather shards with mcpt.dist")
         return acc / max(n, 1)
 

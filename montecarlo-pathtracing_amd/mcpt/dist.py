@@ -2,10 +2,12 @@
 
 One process per GPU (torch.distributed; backend "nccl" = RCCL over xGMI on ROCm).  Every
 pixel×pass is independent and the RNG seed is a pure function of (screen_tc, pass, date),
-so splitting the frame by rows is bit-identical to one GPU: each rank renders the rows
-``y`` with ``(y // band_rows) % world == rank`` for ALL passes, into a compact local
-accumulator, and rank 0 gathers the shards (one RCCL gather of fp32 RGB rows, padded to
-the largest shard) and scatters them back into frame order.  No collective runs on the
+so splitting the frame by rows is bit-identical to one GPU: each rank renders its rows for
+ALL passes, into a compact local accumulator, and rank 0 gathers the shards (one RCCL
+gather of fp32 RGB rows, padded to the largest shard) and scatters them back into frame
+order.  Partitions: "balanced" (default; mcpt_balanced_rows: 8-row bands dealt with a
+per-period rotation, leftover rows dealt singly, row counts equal within one) and "bands"
+(``(y // band_rows) % world == rank``, mcpt_set_target).  No collective runs on the
 data path of the render itself; the gather is the frame's only exchange step.
 
 The gather/reassembly here is device-agnostic torch code so the N>1 path is covered by
@@ -20,22 +22,51 @@ import torch
 import torch.distributed as dist
 
 
-def local_rows(H: int, band_rows: int, world: int, rank: int) -> np.ndarray:
-    """Global row ids (increasing) owned by `rank` — matches mcpt_set_target."""
+PARTITIONS = ("balanced", "bands")
+
+
+def band_owner(H: int, band_rows: int, world: int) -> np.ndarray:
+    """Owner rank of every row, interleaved bands: band (y // band_rows) % world — mcpt_set_target."""
+    return (np.arange(H) // band_rows) % world
+
+
+def balanced_owner(H: int, band_rows: int, world: int) -> np.ndarray:
+    """Owner rank of every row, balanced partition — mcpt_balanced_rows (include/mcpt.h).
+
+    Whole periods of `world` bands: in period j, rank r takes band j·world + (r + j) % world,
+    so every rank holds every band position of a period equally often (no rank always gets
+    the top band of each period); the rows after the last whole period are dealt one at a
+    time with the same rotation, so row counts differ by at most one.
+    """
     y = np.arange(H)
-    return y[(y // band_rows) % world == rank]
+    periods = (H // band_rows) // world
+    rest0 = periods * world * band_rows
+    b = y // band_rows
+    owner = ((b % world) - (b // world) % world) % world
+    tail = y >= rest0
+    owner[tail] = ((y[tail] - rest0) + periods) % world
+    return owner
 
 
-def max_local_rows(H: int, band_rows: int, world: int) -> int:
-    return max(len(local_rows(H, band_rows, world, r)) for r in range(world))
+def local_rows(H: int, band_rows: int, world: int, rank: int, partition: str = "bands") -> np.ndarray:
+    """Global row ids (increasing) owned by `rank` under `partition` ("bands": mcpt_set_target,
+    "balanced": mcpt_balanced_rows)."""
+    if partition not in PARTITIONS:
+        raise ValueError(f"partition must be one of {PARTITIONS}")
+    owner = (balanced_owner if partition == "balanced" else band_owner)(H, band_rows, world)
+    return np.nonzero(owner == rank)[0]
 
 
-def frame_row_index(H: int, band_rows: int, world: int) -> np.ndarray:
+def max_local_rows(H: int, band_rows: int, world: int, partition: str = "bands") -> int:
+    return max(len(local_rows(H, band_rows, world, r, partition)) for r in range(world))
+
+
+def frame_row_index(H: int, band_rows: int, world: int, partition: str = "bands") -> np.ndarray:
     """For the padded gather buffer [world, max_rows, ...]: flat source index of each frame row."""
-    m = max_local_rows(H, band_rows, world)
+    m = max_local_rows(H, band_rows, world, partition)
     src = np.empty(H, np.int64)
     for r in range(world):
-        rows = local_rows(H, band_rows, world, r)
+        rows = local_rows(H, band_rows, world, r, partition)
         src[rows] = r * m + np.arange(len(rows))
     return src
 
@@ -48,11 +79,11 @@ class FrameGather:
     """
 
     def __init__(self, H: int, W: int, band_rows: int, world: int, rank: int, device: torch.device,
-                 dst: int = 0, group=None, use_gather: bool = True):
+                 dst: int = 0, group=None, use_gather: bool = True, partition: str = "bands"):
         self.H, self.W, self.band_rows, self.world, self.rank = H, W, band_rows, world, rank
-        self.dst, self.group, self.device = dst, group, device
-        self.m = max_local_rows(H, band_rows, world)
-        self.n_local = len(local_rows(H, band_rows, world, rank))
+        self.dst, self.group, self.device, self.partition = dst, group, device, partition
+        self.m = max_local_rows(H, band_rows, world, partition)
+        self.n_local = len(local_rows(H, band_rows, world, rank, partition))
         self.send = torch.zeros((self.m, W, 3), dtype=torch.float32, device=device)
         self.use_gather = use_gather
         if rank == dst or not use_gather:
@@ -60,7 +91,7 @@ class FrameGather:
             self.recv_list = list(self.recv.view(world, self.m, W, 3).unbind(0))
         else:
             self.recv, self.recv_list = None, None
-        self.index = torch.as_tensor(frame_row_index(H, band_rows, world), device=device)
+        self.index = torch.as_tensor(frame_row_index(H, band_rows, world, partition), device=device)
         self.frame = (torch.empty((H, W, 3), dtype=torch.float32, device=device)
                       if rank == dst and world > 1 else None)
 
@@ -88,19 +119,27 @@ class FrameGather:
 
 
 class ShardedRenderer:
-    """mcpt.Renderer for this rank's row bands + the RCCL gather (GPU path)."""
+    """mcpt.Renderer for this rank's rows + the RCCL gather (GPU path).
+
+    partition "balanced" (default): mcpt_balanced_rows — equal row counts (±1) and rotated
+    band positions; "bands": the plain interleaved bands of mcpt_set_target.
+    """
 
     def __init__(self, W: int, H: int, band_rows: int = 8, world: int = 1, rank: int = 0,
-                 local_rank: int = 0, group=None):
+                 local_rank: int = 0, group=None, partition: str = "balanced"):
         import mcpt
         self.device = torch.device("cuda", local_rank)
         self.r = mcpt.Renderer(local_rank)
         # kernels, D2D copy and the collective all run on torch's current stream of this device
         with torch.cuda.device(self.device):
             self.r.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
-        self.r.set_target(W, H, band_rows, world, rank)
+        if partition == "bands":
+            self.r.set_target(W, H, band_rows, world, rank)
+        else:
+            self.r.set_target_rows(W, H, local_rows(H, band_rows, world, rank, partition))
         self.W, self.H, self.band_rows, self.world, self.rank = W, H, band_rows, world, rank
-        self.g = FrameGather(H, W, band_rows, world, rank, self.device, group=group)
+        self.partition = partition
+        self.g = FrameGather(H, W, band_rows, world, rank, self.device, group=group, partition=partition)
 
     def upload_scene(self, scene) -> None:
         self.r.upload_scene(scene)

@@ -25,7 +25,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, W, H, band_rows, use_gather, q):
+def _worker(rank, world, port, W, H, band_rows, use_gather, partition, q):
     import sys
     sys.path.insert(0, REPO)
     sys.path.insert(0, os.path.join(REPO, "montecarlo-pathtracing_amd"))
@@ -37,8 +37,9 @@ def _worker(rank, world, port, W, H, band_rows, use_gather, q):
         prims, nodes, leaves, d, _ = orc.scene(6)
         ipv, iv = orc.camera(W, H)
         full, _ = orc.render(prims, nodes, leaves, d, ipv, iv, W, H, 1, 2, 0.0, 4, 1.0, 0, n_threads=2)
-        rows = local_rows(H, band_rows, world, rank)
-        g = FrameGather(H, W, band_rows, world, rank, torch.device("cpu"), use_gather=use_gather)
+        rows = local_rows(H, band_rows, world, rank, partition)
+        g = FrameGather(H, W, band_rows, world, rank, torch.device("cpu"), use_gather=use_gather,
+                        partition=partition)
         frame = g.gather(torch.from_numpy(np.ascontiguousarray(full[rows])))
         if rank == 0:
             q.put(bool(np.array_equal(frame.numpy().view(np.uint32), full.view(np.uint32))))
@@ -46,13 +47,15 @@ def _worker(rank, world, port, W, H, band_rows, use_gather, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,band_rows,use_gather", [(2, 8, True), (2, 3, False), (3, 4, True)])
-def test_row_band_gather_bit_equal(world, band_rows, use_gather):
+@pytest.mark.parametrize("world,band_rows,use_gather,partition",
+                         [(2, 8, True, "bands"), (2, 3, False, "bands"), (3, 4, True, "bands"),
+                          (2, 8, True, "balanced"), (3, 2, False, "balanced")])
+def test_row_band_gather_bit_equal(world, band_rows, use_gather, partition):
     W, H = 20, 29
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    mp.start_processes(_worker, args=(world, _free_port(), W, H, band_rows, use_gather, q), nprocs=world,
-                       join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(world, _free_port(), W, H, band_rows, use_gather, partition, q),
+                       nprocs=world, join=True, start_method="spawn")
     assert q.get(timeout=60) is True
 
 
@@ -69,3 +72,34 @@ def test_partition_covers_frame():
     # 1080p over 8 ranks: 17 or 16 bands of 8 rows each
     sizes = [len(local_rows(1080, 8, 8, r)) for r in range(8)]
     assert max(sizes) - min(sizes) <= 8
+
+
+def test_balanced_partition():
+    """mcpt_balanced_rows / mcpt.dist balanced partition: a disjoint cover of the frame, row
+    counts within one of each other, every rank holding each band position of a period
+    equally often, and the C ABI's rows equal to the Python restatement."""
+    import ctypes
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "montecarlo-pathtracing_amd"))
+    import mcpt
+    from mcpt.dist import frame_row_index, local_rows, max_local_rows
+    for H, b, w in [(1080, 8, 8), (2160, 8, 8), (1080, 8, 2), (1080, 8, 4), (1080, 8, 3), (53, 4, 3),
+                    (7, 8, 2), (100, 8, 8), (5, 1, 8), (1080, 8, 1)]:
+        per = [local_rows(H, b, w, r, "balanced") for r in range(w)]
+        assert sorted(np.concatenate(per).tolist()) == list(range(H))
+        sizes = [len(x) for x in per]
+        assert max(sizes) - min(sizes) <= 1, (H, b, w, sizes)
+        idx = frame_row_index(H, b, w, "balanced")
+        assert len(set(idx.tolist())) == H and idx.max() < w * max_local_rows(H, b, w, "balanced")
+        periods = (H // b) // w
+        for r in range(w):
+            full = per[r][per[r] < periods * w * b]
+            pos = np.bincount(np.unique(full // b) % w, minlength=w)   # bands per period position
+            assert pos.max() - pos.min() <= 1 or periods < w
+            n = ctypes.c_int()
+            assert mcpt.lib().mcpt_balanced_rows(H, w, r, b, None, ctypes.byref(n)) == 0 and n.value == sizes[r]
+            out = np.zeros(max(n.value, 1), np.int32)
+            assert mcpt.lib().mcpt_balanced_rows(H, w, r, b, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+                                                 ctypes.byref(n)) == 0
+            assert np.array_equal(out[:n.value], per[r])
+    assert mcpt.lib().mcpt_balanced_rows(10, 2, 2, 8, None, ctypes.byref(ctypes.c_int())) != 0

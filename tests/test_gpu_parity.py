@@ -169,6 +169,24 @@ def test_row_band_shards_bit_equal(mcpt_mod, renderer, world, band_rows):
         assert np.array_equal(part.view(np.uint32), full[rows].view(np.uint32))
 
 
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_balanced_shards_bit_equal(mcpt_mod, renderer, world):
+    """mcpt_set_target_rows with the balanced partition (and a reversed row list): each
+    local row equals the full-frame render's row, bit for bit."""
+    from mcpt.dist import local_rows
+    W, H = 40, 53
+    full = _gpu(mcpt_mod, renderer, 6, W, H, 1, 2, 8)
+    ipv, iv = mcpt_mod.camera_canonical(W, H)
+    for rank in range(world):
+        for rows in (local_rows(H, 8, world, rank, "balanced"), local_rows(H, 8, world, rank, "balanced")[::-1]):
+            renderer.set_target_rows(W, H, rows)
+            assert np.array_equal(renderer.local_row_ids(), rows)
+            renderer.render(ipv, iv, 1, 2, 0.0, 8, 1.0, 0)
+            part, n = renderer.read_accum()
+            assert n == 2 and part.shape[0] == len(rows)
+            assert np.array_equal(part.view(np.uint32), full[rows].view(np.uint32))
+
+
 @pytest.mark.parametrize("traversal", TRAVERSALS)
 @pytest.mark.parametrize("scene_id,B", [(6, 8), (8, 12), (7, 8), (1, 3)])
 def test_event_counters_match_oracle(mcpt_mod, oracle_mod, renderer, scene_id, B, traversal):

@@ -9,9 +9,9 @@ wall time around synchronised launches (`wall_ms`):
   C2  scene 6, 1920x1080, 256 spp, B 8  (= bench.py's workload)
   C3  scene 6, 1920x1080, 1024 spp, B 8, IOR 1.5, roughness of every non-emissive primitive
       swept over 0, 0.5, 0.9, 0.99, 1
-  C4  scene 8, 1920x1080, 512 spp, B 12, 8-GPU row bands: each of the 8 shards measured in
+  C4  scene 8, 1920x1080, 512 spp, B 12, 8-GPU balanced row shards: each of the 8 shards measured in
       turn on this GPU (world 8, rank r); projected 8-GPU rate = all samples / slowest shard
-  C5  scene 6, 3840x2160, 8-GPU row bands, progressive: 1024 spp per shard measured (of the
+  C5  scene 6, 3840x2160, 8-GPU balanced row shards, progressive: 1024 spp per shard measured (of the
       84,000 spp target); projected time to 84,000 spp on 8 GPUs from the slowest shard
 Synthetic inputs: the reference scenes built by the C++ scene producer, canonical camera.
 """
@@ -29,6 +29,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402,F401  (HIP runtime first)
 
 import mcpt  # noqa: E402
+from mcpt.dist import local_rows  # noqa: E402
 
 
 def timed_render(r, ipv, iv, first, spp, B, ior, chunk=256):
@@ -125,7 +126,7 @@ def main():
         ipv, iv = mcpt.camera_canonical(W, H)
         shard_ms = []
         for rank in range(8):
-            r.set_target(W, H, 8, 8, rank)
+            r.set_target_rows(W, H, local_rows(H, 8, 8, rank, "balanced"))   # = bench.py's partition
             if rank == 0:
                 tune(r, ipv, iv, B, 1.0)
                 timed_render(r, ipv, iv, 1, 32, B, 1.0)
