@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
-"""BASELINE config C5 at its full target: scene 6, 3840x2160, 84,000 spp, B 8, the 8 row-band
-shards of an 8-GPU run, each rendered on this GPU as ONE mcpt_render call of 84,000 passes
+"""BASELINE config C5 at its full target: scene 6, 3840x2160, 84,000 spp, B 8, the 8 row
+shards of an 8-GPU run (the balanced partition bench.py uses, mcpt_balanced_rows), each rendered on this GPU as ONE mcpt_render call of 84,000 passes
 (the library cuts it into chunk-aligned launches within its segment-sum budget).
 
 Per shard: kernel time (sum over the call's launches, HIP events), wall time of the call,
@@ -23,6 +23,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402,F401  (HIP runtime first)
 
 import mcpt  # noqa: E402
+from mcpt.dist import local_rows  # noqa: E402
 
 W, H, B, WORLD, BAND = 3840, 2160, 8, 8, 8
 
@@ -36,13 +37,13 @@ def main():
     r = mcpt.Renderer(0)
     r.upload_scene(mcpt.Scene.reference(6))
     ipv, iv = mcpt.camera_canonical(W, H)
-    r.set_target(W, H, BAND, WORLD, 0)
+    r.set_target_rows(W, H, local_rows(H, BAND, WORLD, 0, "balanced"))
     # AUTO traversal trials on this launch shape first (same bits either way)
     for _ in range(2):
         r.render(ipv, iv, 1, 256, 0.0, B, 1.0, 0)
     shard_ms = []
     for rank in a.ranks:
-        r.set_target(W, H, BAND, WORLD, rank)
+        r.set_target_rows(W, H, local_rows(H, BAND, WORLD, rank, "balanced"))
         r.synchronize()
         t0 = time.perf_counter()
         r.render(ipv, iv, 1, a.passes, 0.0, B, 1.0, 0)
