@@ -76,15 +76,18 @@ struct mcpt_ctx {
   bool timed = false;
   size_t partial_budget = kDefaultPartialBudget;
   int traversal = MCPT_TRAVERSAL_AUTO;
-  // AUTO traversal: the first two sizeable launches after a scene upload run the per-lane and
-  // the wave-coherent walk once each (kernel time per sample from the launch events), later
-  // launches use the faster one (results are identical either way)
-  int tune_pending = 0;             // mode of the launch whose timing is not collected yet
+  // AUTO schedule: the first sizeable launches after a scene upload run each candidate once
+  // (kernel time per sample from the launch events), later launches use the fastest (results
+  // are identical either way).  Candidates: 1 = per-lane walk, 2 = wave-coherent walk, and
+  // on launches large enough for it (kSeg2Items) 3 = per-lane walk with two pass segments
+  // per work item.
+  int tune_pending = 0;             // candidate of the launch whose timing is not collected yet
   double tune_samples = 0.0;        // samples of that launch
   long long tune_shape[2] = {0, 0};      // (local pixels, passes) of that launch
   long long meas_shape[2] = {0, 0};      // shape the measurements below were taken on
-  double tune_ns[3] = {0.0, 0.0, 0.0};   // ns per sample measured, by mode (same shape)
-  int tune_choice = 0;              // resolved mode once both are measured
+  bool meas_big = false;            // that shape admits candidate 3
+  double tune_ns[4] = {0.0, 0.0, 0.0, 0.0};   // ns per sample measured, by candidate (same shape)
+  int tune_choice = 0;              // resolved candidate once all are measured
   int walk_exit = -1;               // mcpt_set_walk_exit; -1: by BVH depth
   int leaf_batch = -1;              // MCPT_LEAF_BATCH env (tuning); -1: default
 };
@@ -138,18 +141,31 @@ static int resolve_leaf_batch(const mcpt_ctx* c) {
   return c->depth >= 8 ? 8 : 0;
 }
 
-static int resolve_traversal(const mcpt_ctx* c) {
+constexpr int kCandLaneSeg2 = 3;
+// two segments per work item need a grid of >= 16 rounds of resident workgroups at K = 2
+// (256 CUs x 7): below that the grid tail costs more than the lanes' pass-count tails save
+constexpr long long kSeg2Items = 2LL * 16 * 256 * 7;
+
+// schedule candidate of the next launch; `big`: the launch admits candidate 3
+static int resolve_candidate(const mcpt_ctx* c, bool big) {
   if (c->traversal != MCPT_TRAVERSAL_AUTO) return c->traversal;
   if (c->tune_choice) return c->tune_choice;
-  // next trial: the walk not yet timed on the measured launch shape
-  return c->tune_ns[MCPT_TRAVERSAL_LANE] > 0.0 ? MCPT_TRAVERSAL_WAVE : MCPT_TRAVERSAL_LANE;
+  // next trial: the first candidate not yet timed on the measured launch shape
+  if (!(c->tune_ns[MCPT_TRAVERSAL_LANE] > 0.0)) return MCPT_TRAVERSAL_LANE;
+  if (!(c->tune_ns[MCPT_TRAVERSAL_WAVE] > 0.0)) return MCPT_TRAVERSAL_WAVE;
+  return big ? kCandLaneSeg2 : MCPT_TRAVERSAL_LANE;
+}
+static int resolve_traversal(const mcpt_ctx* c) {
+  const int cand = resolve_candidate(c, c->meas_big);
+  return cand == kCandLaneSeg2 ? MCPT_TRAVERSAL_LANE : cand;
 }
 
 static void reset_tuning(mcpt_ctx* c) {
   c->tune_pending = 0;
   c->tune_samples = 0.0;
   c->tune_shape[0] = c->tune_shape[1] = c->meas_shape[0] = c->meas_shape[1] = 0;
-  c->tune_ns[0] = c->tune_ns[1] = c->tune_ns[2] = 0.0;
+  c->meas_big = false;
+  for (double& t : c->tune_ns) t = 0.0;
   c->tune_choice = 0;
 }
 
@@ -162,15 +178,19 @@ static hipError_t collect_tuning(mcpt_ctx* c) {
   // per-sample times are compared only between launches of the same shape (pixels, passes):
   // a launch of another shape restarts the comparison
   if (c->tune_shape[0] != c->meas_shape[0] || c->tune_shape[1] != c->meas_shape[1]) {
-    c->tune_ns[0] = c->tune_ns[1] = c->tune_ns[2] = 0.0;
+    for (double& t : c->tune_ns) t = 0.0;
     c->meas_shape[0] = c->tune_shape[0];
     c->meas_shape[1] = c->tune_shape[1];
   }
   c->tune_ns[c->tune_pending] = (double)ms * 1e6 / c->tune_samples;
   c->tune_pending = 0;
-  if (c->tune_ns[MCPT_TRAVERSAL_LANE] > 0.0 && c->tune_ns[MCPT_TRAVERSAL_WAVE] > 0.0)
-    c->tune_choice = c->tune_ns[MCPT_TRAVERSAL_WAVE] < c->tune_ns[MCPT_TRAVERSAL_LANE] ? MCPT_TRAVERSAL_WAVE
-                                                                                    : MCPT_TRAVERSAL_LANE;
+  const double* t = c->tune_ns;
+  if (t[MCPT_TRAVERSAL_LANE] > 0.0 && t[MCPT_TRAVERSAL_WAVE] > 0.0 && (!c->meas_big || t[kCandLaneSeg2] > 0.0)) {
+    int best = MCPT_TRAVERSAL_LANE;
+    if (t[MCPT_TRAVERSAL_WAVE] < t[best]) best = MCPT_TRAVERSAL_WAVE;
+    if (c->meas_big && t[kCandLaneSeg2] < t[best]) best = kCandLaneSeg2;
+    c->tune_choice = best;
+  }
   return hipSuccess;
 }
 constexpr double kTuneMinSamples = 1 << 24;   // launches smaller than this are not timed
@@ -547,21 +567,29 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   p.mverts = c->d_mverts; p.mnorms = c->d_mnorms; p.n_meshes = c->n_meshes; p.flat_face = c->flat_face;
   HIP_OR_RETURN(collect_tuning(c));
   // (the counting build is not timed: AUTO counts with the per-lane walk)
-  const int mode = count ? (c->traversal == MCPT_TRAVERSAL_AUTO ? MCPT_TRAVERSAL_LANE : c->traversal)
-                         : resolve_traversal(c);
+  p.n_tiles = ((c->W + mcpt::kTileW - 1) / mcpt::kTileW) * ((c->n_local_rows + mcpt::kTileH - 1) / mcpt::kTileH);
+  auto fdiv = [](int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); };
+  const long long total_seg = n_passes > 0 ? fdiv(first_pass + n_passes - 2, mcpt::kPassChunk) -
+                                                 fdiv(first_pass - 1, mcpt::kPassChunk) + 1
+                                           : 0;
+  const bool big = (long long)p.n_tiles * total_seg >= kSeg2Items;
+  const int cand = count ? (c->traversal == MCPT_TRAVERSAL_AUTO ? MCPT_TRAVERSAL_LANE : c->traversal)
+                         : resolve_candidate(c, big);
+  const int mode = cand == kCandLaneSeg2 ? MCPT_TRAVERSAL_LANE : cand;
   p.wave_traversal = (mode == MCPT_TRAVERSAL_WAVE) ? 1 : 0;
   p.walk_exit = resolve_walk_exit(c);
   p.leaf_batch = resolve_leaf_batch(c);
+  // pass segments per work item: candidate 3 of AUTO runs two; MCPT_SEG_PER_ITEM overrides
+  const int env_seg = env_int("MCPT_SEG_PER_ITEM", 0);
+  p.seg_per_item = env_seg > 0 ? env_seg : (cand == kCandLaneSeg2 ? 2 : 1);
   p.first_pass = first_pass; p.n_passes = n_passes; p.bounces = bounces; p.variant = variant;
   p.date = date; p.ior = refract_ind;
   p.n_local_px = (long long)c->n_local_rows * c->W;
-  p.n_tiles = ((c->W + mcpt::kTileW - 1) / mcpt::kTileW) * ((c->n_local_rows + mcpt::kTileH - 1) / mcpt::kTileH);
   // The call's pass range is cut at accumulation-chunk boundaries into sub-launches of at
   // most max_seg segments, so that the segment-sum buffer stays within partial_budget and
   // the grid within 2^32 work-items (an 84,000-pass 4K call is ~2,600 segments: 261 GB of
   // segment sums in one launch).  Chunk sums still reach the accumulator in chunk order, so
   // the result is bit-identical to one launch.
-  auto fdiv = [](int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); };
   const long long seg_bytes = p.n_local_px * 3 * (long long)sizeof(float);
   const long long max_items = (1LL << 32) / mcpt::kTileThreads - 1;
   if (p.n_tiles > max_items) return set_err(MCPT_ERR_INVALID_ARG, "render target too large for one launch");
@@ -573,9 +601,6 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
     lo = std::min(end, (c0 + max_seg) * mcpt::kPassChunk + 1);
   }
   HIP_OR_RETURN(ensure_events(c, std::max(n_sub, 1)));
-  const long long total_seg = n_passes > 0 ? fdiv(first_pass + n_passes - 2, mcpt::kPassChunk) -
-                                                 fdiv(first_pass - 1, mcpt::kPassChunk) + 1
-                                           : 0;
   const long long segs = std::min(max_seg, total_seg);   // most segments of one sub-launch
   if (segs > 1 && (size_t)segs * (size_t)seg_bytes > c->partial_bytes) {
     const size_t need = (size_t)segs * (size_t)seg_bytes;
@@ -590,7 +615,8 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   if (count) HIP_OR_RETURN(hipMemsetAsync(c->d_events, 0, sizeof(unsigned long long) * mcpt::EV_COUNT, c->stream));
   const double samples = (double)p.n_local_px * n_passes;
   if (!count && c->traversal == MCPT_TRAVERSAL_AUTO && !c->tune_choice && samples >= kTuneMinSamples) {
-    c->tune_pending = mode;
+    if (p.n_local_px != c->meas_shape[0] || n_passes != c->meas_shape[1]) c->meas_big = big;
+    c->tune_pending = cand;
     c->tune_samples = samples;
     c->tune_shape[0] = p.n_local_px;
     c->tune_shape[1] = n_passes;

@@ -856,14 +856,20 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
   // segment-fastest item order: the pass segments of one tile are consecutive workgroups
   // (tile-fastest order was 1-12 % slower on one GPU and 7 % on a 1/8-row shard's launch:
   // profiles/r01_ab42_item_order.jsonl)
-  const int tile = item / p.n_segments, seg = item % p.n_segments;
+  // a work item runs K = seg_per_item consecutive segments of its tile (one lane: the pixel's
+  // passes straight through them, each segment's sum written when its chunk ends)
+  const int K = p.seg_per_item > 1 ? p.seg_per_item : 1;
+  const int n_groups = (p.n_segments + K - 1) / K;
+  const int tile = item / n_groups, seg_lo = (item % n_groups) * K;
+  const int seg_n = min(K, p.n_segments - seg_lo);
+  int seg = seg_lo;
   const int tiles_x = (p.W + kTileW - 1) / kTileW;
   const int x = (tile % tiles_x) * kTileW + (wave % (kTileW / 8)) * 8 + (lane & 7);
   const int lr = (tile / tiles_x) * kTileH + (wave / (kTileW / 8)) * 8 + (lane >> 3);
   const bool live = x < p.W && lr < p.n_local_rows;   // (no early return: LDS staging barrier)
-  const int c0 = floordiv(p.first_pass - 1, kPassChunk) + seg;
+  const int c0 = floordiv(p.first_pass - 1, kPassChunk) + seg_lo;
   const int pass_begin = max(p.first_pass, c0 * kPassChunk + 1);
-  const int pass_end = min(p.first_pass + p.n_passes, (c0 + 1) * kPassChunk + 1);
+  const int pass_end = min(p.first_pass + p.n_passes, (c0 + seg_n) * kPassChunk + 1);
   const int y = live ? p.rows[lr] : 0;   // this shard's local row -> image row (mcpt_set_target*)
 
   SceneT<MESH, LDSS> s{p.nodes, p.leaves, p.ptype, p.prims, p.depth, p.minfo, p.mnodes, p.mleaves, p.mtris,
@@ -953,6 +959,25 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
 #ifdef MCPT_STAMPS
   const unsigned long long st_p = __builtin_amdgcn_s_memtime() - st_k0;
 #endif
+  // this segment's sum -> accumulator (one-segment launch) or its segment slot
+  auto flush_sum = [&]() {
+    const size_t px = (size_t)lr * p.W + x;
+    if (p.n_segments == 1) {
+      float* accp = p.accum + px * 3;
+      accp[0] = accp[0] + s_pix[12][tid]; accp[1] = accp[1] + s_pix[13][tid]; accp[2] = accp[2] + s_pix[14][tid];
+    } else {
+      float* part = p.partial + ((size_t)seg * p.n_local_px + px) * 3;
+      part[0] = s_pix[12][tid]; part[1] = s_pix[13][tid]; part[2] = s_pix[14][tid];
+    }
+  };
+  // after pass++: a pass that opens a new chunk closes the previous segment
+  auto next_chunk = [&]() {
+    if (K > 1 && pass < pass_end && floordiv(pass - 1, kPassChunk) * kPassChunk == pass - 1) {
+      flush_sum();
+      seg++;
+      s_pix[12][tid] = 0.0f; s_pix[13][tid] = 0.0f; s_pix[14][tid] = 0.0f;
+    }
+  };
   Walk walk;
   walk.invD = mk(0.0f, 0.0f, 0.0f); walk.node = 0; walk.level = 0; walk.pending = 0;
   bool walking = false;   // a suspended per-lane walk is waiting to be continued
@@ -1026,6 +1051,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
       s_pix[14][tid] = s_pix[14][tid] + fres.z;
       ev.inc(EV_SAMPLE);
       pass++;
+      next_chunk();
       if (pass < pass_end) {
         rng = seed_for(((float)x + 0.5f) / (float)p.W, ((float)y + 0.5f) / (float)p.H, pass, p.date);
         O = Ocam; D = mk(s_pix[0][tid], s_pix[1][tid], s_pix[2][tid]);
@@ -1155,6 +1181,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
       s_pix[14][tid] = s_pix[14][tid] + res.z;
       ev.inc(EV_SAMPLE);
       pass++;
+      next_chunk();
       rng = seed_for(((float)x + 0.5f) / (float)p.W, ((float)y + 0.5f) / (float)p.H, pass, p.date);   // = (u, v)
       O = Ocam; D = mk(s_pix[0][tid], s_pix[1][tid], s_pix[2][tid]);
       att = mk(0.8f, 0.8f, 0.8f); total = mk(0.0f, 0.0f, 0.0f);
@@ -1194,14 +1221,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
     }
   }
 #endif
-  const size_t px = (size_t)lr * p.W + x;
-  if (p.n_segments == 1) {
-    float* accp = p.accum + px * 3;
-    accp[0] = accp[0] + s_pix[12][tid]; accp[1] = accp[1] + s_pix[13][tid]; accp[2] = accp[2] + s_pix[14][tid];
-  } else {
-    float* part = p.partial + ((size_t)seg * p.n_local_px + px) * 3;
-    part[0] = s_pix[12][tid]; part[1] = s_pix[13][tid]; part[2] = s_pix[14][tid];
-  }
+  flush_sum();
 
   if (COUNT) {
 #pragma unroll
@@ -1306,7 +1326,8 @@ hipError_t mcpt_launch_sample(const mcpt::SampleParams& q, hipStream_t stream) {
 // launch wrapper (host)
 // ------------------------------------------------------------------------------------
 hipError_t mcpt_launch_render(const mcpt::RenderParams& p, bool count, hipStream_t stream) {
-  const long long items = (long long)p.n_tiles * p.n_segments;
+  const int K = p.seg_per_item > 1 ? p.seg_per_item : 1;
+  const long long items = (long long)p.n_tiles * ((p.n_segments + K - 1) / K);
   if (items <= 0) return hipSuccess;
   dim3 block(mcpt::kTileThreads), grid((unsigned)items);
   const bool wave = p.wave_traversal != 0, mesh = p.n_meshes > 0;

@@ -8,6 +8,9 @@ import os
 import sys
 
 import pytest
+# torch first: its HIP runtime must be the process's one before libmcpt.so loads (as in
+# bench.py), or torch.cuda finds no device in a session whose first HIP user was libmcpt
+import torch  # noqa: F401,E402
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "montecarlo-pathtracing_amd")

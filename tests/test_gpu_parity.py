@@ -299,3 +299,46 @@ def test_auto_traversal_tuning(mcpt_mod, renderer):
     assert n_a == n_l == 48
     assert np.array_equal(auto.view(np.uint32), lane.view(np.uint32))
 
+
+
+@pytest.mark.parametrize("k", [2, 3, 5])
+@pytest.mark.parametrize("first,S", [(1, 160), (17, 100)])
+def test_segments_per_item_bit_equal(mcpt_mod, oracle_mod, renderer, monkeypatch, k, first, S):
+    """Work items of k consecutive pass segments (MCPT_SEG_PER_ITEM; AUTO's candidate 3 runs
+    k = 2): each segment's sum is written when its chunk ends — bits equal to one segment per
+    item and to the oracle."""
+    ref, _ = _oracle(oracle_mod, 6, 24, 16, first, S, 8)
+    monkeypatch.setenv("MCPT_SEG_PER_ITEM", "1")
+    one = _gpu(mcpt_mod, renderer, 6, 24, 16, first, S, 8, traversal=1)
+    monkeypatch.setenv("MCPT_SEG_PER_ITEM", str(k))
+    for trav in TRAVERSALS:
+        gpu = _gpu(mcpt_mod, renderer, 6, 24, 16, first, S, 8, traversal=trav)
+        assert np.array_equal(gpu.view(np.uint32), one.view(np.uint32)), (k, trav)
+    _compare(one, ref, f"passes {first}..{first + S - 1}, {k} segments per item")
+
+
+def test_auto_schedule_three_candidates(mcpt_mod, renderer):
+    """On a launch large enough for two segments per work item (1080p x 256 passes), AUTO
+    times three candidates (per-lane, wave-coherent, per-lane with two segments per item)
+    before it settles; the image equals a fixed per-lane render."""
+    W, H, S = 1920, 1080, 256
+    ipv, iv = mcpt_mod.camera_canonical(W, H)
+
+    def run(mode):
+        renderer.set_traversal(mode)
+        renderer.upload_scene(mcpt_mod.Scene.reference(6))
+        renderer.set_target(W, H)
+        seen = []
+        for k in range(4):
+            seen.append(renderer.traversal())
+            renderer.render(ipv, iv, 1 + S * k, S, 0.0, 3, 1.0, 0)
+        seen.append(renderer.traversal())
+        acc, n = renderer.read_accum()
+        return acc, n, seen
+
+    auto, n_a, seen = run(0)
+    lane, n_l, _ = run(1)
+    renderer.set_traversal(0)
+    assert seen[:3] == [1, 1, 2] and seen[3] == 1 and seen[4] in (1, 2), seen
+    assert n_a == n_l == 4 * S
+    assert np.array_equal(auto.view(np.uint32), lane.view(np.uint32))

@@ -48,9 +48,9 @@ def timed_render(r, ipv, iv, first, spp, B, ior, chunk=256):
 
 
 def tune(r, ipv, iv, B, ior, chunk=256):
-    """AUTO traversal's two timing trials (after each scene upload), outside the measurements,
+    """AUTO schedule timing trials (after each scene upload), outside the measurements,
     on launches of the measured shape (timed_render's chunk)."""
-    for _ in range(2):
+    for _ in range(3):
         r.render(ipv, iv, 1, chunk, 0.0, B, ior, mcpt.MONTECARLO)
     r.clear_accum()
 

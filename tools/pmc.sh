@@ -5,7 +5,7 @@ set -e
 OUT=$1; shift
 export TMPDIR=/tmp
 mkdir -p "$OUT"
-# two warm-up steps: AUTO traversal's timing trials; the summary reads the timed step's launch
+# warm-up steps; the summary reads the timed step's launch (bench.py runs AUTO's timing trials first)
 ARGS="--steps 1 --warmup 2 --no-cpu-baseline --no-count $*"
 run() {  # name counters...
   local name=$1; shift

@@ -22,7 +22,7 @@ KERNEL = "render_kernel<false"
 
 def load(d):
     """Counters of the LAST path-tracing launch of each pass (the timed step: earlier launches
-    are warm-up, including AUTO traversal's two timing trials, which run other kernels)."""
+    are warm-up, including AUTO's timing trials, which run other kernels)."""
     out = {}
     for f in glob.glob(os.path.join(d, "*", "run_counter_collection.csv")):
         per_dispatch = collections.defaultdict(dict)
