@@ -79,8 +79,7 @@ struct mcpt_ctx {
   // AUTO schedule: the first sizeable launches after a scene upload run each candidate once
   // (kernel time per sample from the launch events), later launches use the fastest (results
   // are identical either way).  Candidates: 1 = per-lane walk, 2 = wave-coherent walk, and
-  // on launches large enough for it (kSeg2Items) 3 = per-lane walk with two pass segments
-  // per work item.
+  // on launches of >= 2 pass segments 3 = per-lane walk with two pass segments per work item.
   int tune_pending = 0;             // candidate of the launch whose timing is not collected yet
   double tune_samples = 0.0;        // samples of that launch
   long long tune_shape[2] = {0, 0};      // (local pixels, passes) of that launch
@@ -142,9 +141,6 @@ static int resolve_leaf_batch(const mcpt_ctx* c) {
 }
 
 constexpr int kCandLaneSeg2 = 3;
-// two segments per work item need a grid of >= 16 rounds of resident workgroups at K = 2
-// (256 CUs x 7): below that the grid tail costs more than the lanes' pass-count tails save
-constexpr long long kSeg2Items = 2LL * 16 * 256 * 7;
 
 // schedule candidate of the next launch; `big`: the launch admits candidate 3
 static int resolve_candidate(const mcpt_ctx* c, bool big) {
@@ -572,7 +568,9 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   const long long total_seg = n_passes > 0 ? fdiv(first_pass + n_passes - 2, mcpt::kPassChunk) -
                                                  fdiv(first_pass - 1, mcpt::kPassChunk) + 1
                                            : 0;
-  const bool big = (long long)p.n_tiles * total_seg >= kSeg2Items;
+  // candidate 3 needs two segments to pair; whether the longer items' grid tail costs more
+  // than the lanes' pass-count tails save depends on the scene and launch: timed, not guessed
+  const bool big = total_seg >= 2;
   const int cand = count ? (c->traversal == MCPT_TRAVERSAL_AUTO ? MCPT_TRAVERSAL_LANE : c->traversal)
                          : resolve_candidate(c, big);
   const int mode = cand == kCandLaneSeg2 ? MCPT_TRAVERSAL_LANE : cand;

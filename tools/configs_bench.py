@@ -127,11 +127,11 @@ def main():
         shard_ms = []
         for rank in range(8):
             r.set_target_rows(W, H, local_rows(H, 8, 8, rank, "balanced"))   # = bench.py's partition
-            if rank == 0:
-                tune(r, ipv, iv, B, 1.0)
+            if rank == 0:   # one call of all S passes per shard, as an N-GPU run makes it
+                tune(r, ipv, iv, B, 1.0, chunk=S)
                 timed_render(r, ipv, iv, 1, 32, B, 1.0)
                 r.clear_accum()
-            kms, wms = timed_render(r, ipv, iv, 1, S, B, 1.0)
+            kms, wms = timed_render(r, ipv, iv, 1, S, B, 1.0, chunk=S)
             shard_ms.append(kms)
             emit({"config": cfg, "scene": sid, "width": W, "height": H, "spp": S, "bounces": B, "world": 8,
                   "rank": rank, "shard_rows": r.n_local_rows, "kernel_ms": round(kms, 3), "wall_ms": round(wms, 3),
