@@ -342,3 +342,12 @@ def test_auto_schedule_three_candidates(mcpt_mod, renderer):
     assert seen[:3] == [1, 1, 2] and seen[3] == 1 and seen[4] in (1, 2), seen
     assert n_a == n_l == 4 * S
     assert np.array_equal(auto.view(np.uint32), lane.view(np.uint32))
+
+
+def test_set_target_rows_rejects_bad_rows(mcpt_mod, renderer):
+    """mcpt_set_target_rows: rows must be distinct and inside [0, H)."""
+    for rows in ([0, 1, 1], [0, 5], [-1, 2]):
+        with pytest.raises(mcpt_mod.MCPTError):
+            renderer.set_target_rows(8, 5, rows)
+    renderer.set_target_rows(8, 5, [4, 0])
+    assert renderer.local_row_ids().tolist() == [4, 0]
