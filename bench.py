@@ -12,9 +12,9 @@ Scene buffers and the framebuffer are resident in HBM before the timed region.
 
 Multi-GPU: weak scaling — per-GPU work fixed at one C2 frame's worth of samples: at N GPUs
 a step accumulates 256·N passes of the 1080p frame (progressive accumulation, as configs
-C4/C5 do), the frame split into interleaved 8-row bands across ranks (each rank: H/N rows
-× 256·N passes = one C2 frame of samples), then one RCCL gather of the fp32 RGB shards to
-rank 0 inside the timed region.  Bit-identical to rendering the same passes on one GPU.
+C4/C5 do), the frame split into balanced row shards across ranks (mcpt_balanced_rows:
+rotated 8-row bands; each rank H/N rows × 256·N passes = one C2 frame of samples), then one
+RCCL gather of the fp32 RGB shards to rank 0 inside the timed region.  Bit-identical to rendering the same passes on one GPU.
 
 Prints ONE JSON line (rank 0) with `roofline` (dominant kernel = the path-tracing
 kernel; achieved = algorithmic bytes per launch, counted exactly by the counting build
@@ -213,7 +213,7 @@ def main():
                 "scene": args.scene, "width": W, "height": H, "spp_per_step": S,
                 "spp_per_gpu_step": args.spp, "bounces": B,
                 "ior": args.ior, "light_intensity": args.light, "variant": "montecarlo.frag",
-                "parallelism": f"row-bands({args.band_rows} rows) x{world} + RCCL gather" if world > 1
+                "parallelism": f"balanced row shards ({args.band_rows}-row bands) x{world} + RCCL gather" if world > 1
                                else "single GPU",
             },
             "kernel_ms": {"trace_avg": round(avg_trace_ms, 3), "combine_avg": round(avg_combine_ms, 3)},
