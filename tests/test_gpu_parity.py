@@ -351,3 +351,19 @@ def test_set_target_rows_rejects_bad_rows(mcpt_mod, renderer):
             renderer.set_target_rows(8, 5, rows)
     renderer.set_target_rows(8, 5, [4, 0])
     assert renderer.local_row_ids().tolist() == [4, 0]
+
+
+def test_empty_and_tiny_shards(mcpt_mod, renderer):
+    """More ranks than rows (H = 5, world = 8): the balanced partition leaves some ranks with no
+    rows; those render nothing and read back an empty accumulator, the others match the frame."""
+    from mcpt.dist import local_rows
+    W, H = 40, 5
+    full = _gpu(mcpt_mod, renderer, 6, W, H, 1, 2, 8)
+    ipv, iv = mcpt_mod.camera_canonical(W, H)
+    for rank in range(8):
+        rows = local_rows(H, 8, 8, rank, "balanced")
+        renderer.set_target_rows(W, H, rows)
+        renderer.render(ipv, iv, 1, 2, 0.0, 8, 1.0, 0)
+        part, n = renderer.read_accum()
+        assert n == 2 and part.shape == (len(rows), W, 3)
+        assert np.array_equal(part.view(np.uint32), full[rows].view(np.uint32))
