@@ -33,8 +33,13 @@ def main():
     ap.add_argument("--passes", type=int, default=84000)
     ap.add_argument("--ranks", type=int, nargs="+", default=list(range(WORLD)))
     ap.add_argument("--no-progressive-check", action="store_true")
+    ap.add_argument("--traversal", type=int, default=0, help="0 AUTO (trials on 256-pass launches), 1 lane, 2 wave")
+    ap.add_argument("--seg-per-item", type=int, default=0, help="> 0: MCPT_SEG_PER_ITEM for every launch")
     a = ap.parse_args()
+    if a.seg_per_item > 0:
+        os.environ["MCPT_SEG_PER_ITEM"] = str(a.seg_per_item)
     r = mcpt.Renderer(0)
+    r.set_traversal(a.traversal)
     r.upload_scene(mcpt.Scene.reference(6))
     ipv, iv = mcpt.camera_canonical(W, H)
     r.set_target_rows(W, H, local_rows(H, BAND, WORLD, 0, "balanced"))
@@ -71,6 +76,7 @@ def main():
         shard_ms.append(wall)
         print(json.dumps(rec), flush=True)
     print(json.dumps({"config": "C5", "summary": True, "spp": a.passes, "ranks": a.ranks,
+                      "traversal": a.traversal, "seg_per_item": a.seg_per_item,
                       "slowest_shard_wall_s": round(max(shard_ms) / 1e3, 2),
                       "shard_balance": round(min(shard_ms) / max(shard_ms), 3),
                       "projected_8gpu_msamples_s": round(W * H * a.passes / max(shard_ms) / 1e3, 1),
