@@ -826,10 +826,12 @@ __device__ __forceinline__ float schlick(float ior, f3 I, f3 N) {   // :91-98
 // ------------------------------------------------------------------------------------
 __device__ __forceinline__ int floordiv(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
 
-// Work item = (32x8 pixel tile of four 8x8 waves, pass segment).  A segment is the part of the launch's
-// pass range inside one accumulation chunk of kPassChunk absolute passes:
-// segments of one pixel are independent items (strong-scaling parallelism beyond one
-// lane per pixel); their sums are combined in chunk order by combine_kernel.
+// Work item = (32x8 pixel tile of four 8x8 waves, group of seg_per_item pass segments).  A
+// segment is the part of the launch's pass range inside one accumulation chunk of kPassChunk
+// absolute passes: segments of one pixel are independent (strong-scaling
+// parallelism beyond one lane per pixel); their sums are combined in chunk order by
+// combine_kernel.  Lanes: one pixel each; a lane whose path ends starts the pixel's next pass
+// in the same loop iteration (sky / end folds below).
 // LDSS: the scene (nodes, primitive records, leaves, type codes: RenderParams::lds_scene_bytes
 // <= kLdsSceneBytes) is copied into the workgroup's LDS first, so the traversal's dependent
 // node loads are LDS reads instead of L1/L2 gathers.
