@@ -79,13 +79,14 @@ struct mcpt_ctx {
   // AUTO schedule: the first sizeable launches after a scene upload run each candidate once
   // (kernel time per sample from the launch events), later launches use the fastest (results
   // are identical either way).  Candidates: 1 = per-lane walk, 2 = wave-coherent walk, and
-  // on launches of >= 2 pass segments 3 = per-lane walk with two pass segments per work item.
+  // per-lane walks with 2 (3, on launches of >= 2 pass segments) or 4 (4, >= 4 segments) pass
+  // segments per work item.
   int tune_pending = 0;             // candidate of the launch whose timing is not collected yet
   double tune_samples = 0.0;        // samples of that launch
   long long tune_shape[2] = {0, 0};      // (local pixels, passes) of that launch
   long long meas_shape[2] = {0, 0};      // shape the measurements below were taken on
-  bool meas_big = false;            // that shape admits candidate 3
-  double tune_ns[4] = {0.0, 0.0, 0.0, 0.0};   // ns per sample measured, by candidate (same shape)
+  int meas_segs = 0;                // pass segments of that shape (which candidates apply)
+  double tune_ns[5] = {0.0, 0.0, 0.0, 0.0, 0.0};   // ns per sample measured, by candidate (same shape)
   int tune_choice = 0;              // resolved candidate once all are measured
   int walk_exit = -1;               // mcpt_set_walk_exit; -1: by BVH depth
   int leaf_batch = -1;              // MCPT_LEAF_BATCH env (tuning); -1: default
@@ -140,27 +141,32 @@ static int resolve_leaf_batch(const mcpt_ctx* c) {
   return c->depth >= 8 ? 8 : 0;
 }
 
-constexpr int kCandLaneSeg2 = 3;
+constexpr int kCandLaneSeg2 = 3, kCandLaneSeg4 = 4;
+// the candidates that apply to a launch of `segs` pass segments
+static bool cand_applies(int cand, long long segs) {
+  return cand <= 2 || (cand == kCandLaneSeg2 && segs >= 2) || (cand == kCandLaneSeg4 && segs >= 4);
+}
+static int cand_seg_per_item(int cand) { return cand == kCandLaneSeg2 ? 2 : cand == kCandLaneSeg4 ? 4 : 1; }
 
-// schedule candidate of the next launch; `big`: the launch admits candidate 3
-static int resolve_candidate(const mcpt_ctx* c, bool big) {
+// schedule candidate of the next launch (`segs`: its pass segments)
+static int resolve_candidate(const mcpt_ctx* c, long long segs) {
   if (c->traversal != MCPT_TRAVERSAL_AUTO) return c->traversal;
   if (c->tune_choice) return c->tune_choice;
-  // next trial: the first candidate not yet timed on the measured launch shape
-  if (!(c->tune_ns[MCPT_TRAVERSAL_LANE] > 0.0)) return MCPT_TRAVERSAL_LANE;
-  if (!(c->tune_ns[MCPT_TRAVERSAL_WAVE] > 0.0)) return MCPT_TRAVERSAL_WAVE;
-  return big ? kCandLaneSeg2 : MCPT_TRAVERSAL_LANE;
+  // next trial: the first applicable candidate not yet timed on the measured launch shape
+  for (int k = 1; k <= kCandLaneSeg4; ++k)
+    if (cand_applies(k, segs) && !(c->tune_ns[k] > 0.0)) return k;
+  return MCPT_TRAVERSAL_LANE;
 }
 static int resolve_traversal(const mcpt_ctx* c) {
-  const int cand = resolve_candidate(c, c->meas_big);
-  return cand == kCandLaneSeg2 ? MCPT_TRAVERSAL_LANE : cand;
+  const int cand = resolve_candidate(c, c->meas_segs);
+  return cand >= kCandLaneSeg2 ? MCPT_TRAVERSAL_LANE : cand;
 }
 
 static void reset_tuning(mcpt_ctx* c) {
   c->tune_pending = 0;
   c->tune_samples = 0.0;
   c->tune_shape[0] = c->tune_shape[1] = c->meas_shape[0] = c->meas_shape[1] = 0;
-  c->meas_big = false;
+  c->meas_segs = 0;
   for (double& t : c->tune_ns) t = 0.0;
   c->tune_choice = 0;
 }
@@ -181,12 +187,14 @@ static hipError_t collect_tuning(mcpt_ctx* c) {
   c->tune_ns[c->tune_pending] = (double)ms * 1e6 / c->tune_samples;
   c->tune_pending = 0;
   const double* t = c->tune_ns;
-  if (t[MCPT_TRAVERSAL_LANE] > 0.0 && t[MCPT_TRAVERSAL_WAVE] > 0.0 && (!c->meas_big || t[kCandLaneSeg2] > 0.0)) {
-    int best = MCPT_TRAVERSAL_LANE;
-    if (t[MCPT_TRAVERSAL_WAVE] < t[best]) best = MCPT_TRAVERSAL_WAVE;
-    if (c->meas_big && t[kCandLaneSeg2] < t[best]) best = kCandLaneSeg2;
-    c->tune_choice = best;
+  bool all = true;
+  int best = MCPT_TRAVERSAL_LANE;
+  for (int k = 1; k <= kCandLaneSeg4; ++k) {
+    if (!cand_applies(k, c->meas_segs)) continue;
+    if (!(t[k] > 0.0)) all = false;
+    else if (t[k] < t[best]) best = k;
   }
+  if (all) c->tune_choice = best;
   return hipSuccess;
 }
 constexpr double kTuneMinSamples = 1 << 24;   // launches smaller than this are not timed
@@ -568,18 +576,18 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   const long long total_seg = n_passes > 0 ? fdiv(first_pass + n_passes - 2, mcpt::kPassChunk) -
                                                  fdiv(first_pass - 1, mcpt::kPassChunk) + 1
                                            : 0;
-  // candidate 3 needs two segments to pair; whether the longer items' grid tail costs more
-  // than the lanes' pass-count tails save depends on the scene and launch: timed, not guessed
-  const bool big = total_seg >= 2;
+  // segment groups need segments to group; whether longer items pay (the lanes' pass-count
+  // tails average out) or cost (longer grid tail) depends on the scene and the launch: timed,
+  // not guessed (profiles/r01_ab44_seg_per_item.jsonl, r01_ab49_seg_groups_tail.jsonl)
   const int cand = count ? (c->traversal == MCPT_TRAVERSAL_AUTO ? MCPT_TRAVERSAL_LANE : c->traversal)
-                         : resolve_candidate(c, big);
-  const int mode = cand == kCandLaneSeg2 ? MCPT_TRAVERSAL_LANE : cand;
+                         : resolve_candidate(c, total_seg);
+  const int mode = cand >= kCandLaneSeg2 ? MCPT_TRAVERSAL_LANE : cand;
   p.wave_traversal = (mode == MCPT_TRAVERSAL_WAVE) ? 1 : 0;
   p.walk_exit = resolve_walk_exit(c);
   p.leaf_batch = resolve_leaf_batch(c);
   // pass segments per work item: candidate 3 of AUTO runs two; MCPT_SEG_PER_ITEM overrides
   const int env_seg = env_int("MCPT_SEG_PER_ITEM", 0);
-  p.seg_per_item = env_seg > 0 ? env_seg : (cand == kCandLaneSeg2 ? 2 : 1);
+  p.seg_per_item = env_seg > 0 ? env_seg : cand_seg_per_item(cand);
   p.first_pass = first_pass; p.n_passes = n_passes; p.bounces = bounces; p.variant = variant;
   p.date = date; p.ior = refract_ind;
   p.n_local_px = (long long)c->n_local_rows * c->W;
@@ -613,7 +621,7 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   if (count) HIP_OR_RETURN(hipMemsetAsync(c->d_events, 0, sizeof(unsigned long long) * mcpt::EV_COUNT, c->stream));
   const double samples = (double)p.n_local_px * n_passes;
   if (!count && c->traversal == MCPT_TRAVERSAL_AUTO && !c->tune_choice && samples >= kTuneMinSamples) {
-    if (p.n_local_px != c->meas_shape[0] || n_passes != c->meas_shape[1]) c->meas_big = big;
+    if (p.n_local_px != c->meas_shape[0] || n_passes != c->meas_shape[1]) c->meas_segs = (int)total_seg;
     c->tune_pending = cand;
     c->tune_samples = samples;
     c->tune_shape[0] = p.n_local_px;

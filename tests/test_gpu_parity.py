@@ -318,9 +318,9 @@ def test_segments_per_item_bit_equal(mcpt_mod, oracle_mod, renderer, monkeypatch
 
 
 def test_auto_schedule_three_candidates(mcpt_mod, renderer):
-    """On a launch large enough for two segments per work item (1080p x 256 passes), AUTO
-    times three candidates (per-lane, wave-coherent, per-lane with two segments per item)
-    before it settles; the image equals a fixed per-lane render."""
+    """On a launch of 8 pass segments (1080p x 256 passes) AUTO times four candidates
+    (per-lane, wave-coherent, per-lane with two and with four segments per work item) before
+    it settles; the image equals a fixed per-lane render."""
     W, H, S = 1920, 1080, 256
     ipv, iv = mcpt_mod.camera_canonical(W, H)
 
