@@ -500,8 +500,10 @@ class Renderer:
     def read_image(self) -> np.ndarray:
         """Averaged image (fs_frag: accum / nb, montecarlo.cpp:59-70); single-shard only."""
         acc, n = self.read_accum()
-        if self.n_local_rows != self.H:
-            raise MCPTError("read_image needs the full frame; gather shards with mcpt.dist")
+        full = self.n_local_rows == self.H and (self.world != 0 or
+                                                np.array_equal(self.local_row_ids(), np.arange(self.H)))
+        if not full:
+            raise MCPTError("read_image needs the full frame in row order; gather shards with mcpt.dist")
         return acc / max(n, 1)
 
     def clear_accum(self) -> None:
