@@ -1,18 +1,27 @@
 #!/bin/bash
-# One GPU-box session: parity tests, smoke, PMC passes (-> profiles/pmc_traffic.json for the
-# bench's `traffic`/`valu` fields), bench, kernel-trace profile, and (full) the N=2 gloo
-# rehearsal.  Every GPU step has its own time limit; the chain stops at the first failure.
-#   tools/gpu_check.sh TAG [full]
+# One GPU-box session: parity tests, smoke, PMC passes of the C2 and C4 bench workloads
+# (-> profiles/pmc_records.json records keyed by libmcpt.so's sha256, which bench.py's
+# roofline reads), bench, kernel-trace profile, and (full) the N=2 gloo rehearsal.  Every GPU
+# step has its own time limit; the chain stops at the first failure.
+#   tools/gpu_check.sh TAG [full|notest]
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/${1:-run}
 mkdir -p $O
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > $O/pytest_gpu.log 2>&1 && echo "pytest ok" &&
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && echo "smoke ok" &&
-bash tools/pmc.sh $O/pmc && echo "pmc ok" &&
-python tools/pmc_summary.py $O/pmc scene6_1920x1080_256spp_B8 $O/pmc_traffic.json > /dev/null &&
-cp $O/pmc_traffic.json profiles/pmc_traffic.json &&
+if [ "${2:-}" != "notest" ]; then
+  timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+    > $O/pytest_gpu.log 2>&1 && echo "pytest ok" &&
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && echo "smoke ok" || exit $?
+fi
+cp profiles/pmc_records.json $O/pmc_records.json 2>/dev/null
+bash tools/pmc.sh $O/pmc && echo "pmc c2 ok" &&
+python tools/pmc_summary.py $O/pmc scene6_1920x1080_256spp_B8 $O/pmc_records.json > /dev/null &&
+bash tools/pmc.sh $O/pmc_c4 --config c4 && echo "pmc c4 ok" &&
+python tools/pmc_summary.py $O/pmc_c4 scene8_1920x1080_512spp_B12 $O/pmc_records.json > /dev/null &&
+cp $O/pmc_records.json profiles/pmc_records.json &&
 timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err && echo "bench ok" && cat $O/bench.json &&
+timeout -k 10 400 python bench.py --config c4 --no-cpu-baseline > $O/bench_c4.json 2> $O/bench_c4.err &&
+echo "bench c4 ok" && cat $O/bench_c4.json &&
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline > $O/prof_bench.json 2> $O/prof.err && echo "prof ok" || exit $?
 [ "${2:-}" = "full" ] || exit 0
 # N>1 path rehearsal on the one GPU: 2 ranks share cuda:0, gloo collectives (RCCL needs

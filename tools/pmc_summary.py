@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise the PMC passes of tools/pmc.sh into profiles/pmc_<tag>.json.
+"""Summarise the PMC passes of tools/pmc.sh into a record of profiles/pmc_records.json.
 
 HBM traffic per launch of the path-tracing kernel, corrected as MI355X_MICROARCH.md
 §HBM prescribes: FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports
@@ -8,16 +8,22 @@ scene records served from L2, so the read side is tiny either way).  The SQ coun
 give the VALU issue picture (SQ_* wave counters are quad-cycle units; GRBM_GUI_ACTIVE is
 summed over the 8 XCDs).
 
-    python tools/pmc_summary.py gpurun_out/pmc_<run> <workload> profiles/pmc_traffic.json
+    python tools/pmc_summary.py gpurun_out/<run>/pmc <workload> profiles/pmc_records.json
+
+The record carries the sha256 of the libmcpt.so that was profiled; bench.py uses a record only
+for that exact build (records of other builds are dropped from the file on merge).
 """
 import collections
 import csv
 import glob
+import hashlib
 import json
 import os
 import sys
 
 KERNEL = "render_kernel<false"
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(REPO, "montecarlo-pathtracing_amd", "mcpt", "libmcpt.so")
 
 
 def load(d):
@@ -48,6 +54,7 @@ def main():
     write_b = c["WRITE_SIZE"] * 1024
     rec = {
         "workload": workload,
+        "lib_sha256": hashlib.sha256(open(LIB, "rb").read()).hexdigest(),
         "kernel": kernel,
         "source": f"rocprofv3 --pmc passes of tools/pmc.sh ({os.path.basename(d.rstrip('/'))})",
         "hbm_bytes_per_launch": fetch_b + write_b,
@@ -69,8 +76,15 @@ def main():
         # fp32 flop upper bound (every lane active): FMA = 2, MUL / ADD = 1
         rec["f32_flop_per_launch_upper"] = 64.0 * (2 * c["SQ_INSTS_VALU_FMA_F32"] + c["SQ_INSTS_VALU_MUL_F32"] +
                                                    c["SQ_INSTS_VALU_ADD_F32"])
+    try:
+        with open(out) as f:
+            recs = json.load(f)["records"]
+    except (OSError, ValueError, KeyError):
+        recs = []
+    recs = [r for r in recs if r.get("lib_sha256") == rec["lib_sha256"] and r.get("workload") != workload]
+    recs.append(rec)
     with open(out, "w") as f:
-        json.dump(rec, f, indent=1)
+        json.dump({"records": recs}, f, indent=1)
     print(json.dumps(rec, indent=1))
 
 
