@@ -50,6 +50,7 @@ def lib() -> ctypes.CDLL:
             "orc_scene_export": (i, [_vp, _fp, _fp, _ip]),
             "orc_camera": (None, [i, i, _fp, _fp]),
             "orc_render": (i, [_fp, i, _fp, _ip, i, _fp, _fp, i, i, i, i, f, i, f, i, i, i, i, _fp, _u64p, _up, _vp]),
+            "orc_render_pixels": (i, [_fp, i, _fp, _ip, i, _fp, _fp, i, i, _ip, i, i, i, f, i, f, i, i, i, _fp]),
             "orc_xxhash32": (ctypes.c_uint, [ctypes.c_uint, ctypes.c_uint, ctypes.c_uint]),
             "orc_srand": (None, [f, f, i, f, _up]),
             "orc_random_floats": (None, [_up, i, _fp]),
@@ -172,6 +173,27 @@ def render(prims, nodes, leaves, depth, invPV, invV, W, H, first_pass=1, n_passe
     if r != 0:
         raise RuntimeError(f"orc_render failed ({r})")
     return accum, ev
+
+
+def render_pixels(prims, nodes, leaves, depth, invPV, invV, W, H, xy, first_pass=1, n_passes=1, date=0.0,
+                  bounces=3, ior=1.0, variant=0, per_pass=False, n_threads=0):
+    """Sums of passes [first_pass, first_pass+n_passes) for an explicit pixel list xy (n × 2 of
+    (x, y), row 0 = bottom); returns n × 3 f32.  per_pass=True blends pass by pass in the
+    reference's order (montecarlo.cpp:450-466); False follows the chunked accumulation contract
+    (bit-equal to render() on the same pixels)."""
+    prims = np.ascontiguousarray(prims, np.float32)
+    nodes = np.ascontiguousarray(nodes, np.float32)
+    leaves = np.ascontiguousarray(leaves, np.int32)
+    invPV = np.ascontiguousarray(invPV, np.float32)
+    invV = np.ascontiguousarray(invV, np.float32)
+    xy = np.ascontiguousarray(np.asarray(xy).reshape(-1, 2), np.int32)
+    out = np.zeros((xy.shape[0], 3), np.float32)
+    r = lib().orc_render_pixels(P(prims), prims.size // 64, P(nodes), P(leaves, _ip), int(depth), P(invPV), P(invV),
+                                int(W), int(H), P(xy, _ip), xy.shape[0], int(first_pass), int(n_passes), float(date),
+                                int(bounces), float(ior), int(variant), int(bool(per_pass)), int(n_threads), P(out))
+    if r != 0:
+        raise RuntimeError(f"orc_render_pixels failed ({r})")
+    return out
 
 
 def xxhash32(x: int, y: int, z: int) -> int:
