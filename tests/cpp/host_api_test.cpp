@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <vector>
 
 #include "mcpt.hpp"
@@ -60,6 +61,63 @@ int main(int argc, char** argv) {
     std::printf("clear + rebuild: %s\n", ok ? "ok" : "FAIL");
     fails += !ok;
   }
+  // RTViewer's ownership (montecarlo.cpp:92-93, 133): a ScenePrimitives the caller owns and a
+  // BVH_GPU_Scene over it; prim_data() / the root BVH's data_BB / data_ind in the reference's
+  // record types carry exactly the flat buffers
+  {
+    mcpt::ScenePrimitives prims;
+    mcpt::BVH_GPU_Scene bvh_scene(prims);
+    scene_4boules(bvh_scene, 1.2f);
+    bvh_scene.finalize();
+    mcpt::BVH_GPU_Scene ref;
+    ref.build_reference(6, 1.2f);
+    std::vector<float> p2, n2;
+    std::vector<int> l2;
+    ref.buffers(p2, n2, l2);
+    const mcpt::PrimData* pd = prims.prim_data();
+    std::vector<mcpt::BB> bbs;
+    std::vector<int> ind;
+    bvh_scene.bvh(bbs, ind);
+    const bool ok = prims.nb() == 6 && &bvh_scene.scene() == &prims &&
+                    same_bits(pd, p2.data(), p2.size() * 4) && bbs.size() * 6 == n2.size() &&
+                    same_bits(bbs.data(), n2.data(), n2.size() * 4) && ind == l2 &&
+                    pd[0].mat_info[2] > 0.0f && pd[0].type_[0] == 5.0f;   // emissive quad first
+    std::printf("BVH_GPU_Scene(ScenePrimitives&) + PrimData/BB records == reference build: %s\n", ok ? "ok" : "MISMATCH");
+    fails += !ok;
+  }
+  // add_mesh / place_mesh (gpu_bvh_scene.h:84-92) through mcpt.hpp
+  {
+    auto m = std::make_shared<mcpt::Mesh>();
+    for (int j = 0; j < 3; ++j)
+      for (int i = 0; i < 3; ++i) {
+        m->vertices_.push_back(mcpt::GLVec3((float)i - 1.0f, (float)j - 1.0f, 0.0f));
+        m->normals_.push_back(mcpt::GLVec3(0.0f, 0.0f, 1.0f));
+      }
+    for (int j = 0; j < 2; ++j)
+      for (int i = 0; i < 2; ++i) {
+        const unsigned a = (unsigned)(j * 3 + i);
+        for (unsigned v : {a, a + 1, a + 3, a + 1, a + 4, a + 3}) m->tri_indices.push_back(v);
+      }
+    mcpt::ScenePrimitives prims;
+    mcpt::BVH_GPU_Scene s(prims);
+    const int id = s.add_mesh(m);
+    s.place_mesh(id, Transfo::translate(0, 0, 10) * Transfo::scale(30), Material(BLANC, 0.2f, 0.5f));
+    s.place_mesh(id, Transfo::translate(60, 0, 10) * Transfo::scale(20), Material(ROUGE));
+    s.add_orientedQuad(Transfo::translate(0, 0, 100) * Transfo::scale(20, 20, 1), Material::light(BLANC, 10));
+    s.finalize();
+    bool threw = false;
+    try {
+      auto bad = std::make_shared<mcpt::Mesh>();
+      bad->vertices_ = m->vertices_;   // no normals
+      bad->tri_indices = m->tri_indices;
+      s.add_mesh(bad);
+    } catch (const mcpt::Error&) {
+      threw = true;
+    }
+    const bool ok = id == 0 && s.nb_meshes() == 1 && s.nb_prim() == 3 && s.nb_emissives() == 1 && threw;
+    std::printf("add_mesh + place_mesh: %s\n", ok ? "ok" : "FAIL");
+    fails += !ok;
+  }
   // errors surface as mcpt::Error with the C status
   try {
     mcpt::BVH_GPU_Scene s;
@@ -81,6 +139,26 @@ int main(int argc, char** argv) {
     for (float v : img) sum += v;
     std::printf("gpu image sum %.6f\n", sum);
     fails += !(std::isfinite(sum) && sum > 0);
+    // the reference's own arrays passed straight through (INTEGRATION.md adapter):
+    // ScenePrimitives::prim_data() + BVH_KDtree::data_BB()/data_ind()/depth()
+    std::vector<float> acc1, acc2;
+    const int n1 = r.read_accum(acc1);
+    mcpt::ScenePrimitives prims;
+    mcpt::BVH_GPU_Scene s2(prims);
+    scene_4boules(s2, 1.2f);
+    s2.finalize();
+    std::vector<mcpt::BB> bbs;
+    std::vector<int> ind;
+    s2.bvh(bbs, ind);
+    std::vector<mcpt::PrimData> pd(prims.prim_data(), prims.prim_data() + prims.nb());
+    mcpt::Renderer r2(0);
+    r2.upload(pd.data(), (int)pd.size(), bbs.data(), ind.data(), s2.depth(), s2.nb_emissives());
+    r2.set_target(64, 48);
+    r2.render(mcpt::Camera::canonical(64, 48), 1, 4, 0.0f, 8, 1.0f);
+    const int n2 = r2.read_accum(acc2);
+    const bool same = n1 == n2 && acc1.size() == acc2.size() && same_bits(acc1.data(), acc2.data(), acc1.size() * 4);
+    std::printf("gpu reference-layout upload bit-equal: %s\n", same ? "ok" : "MISMATCH");
+    fails += !same;
   }
   return fails ? 1 : 0;
 }

@@ -24,7 +24,7 @@ def host_test_bin(tmp_path_factory, mcpt_mod):
 def test_cpp_scene_api_matches_reference_build(host_test_bin):
     r = subprocess.run([host_test_bin], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert r.stdout.count(": ok") >= 4, r.stdout
+    assert r.stdout.count(": ok") >= 6, r.stdout
 
 
 def test_transfo_matches_scene_producer(mcpt_mod):
@@ -102,6 +102,7 @@ def test_cpp_host_renders_on_gpu(host_test_bin):
     r = subprocess.run([host_test_bin, "gpu"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "gpu image sum" in r.stdout
+    assert "gpu reference-layout upload bit-equal: ok" in r.stdout, r.stdout
 
 
 @pytest.mark.gpu
