@@ -8,6 +8,10 @@
    (double product + TwoSum + midpoint fix-up), so the vectors are bit-exact.
 2. img_s{scene}_v{variant}.npy — small accumulator images rendered by the C++ oracle
    (regression pins for the oracle and direct fixtures for the GPU tests).
+3. paths.npz (`python gen_golden.py paths`) — 320 whole samples of the integrator
+   ((pixel, pass) at 1080p on scenes 1, 6 at IOR 1.0 and 1.5, 8, and a scene with the pure
+   refraction branch) from the same independent numpy restatement extended to the camera
+   ray, the BVH DFS, intersection_info and random_path, with the branch sequence each took.
 
 The reference itself cannot run here (no GL 4.3 / Eigen / GLFW / assimp):
 parity with the executed GLSL is unpinned; these fixtures pin the restatement.
@@ -229,20 +233,23 @@ EPS = f32(1e-10)
 FMAX = f32(3.402823e38)
 
 
-def intersect_prim(rec, Ow, Dw):
+def intersect_prim(rec, Ow, Dw, best=None, index=0):
+    """intersect_prim :681-705 on one primitive record; `best` is the closest_intersection
+    record shared along a traversal (a fresh one when None)."""
     rec = np.asarray(rec, np.float32)
     t = int(rec[48])
     inv, trf = rec[16:32], rec[0:16]
     O = xpoint(inv, Ow)
     D = normalize(xdir(inv, Dw))
-    best = {"shape": -1, "dist": FMAX, "dir": -1, "pl": [f32(0)] * 3, "pg": [f32(0)] * 3}
+    if best is None:
+        best = {"shape": -1, "dist": FMAX, "dir": -1, "pl": [f32(0)] * 3, "pg": [f32(0)] * 3, "index": -1}
 
     def cand(a, shape, d):
         Pl = vadd(O, vmul(D, a))
         Pg = xpoint(trf, Pl)
         dist = length(vsub([f32(v) for v in Ow], Pg))
         if dist < best["dist"]:
-            best.update(shape=shape, dist=dist, dir=d, pl=Pl, pg=Pg)
+            best.update(shape=shape, dist=dist, dir=d, pl=Pl, pg=Pg, index=index)
 
     if t == 1:
         OO, OD, D2 = dot3(O, O), dot3(O, D), dot3(D, D)
@@ -321,6 +328,242 @@ def intersect_prim(rec, Ow, Dw):
         if tl < FMAX:
             cand(tl, 4, cl)
     return best
+
+
+# ----------------------------------------------------------------------------------
+# one whole sample of the integrator, for the path KATs (paths.npz): the camera ray
+# (shaders/raytracer.vert:9-22 + strip interpolation), intersect_bvh's DFS
+# (raytracer_func.frag:734-769) with intersect_bv (:314-352), intersection_info (:812-897)
+# and random_path (tp/montecarlo.frag:100-179), written from the GLSL text and the
+# arithmetic contract of DESIGN.md §3 (binary32 round-to-nearest, no contraction except the
+# fma chains of dot / mat·vec, box-test divisions as correctly rounded reciprocals hoisted to
+# node upload and ray set-up, GLSL builtins by their definitions) — not from oracle.cpp.
+# ----------------------------------------------------------------------------------
+BIAS = f32(1e-2)
+
+
+def rcp(x):
+    return f32(f32(1.0) / f32(x))
+
+
+def glsl_mix(x, y, a):                       # x·(1−a) + y·a
+    return f32(f32(f32(x) * f32(f32(1.0) - f32(a))) + f32(f32(y) * f32(a)))
+
+
+def glsl_reflect(I, N):                      # I − 2·dot(N,I)·N
+    d2 = f32(f32(2.0) * dot3(N, I))
+    return [f32(I[k] - f32(d2 * N[k])) for k in range(3)]
+
+
+def glsl_refract(I, N, eta):                 # GLSL 4.30 §8.5
+    eta = f32(eta)
+    d = dot3(N, I)
+    k = f32(f32(1.0) - f32(f32(eta * eta) * f32(f32(1.0) - f32(d * d))))
+    if k < 0:
+        return [f32(0.0)] * 3
+    t = f32(f32(eta * d) + f32(np.sqrt(k)))
+    return [f32(f32(eta * I[c]) - f32(t * N[c])) for c in range(3)]
+
+
+def r_schlick(ior, I, N):                    # tp/montecarlo.frag:91-98
+    ior = f32(ior)
+    r0 = f32(f32(ior - f32(1.0)) / f32(ior + f32(1.0)))
+    r0 = f32(r0 * r0)
+    x = f32(f32(1.0) - dot3(N, I))
+    v = f32(f32(1.0) - r0)
+    for _ in range(5):
+        v = f32(v * x)
+    v = f32(r0 + v)
+    return min(max(v, f32(0.0)), f32(1.0))
+
+
+def node_boxes(nodes):
+    """intersect_bv's centre and half-width (bbmin+bbmax)/2, 0.5·(bbmax−bbmin) per node, and the
+    hoisted 1/half-width (contract §3.5)."""
+    out = []
+    for b in np.asarray(nodes, np.float32).reshape(-1, 6):
+        c = [f32(f32(b[k] + b[3 + k]) / f32(2.0)) for k in range(3)]
+        w = [f32(f32(0.5) * f32(b[3 + k] - b[k])) for k in range(3)]
+        with np.errstate(divide="ignore"):
+            iw = [rcp(v) for v in w]
+        out.append((c, w, iw))
+    return out
+
+
+def intersect_bv(box, O, D, invD, closest_dist):
+    c, w, iw = box
+    with np.errstate(invalid="ignore", over="ignore"):
+        Oi = [f32(f32(O[k] - c[k]) * iw[k]) for k in range(3)]
+        Di = [f32(D[k] * iw[k]) for k in range(3)]
+        if all(abs(Oi[k]) < 1 for k in range(3)):
+            return True
+        al = FMAX
+        for fc in range(6):
+            c0 = fc // 2
+            if abs(Di[c0]) > EPS:
+                c1, c2 = (c0 + 1) % 3, (c0 + 2) % 3
+                cd = f32(-1.0 + 2.0 * (fc % 2))
+                a = f32(f32(cd - Oi[c0]) * f32(invD[c0] * w[c0]))      # (cd − Oi)/Di
+                if a > EPS and abs(f32(Oi[c1] + f32(a * Di[c1]))) <= 1 and abs(f32(Oi[c2] + f32(a * Di[c2]))) <= 1:
+                    if a < al:
+                        al = a
+        if al < FMAX:
+            Pg = [f32(f32(f32(f32(al * Di[k]) + Oi[k]) * w[k]) + c[k]) for k in range(3)]
+            return length(vsub(O, Pg)) <= closest_dist
+    return False
+
+
+def intersect_bvh(prims, boxes, leaves, depth, O, D, stats=None):
+    """traverse_all_bvh: the literal stack of :734-769 (right child popped first)."""
+    best = {"shape": -1, "dist": FMAX, "dir": -1, "pl": [f32(0)] * 3, "pg": [f32(0)] * 3, "index": -1}
+    with np.errstate(divide="ignore"):
+        invD = [rcp(D[k]) for k in range(3)]
+    max_line = 2 ** depth - 1
+    stack = [0]
+    while stack:
+        i = stack.pop()
+        if i >= max_line:
+            p = int(leaves[i - max_line])
+            if p >= 0:
+                if int(prims[p][48]) not in (1, 2, 3, 5):
+                    raise NotImplementedError("path KATs cover sphere / cube / cylinder / quad scenes")
+                intersect_prim(prims[p], O, D, best, p)
+        else:
+            if stats is not None:
+                stats["node"] += 1
+            j = 2 * i + 1
+            if intersect_bv(boxes[j], O, D, invD, best["dist"]):
+                stack.append(j)
+            j += 1
+            if intersect_bv(boxes[j], O, D, invD, best["dist"]):
+                stack.append(j)
+    return best
+
+
+def intersection_info(prims, hit):
+    rec = prims[hit["index"]]
+    pl, Pg, sh, d = hit["pl"], hit["pg"], hit["shape"], hit["dir"]
+    if sh == 1:
+        q = [f32(f32(2.0) * pl[k]) for k in range(3)]
+    elif sh == 2:
+        No = [f32(0.0)] * 3
+        No[d // 2] = f32(1.0) if d % 2 != 0 else f32(-1.0)
+        q = vadd(pl, No)
+    elif sh == 3:
+        No = [f32(0.0), f32(0.0), f32(1.0) if d % 2 != 0 else f32(-1.0)] if d < 2 else [pl[0], pl[1], f32(0.0)]
+        q = vadd(pl, No)
+    elif sh == 5:
+        q = vadd(pl, [f32(0.0), f32(0.0), f32(1.0)])
+    else:
+        raise NotImplementedError(sh)
+    return normalize(vsub(xpoint(rec[0:16], q), Pg)), Pg
+
+
+def camera_dir(invPV, invV, W, H, x, y):
+    """raytracer.vert corner rays, the strip's barycentric interpolation at screen_tc, and
+    raytrace's normalize (montecarlo.frag:182-188).  Returns (Ori, D, u, v)."""
+    def mv4(m, v):     # mat4 · vec4, fma chain x, y, z, w
+        return [fma32(m[12 + r], v[3], fma32(m[8 + r], v[2], fma32(m[4 + r], v[1], f32(m[r] * v[0]))))
+                for r in range(4)]
+    P4 = mv4(invV, [f32(0), f32(0), f32(0), f32(1)])
+    Ori = P4[:3]
+    corners = []
+    for vid in range(4):
+        tc = [f32(vid % 2), f32(vid // 2)]
+        cc = [f32(f32(2.0) * tc[0] - f32(1.0)), f32(f32(2.0) * tc[1] - f32(1.0))]
+        Q = mv4(invPV, [cc[0], cc[1], f32(1), f32(1)])
+        corners.append(normalize([f32(f32(Q[k] / Q[3]) - Ori[k]) for k in range(3)]))
+    u = f32(f32(f32(x) + f32(0.5)) / f32(W))
+    v = f32(f32(f32(y) + f32(0.5)) / f32(H))
+    if f32(u + v) <= 1:
+        w0 = f32(f32(f32(1.0) - u) - v)
+        d = [f32(f32(f32(corners[0][k] * w0) + f32(corners[1][k] * u)) + f32(corners[2][k] * v)) for k in range(3)]
+    else:
+        w1, w3, w2 = f32(f32(1.0) - v), f32(f32(u + v) - f32(1.0)), f32(f32(1.0) - u)
+        d = [f32(f32(f32(corners[1][k] * w1) + f32(corners[3][k] * w3)) + f32(corners[2][k] * w2)) for k in range(3)]
+    return Ori, normalize(d), u, v
+
+
+def random_path(prims, boxes, leaves, depth, seed, D, O, B, ior):
+    """tp/montecarlo.frag:100-179 as written.  Returns (rgb, branch codes taken): S sky,
+    E emissive end, R reflect, T pure refraction, M/m mixed reflect/refract, F diffuse,
+    X budget exhausted (black), I an inner traversal that missed (N, P unchanged)."""
+    trace = []
+    total = [f32(0.0)] * 3
+    stack = [(O, D, [f32(0.8)] * 3)]
+    i = 0
+    while i < B and stack:
+        O, D, att = stack.pop()
+        hit = intersect_bvh(prims, boxes, leaves, depth, O, D)
+        if hit["shape"] < 0:
+            a = max(f32(0.0), D[2])
+            sky = [glsl_mix(f32(0.5), f32(1.0), a), glsl_mix(f32(0.5), f32(1.0), a), glsl_mix(f32(0.9), f32(0.8), a)]
+            trace.append("S")
+            return [f32(total[k] + f32(att[k] * sky[k])) for k in range(3)], trace
+        N, P = intersection_info(prims, hit)
+        rec = prims[hit["index"]]
+        col, mat = rec[52:56], rec[56:60]
+        ray = random_ray(seed, N, f32(f32(1.0) - mat[1]))
+        rs = r_schlick(ior, D, N)
+        R = glsl_reflect([f32(-r) for r in ray], N)
+        E = normalize(vsub(O, P))
+        se = glsl_mix(f32(100.0), f32(2.0), mat[1])
+        spec = mc_pow(max(f32(0.0), dot3(E, R)), se)
+        total = [f32(total[k] + f32(f32(col[k] * f32(0.1)) +
+                                    f32(f32(f32(att[k] * mat[2]) * f32(f32(1.0) - mat[0])) * col[3]))) for k in range(3)]
+        if mat[2] <= 0.5 and len(stack) < 9:
+            mx = [glsl_mix(att[k], col[k], mat[0]) for k in range(3)]
+
+            def reflect_push():
+                na = [f32(f32(col[k] * att[k]) + f32(f32(f32(f32(att[k] * col[3]) * rs) * spec) * mx[k]))
+                      for k in range(3)]
+                rd = random_ray(seed, glsl_reflect(D, N), f32(f32(1.0) - f32(mat[0] * mat[1])))
+                stack.append(([f32(P[k] + f32(BIAS * N[k])) for k in range(3)], rd, na))
+
+            def refract_push(Din):
+                na = [f32(f32(col[k] * att[k]) +
+                          f32(f32(f32(f32(att[k] * f32(f32(1.0) - col[3])) * f32(f32(1.0) - rs)) * spec) * mx[k]))
+                      for k in range(3)]
+                Oin = [f32(P[k] - f32(BIAS * N[k])) for k in range(3)]
+                inner = intersect_bvh(prims, boxes, leaves, depth, Oin, Din)
+                N2, P2 = N, P
+                if inner["shape"] >= 0:
+                    N2, P2 = intersection_info(prims, inner)
+                else:
+                    trace.append("I")          # intersection_info leaves N, P as they were
+                out = glsl_refract(Din, [f32(-n) for n in N2], f32(f32(1.0) / f32(ior)))
+                stack.append(([f32(P2[k] + f32(BIAS * N2[k])) for k in range(3)], out, na))
+
+            if mat[0] > 0 and col[3] == 1:
+                trace.append("R")
+                reflect_push()
+            elif col[3] < 1 and mat[0] == 0:
+                trace.append("T")
+                refract_push(glsl_refract(D, N, ior))
+            elif col[3] < 1 and mat[0] > 0:
+                if random_float(seed) > 0.5:
+                    trace.append("M")
+                    reflect_push()
+                else:
+                    trace.append("m")
+                    refract_push(D)                # the mixed branch does not refract on entry
+            else:
+                trace.append("F")
+                stack.append(([f32(P[k] + f32(BIAS * N[k])) for k in range(3)], ray,
+                              [f32(f32(col[k] * att[k]) + f32(f32(att[k] * spec) * mx[k])) for k in range(3)]))
+        else:
+            trace.append("E")
+            return total, trace
+        i += 1
+    trace.append("X")
+    return [f32(0.0)] * 3, trace
+
+
+def sample(prims, nodes, leaves, depth, invPV, invV, W, H, x, y, npass, B, ior, date=0.0):
+    """One (pixel, pass) sample of montecarlo.frag: srand at screen_tc, then random_path."""
+    Ori, D, u, v = camera_dir(invPV, invV, W, H, x, y)
+    seed = srand(u, v, npass, f32(date))
+    return random_path(prims, node_boxes(nodes), leaves, depth, seed, D, Ori, B, ior)
 
 
 # ----------------------------------------------------------------------------------
@@ -478,8 +721,74 @@ def image_name(c):
     return f"img_s{s}_v{v}_{W}x{H}_p{p}_n{n}_B{B}_ior{ior}_li{li}.npy"
 
 
+def pure_refraction_scene(orc):
+    """A scene for the refraction branch no reference scene reaches (alpha < 1, shininess 0:
+    montecarlo.frag:139-146): glass sphere and cylinder over a diffuse floor, a reflective
+    cube, an emissive quad — built with the oracle's producer (scene.h add_* + finalize)."""
+    def T(tx, ty, tz, sx, sy, sz):   # translate · scale, column-major
+        m = np.eye(4, dtype=np.float32)
+        m[0, 0], m[1, 1], m[2, 2] = sx, sy, sz
+        m[0, 3], m[1, 3], m[2, 3] = tx, ty, tz
+        return m.T.reshape(-1)
+    ops = [(5, T(0, 0, 150, 40, 40, 1), [1.0, 1.0, 1.0, 1.0, 0.0, 0.0, 20.0]),
+           (1, T(-40, 0, 0, 45, 45, 45), [0.7, 0.9, 0.8, 0.4, 0.0, 0.3, 0.0]),
+           (3, T(70, 30, 0, 30, 30, 50), [0.9, 0.6, 0.6, 0.6, 0.0, 0.8, 0.0]),
+           (2, T(0, 0, -60, 400, 400, 5), [0.8, 0.8, 0.8, 1.0, 0.0, 0.5, 0.0]),
+           (2, T(30, -90, -20, 25, 25, 25), [0.5, 0.5, 0.9, 1.0, 0.6, 0.4, 0.0])]
+    return orc.custom_scene([(t, np.asarray(m, np.float32), np.asarray(a, np.float32)) for t, m, a in ops])
+
+
+PATH_CASES = [  # (scene id or 0 = pure_refraction_scene, light, ior, bounces, samples)
+    (1, 1.2, 1.0, 3, 64), (6, 1.2, 1.0, 8, 64), (6, 0.443, 1.5, 8, 64), (8, 1.2, 1.0, 12, 64),
+    (0, 1.2, 1.5, 8, 64),
+]
+
+
+def make_path_kat(orc, rng):
+    """Whole samples of the integrator (pixel, pass) at 1920×1080 with the numpy restatement
+    above: the oracle must reproduce every one bit for bit (tests/test_oracle_paths.py)."""
+    W, H = 1920, 1080
+    ipv, iv = orc.camera(W, H)
+    out = {k: [] for k in ("scene", "light", "ior", "bounces", "x", "y", "npass", "rgb", "trace")}
+    custom = pure_refraction_scene(orc)
+    for scene_id, li, ior, B, n in PATH_CASES:
+        prims, nodes, leaves, depth, _ = custom if scene_id == 0 else orc.scene(scene_id, li)
+        for k in range(n):
+            # pixels near the image centre (objects) or anywhere; every 8th sample is drawn
+            # until its path ends on an emissive primitive (at most 400 draws), so the
+            # emissive end of montecarlo.frag:175-176 is covered
+            for _ in range(400 if k % 8 == 7 else 1):
+                if k % 2 == 0:
+                    x, y = int(rng.integers(W // 4, 3 * W // 4)), int(rng.integers(H // 4, 3 * H // 4))
+                else:
+                    x, y = int(rng.integers(0, W)), int(rng.integers(0, H))
+                npass = int(rng.integers(1, 84001)) if k % 3 else int(rng.integers(1, 33))
+                rgb, tr = sample(prims, nodes, leaves, depth, ipv, iv, W, H, x, y, npass, B, ior)
+                if tr[-1] == "E":
+                    break
+            for key, val in (("scene", scene_id), ("light", li), ("ior", ior), ("bounces", B), ("x", x), ("y", y),
+                             ("npass", npass), ("rgb", rgb), ("trace", "".join(tr))):
+                out[key].append(val)
+    kat = {"path_" + k: np.array(v) for k, v in out.items()}
+    kat["path_rgb"] = np.array(out["rgb"], np.float32)
+    kat["path_light"] = np.array(out["light"], np.float32)
+    kat["path_ior"] = np.array(out["ior"], np.float32)
+    kat["path_trace"] = np.array(out["trace"], "U32")
+    kat["custom_prims"], kat["custom_nodes"], kat["custom_leaves"] = custom[0], custom[1], custom[2]
+    kat["custom_depth"] = np.array(custom[3], np.int32)
+    kat["path_W"], kat["path_H"] = np.array(W, np.int32), np.array(H, np.int32)
+    return kat
+
+
 def main():
     from oracle import oracle as orc
+    if len(sys.argv) > 1 and sys.argv[1] == "paths":   # paths.npz only (round-2 addition)
+        kat = make_path_kat(orc, np.random.default_rng(20250216))
+        np.savez_compressed(os.path.join(HERE, "paths.npz"), **kat)
+        codes = "".join(kat["path_trace"].tolist())
+        print("wrote paths.npz:", len(kat["path_x"]), "samples; branch counts",
+              {c: codes.count(c) for c in "SERTMmFXI"})
+        return
     rng = np.random.default_rng(20241008)
     kat = make_kat(rng)
     prims = [orc.scene(s)[0] for s in (1, 2, 3, 6, 8)]
