@@ -45,6 +45,18 @@
 #ifndef MCPT_FOLD_END
 #define MCPT_FOLD_END 1
 #endif
+// random_ray job compaction (rr_jobs): the shading round's two random_ray calls (the bounce's
+// `ray` and the reflect branch's new direction) run as one compacted batch across the wave.
+// Bit-exact, measured slower (scene 6 -18 %, scene 8 -9 %: DESIGN.md §4.1), off by default.
+#ifndef MCPT_RR_COMPACT
+#define MCPT_RR_COMPACT 0
+#endif
+// per-wave unit pool: a lane whose (pixel, segment) unit ends claims any unclaimed unit of
+// its wave's 64 x K pool (LDS counter) instead of its own pixel's next segment.  Bit-exact,
+// measured no faster than the static order, off by default.
+#ifndef MCPT_UNIT_POOL
+#define MCPT_UNIT_POOL 0
+#endif
 
 
 namespace mcpt {
@@ -822,6 +834,80 @@ __device__ __forceinline__ float schlick(float ior, f3 I, f3 N) {   // :91-98
 }
 
 // ------------------------------------------------------------------------------------
+// random_ray job compaction (north star: ray compaction via wavefront primitives)
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ int mbcnt64(uint64_t m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ uint32_t bperm(int lane, uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(lane << 2, (int)v);
+}
+__device__ __forceinline__ float bpermf(int lane, float v) { return __uint_as_float(bperm(lane, __float_as_uint(v))); }
+
+// One shading round of montecarlo.frag draws up to two random_ray per lane: `ray`
+// (:122, every non-emissive hit) and the reflect branch's new direction (:136 / :155, the
+// reflective branch and the mixed branch's reflect half).  Issued as two call sites, the wave
+// pays for both whenever any lane reflects, each with part of its lanes.  Both are pure
+// functions of (direction, roughness, RNG state), and the state of the second is the first's
+// plus a known number of draws (rng_skip: 2, or 3 after the mixed branch's coin), so they
+// are independent jobs: compacted here into consecutive job slots (ballot + mbcnt), run by
+// the wave's active lanes in batches (the lane of active rank r takes slot base + r and pulls
+// its owner's inputs with ds_bpermute), and pulled back by their owners.  Per lane the values
+// are those of the two calls in order (bit-exact); the wave runs ceil(jobs / active lanes)
+// random_ray bodies instead of two.  own / wl: this wave's 128 + 64 bytes of LDS (job slot ->
+// owner lane, active rank -> lane).  Called at a point every active lane reaches.
+#ifdef MCPT_RR_STATS
+struct RrStats { unsigned long long calls = 0, batches = 0, jobs = 0, active = 0, over = 0, jobs1 = 0; };
+#define MCPT_RR_STATS_ARG , RrStats& st
+#else
+#define MCPT_RR_STATS_ARG
+#endif
+__device__ __forceinline__ void rr_jobs(bool need1, bool need2, const Rng& rng, uint32_t k2, f3 N, f3 D, float mx,
+                                        float my, f3& ray, f3& rd, unsigned char* own, unsigned char* wl,
+                                        int lane MCPT_RR_STATS_ARG) {
+  const uint64_t act = __ballot(1), m1 = __ballot(need1), m2 = __ballot(need2);
+  const int n_act = __builtin_popcountll(act), rank = mbcnt64(act);
+  const int n1 = __builtin_popcountll(m1), n_jobs = n1 + __builtin_popcountll(m2);
+#ifdef MCPT_RR_STATS   // diagnostic build only: per-wave job statistics (wave-uniform values)
+  st.calls++; st.batches += (n_jobs + n_act - 1) / n_act; st.jobs += n_jobs; st.active += n_act;
+  st.over += n_jobs > n_act; st.jobs1 += n1;
+#endif
+  const int s1 = mbcnt64(m1), s2 = n1 + mbcnt64(m2);
+  if (need1) own[s1] = (unsigned char)lane;
+  if (need2) own[s2] = (unsigned char)lane;
+  wl[rank] = (unsigned char)lane;
+  __builtin_amdgcn_wave_barrier();
+  for (int base = 0; base < n_jobs; base += n_act) {   // wave-uniform
+    const int sl = base + rank;
+    const bool job = sl < n_jobs;
+    const int o = job ? (int)own[sl] : lane;
+    Rng r;
+    r.x = bperm(o, rng.x); r.y = bperm(o, rng.y); r.z = bperm(o, rng.z);
+    const uint32_t k = bperm(o, k2);
+    const f3 Nj = mk(bpermf(o, N.x), bpermf(o, N.y), bpermf(o, N.z));
+    const f3 Dj = mk(bpermf(o, D.x), bpermf(o, D.y), bpermf(o, D.z));
+    const float xj = bpermf(o, mx), yj = bpermf(o, my);
+    f3 out = mk(0.0f, 0.0f, 0.0f);
+    if (job) {
+      if (sl >= n1) {   // the reflect branch's direction: random_ray(reflect(D,N), 1-mat.r*mat.g)
+        rng_skip(r, k);
+        out = random_ray(r, greflect(Dj, Nj), 1.0f - xj * yj);
+      } else {          // ray = random_ray(N, 1-mat.g)
+        out = random_ray(r, Nj, 1.0f - yj);
+      }
+    }
+    const bool in1 = need1 && s1 >= base && s1 < base + n_act;
+    const bool in2 = need2 && s2 >= base && s2 < base + n_act;
+    const int w1 = in1 ? (int)wl[s1 - base] : lane, w2 = in2 ? (int)wl[s2 - base] : lane;
+    const f3 o1 = mk(bpermf(w1, out.x), bpermf(w1, out.y), bpermf(w1, out.z));
+    const f3 o2 = mk(bpermf(w2, out.x), bpermf(w2, out.y), bpermf(w2, out.z));
+    if (in1) ray = o1;
+    if (in2) rd = o2;
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+// ------------------------------------------------------------------------------------
 // the kernel
 // ------------------------------------------------------------------------------------
 __device__ __forceinline__ int floordiv(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
@@ -858,21 +944,30 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
   // segment-fastest item order: the pass segments of one tile are consecutive workgroups
   // (tile-fastest order was 1-12 % slower on one GPU and 7 % on a 1/8-row shard's launch:
   // profiles/r01_ab42_item_order.jsonl)
-  // a work item runs K = seg_per_item consecutive segments of its tile (one lane: the pixel's
-  // passes straight through them, each segment's sum written when its chunk ends)
+  // A work item runs K = seg_per_item consecutive segments of its tile.  Each wave holds a
+  // pool of 64 x K units (pixel of its 8x8 block, segment): a lane starts with its own pixel's
+  // first segment and, whenever its unit ends, takes the next unclaimed unit of the pool
+  // (ballot + mbcnt at the end of a round), so a lane whose pixel is cheap (sky) works on
+  // the expensive pixels' other segments instead of idling until the wave's slowest lane
+  // is done.  A unit is one accumulation chunk of one pixel, summed in pass order and written
+  // to its segment slot when it ends: the bits do not depend on which lane runs it.
   const int K = p.seg_per_item > 1 ? p.seg_per_item : 1;
   const int n_groups = (p.n_segments + K - 1) / K;
   const int tile = item / n_groups, seg_lo = (item % n_groups) * K;
   const int seg_n = min(K, p.n_segments - seg_lo);
   int seg = seg_lo;
   const int tiles_x = (p.W + kTileW - 1) / kTileW;
-  const int x = (tile % tiles_x) * kTileW + (wave % (kTileW / 8)) * 8 + (lane & 7);
-  const int lr = (tile / tiles_x) * kTileH + (wave / (kTileW / 8)) * 8 + (lane >> 3);
+  const int bx0 = (tile % tiles_x) * kTileW + (wave % (kTileW / 8)) * 8;   // this wave's 8x8 block
+  const int by0 = (tile / tiles_x) * kTileH + (wave / (kTileW / 8)) * 8;
+  int x = bx0 + (lane & 7);
+  int lr = by0 + (lane >> 3);
   const bool live = x < p.W && lr < p.n_local_rows;   // (no early return: LDS staging barrier)
-  const int c0 = floordiv(p.first_pass - 1, kPassChunk) + seg_lo;
+  const int cbase = floordiv(p.first_pass - 1, kPassChunk);   // chunk of the launch's first pass
+  const int c0 = cbase + seg_lo;
   const int pass_begin = max(p.first_pass, c0 * kPassChunk + 1);
-  const int pass_end = min(p.first_pass + p.n_passes, (c0 + seg_n) * kPassChunk + 1);
-  const int y = live ? p.rows[lr] : 0;   // this shard's local row -> image row (mcpt_set_target*)
+  int pass_end = min(p.first_pass + p.n_passes, (c0 + 1) * kPassChunk + 1);   // this unit's end
+  int y = live ? p.rows[lr] : 0;   // this shard's local row -> image row (mcpt_set_target*)
+  int pslot = tid;                 // LDS slot of this unit's pixel (per-pixel rows of s_pix, s_hit0)
 
   SceneT<MESH, LDSS> s{p.nodes, p.leaves, p.ptype, p.prims, p.depth, p.minfo, p.mnodes, p.mleaves, p.mtris,
                        p.mverts, p.mnorms, p.flat_face};
@@ -918,9 +1013,18 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
   // 19 KB per workgroup, + the staged scene (LDSS, <= kLdsSceneBytes): 7 workgroups/CU.
   __shared__ float s_pix[18][kTileThreads];
   __shared__ int s_hit0[kTileThreads];
+#if MCPT_UNIT_POOL
+  __shared__ unsigned int s_unext[kTileThreads / 64];   // next unclaimed unit of each wave's pool
+#endif
+#if MCPT_RR_COMPACT
+  __shared__ unsigned char s_own[kTileThreads / 64][128], s_wl[kTileThreads / 64][64];   // rr_jobs
+#endif
   const f3 Dcam0 = normalize3(dir);
-  s_pix[0][tid] = Dcam0.x; s_pix[1][tid] = Dcam0.y; s_pix[2][tid] = Dcam0.z;
+  s_pix[0][pslot] = Dcam0.x; s_pix[1][pslot] = Dcam0.y; s_pix[2][pslot] = Dcam0.z;
   s_pix[12][tid] = 0.0f; s_pix[13][tid] = 0.0f; s_pix[14][tid] = 0.0f;   // this segment's sum
+#if MCPT_UNIT_POOL
+  if (lane == 0) s_unext[wave] = 64u;
+#endif
   const f3 Ocam = mk(p.ox, p.oy, p.oz);
 
 
@@ -954,9 +1058,9 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
     shape0 = h.shape; idx0 = h.index;
     if (shape0 >= 0) geom_info<COUNT>(s, h, N0, P0, ev);
   }
-  s_pix[3][tid] = N0.x; s_pix[4][tid] = N0.y; s_pix[5][tid] = N0.z;
-  s_pix[6][tid] = P0.x; s_pix[7][tid] = P0.y; s_pix[8][tid] = P0.z;
-  s_hit0[tid] = shape0 < 0 ? -1 : (shape0 << 28) | idx0;   // idx0 < 2^28 (mcpt_upload_scene)
+  s_pix[3][pslot] = N0.x; s_pix[4][pslot] = N0.y; s_pix[5][pslot] = N0.z;
+  s_pix[6][pslot] = P0.x; s_pix[7][pslot] = P0.y; s_pix[8][pslot] = P0.z;
+  s_hit0[pslot] = shape0 < 0 ? -1 : (shape0 << 28) | idx0;   // idx0 < 2^28 (mcpt_upload_scene)
 
 #ifdef MCPT_STAMPS
   const unsigned long long st_p = __builtin_amdgcn_s_memtime() - st_k0;
@@ -972,16 +1076,49 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
       part[0] = s_pix[12][tid]; part[1] = s_pix[13][tid]; part[2] = s_pix[14][tid];
     }
   };
-  // after pass++: a pass that opens a new chunk closes the previous segment
+  // after pass++: the unit's last pass closes it (its sum to the segment slot) and the lane
+  // takes its next unit: its own pixel's next segment, or (MCPT_UNIT_POOL) the next unclaimed
+  // unit of its wave's pool (an LDS counter per wave: units 0..63 are the lanes' own first
+  // segments; units of pixels outside the shard are skipped).  With none left, pass stays at
+  // pass_end and the lane leaves the loop.
   auto next_chunk = [&]() {
-    if (K > 1 && pass < pass_end && floordiv(pass - 1, kPassChunk) * kPassChunk == pass - 1) {
+    if (pass >= pass_end) {
       flush_sum();
-      seg++;
-      s_pix[12][tid] = 0.0f; s_pix[13][tid] = 0.0f; s_pix[14][tid] = 0.0f;
+#if !MCPT_UNIT_POOL
+      if (seg + 1 < seg_lo + seg_n) {
+        seg++;
+        const int c = c0 + (seg - seg_lo);
+        pass = c * kPassChunk + 1;
+        pass_end = min(p.first_pass + p.n_passes, (c + 1) * kPassChunk + 1);
+        s_pix[12][tid] = 0.0f; s_pix[13][tid] = 0.0f; s_pix[14][tid] = 0.0f;
+      }
+#else
+      const int n_units = 64 * seg_n;
+      for (;;) {
+        const int cu = (int)atomicAdd(&s_unext[wave], 1u);
+        if (cu >= n_units) break;
+        const int up = cu & 63;
+        x = bx0 + (up & 7);
+        lr = by0 + (up >> 3);
+        if (x < p.W && lr < p.n_local_rows) {
+          pslot = wave * 64 + up;
+          y = p.rows[lr];
+          seg = seg_lo + (cu >> 6);
+          const int c = c0 + (cu >> 6);
+          pass = max(p.first_pass, c * kPassChunk + 1);
+          pass_end = min(p.first_pass + p.n_passes, (c + 1) * kPassChunk + 1);
+          s_pix[12][tid] = 0.0f; s_pix[13][tid] = 0.0f; s_pix[14][tid] = 0.0f;
+          break;
+        }
+      }
+#endif
     }
   };
   Walk walk;
   walk.invD = mk(0.0f, 0.0f, 0.0f); walk.node = 0; walk.level = 0; walk.pending = 0;
+#ifdef MCPT_RR_STATS
+  RrStats rrst;
+#endif
   bool walking = false;   // a suspended per-lane walk is waiting to be continued
   while (pass < pass_end) {
 #ifdef MCPT_STAMPS
@@ -996,7 +1133,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
       done = true;   // for(i=0; i<NB_BOUNCES ...) never runs: black
     } else {
       if (first) {
-        const int hv = s_hit0[tid];
+        const int hv = s_hit0[pslot];
         h.shape = hv < 0 ? -1 : hv >> 28;
         h.index = hv < 0 ? -1 : hv & 0x0FFFFFFF;
       } else if (WAVE) {
@@ -1056,17 +1193,54 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
       next_chunk();
       if (pass < pass_end) {
         rng = seed_for(((float)x + 0.5f) / (float)p.W, ((float)y + 0.5f) / (float)p.H, pass, p.date);
-        O = Ocam; D = mk(s_pix[0][tid], s_pix[1][tid], s_pix[2][tid]);
+        O = Ocam; D = mk(s_pix[0][pslot], s_pix[1][pslot], s_pix[2][pslot]);
         att = mk(0.8f, 0.8f, 0.8f); total = mk(0.0f, 0.0f, 0.0f);
         bounce = 0;
-        const int hv = s_hit0[tid];
+        const int hv = s_hit0[pslot];
         h.shape = hv < 0 ? -1 : hv >> 28;
         h.index = hv < 0 ? -1 : hv & 0x0FFFFFFF;
         first = true;
       } else {
-        ready = false;   // segment finished: the loop ends for this lane
+        ready = false;   // unit finished: the lane claims another at the end of the round
       }
     }
+#endif
+#if MCPT_RR_COMPACT
+    // shading part A (montecarlo.frag:118-124): the hit's N, P, colour and material, and the
+    // random_ray jobs of this round — `ray` for a non-emissive hit, and the reflect branch's
+    // direction where the lane will take it (the mixed branch's coin is drawn ahead at its
+    // place in the sequence, rng + 2)
+    const bool shade0 = ready && run && p.variant == 0 && phase == 0 && h.shape >= 0;
+    float4 c4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), m4 = c4;
+    bool need1 = false, need2 = false, mixed = false;
+    if (shade0) {
+      if (first) {
+        N = mk(s_pix[3][pslot], s_pix[4][pslot], s_pix[5][pslot]);
+        P = mk(s_pix[6][pslot], s_pix[7][pslot], s_pix[8][pslot]);
+      } else {
+        geom_info<COUNT>(s, h, N, P, ev);
+      }
+      ev.inc(EV_COLMAT);
+      c4 = s.prims[(size_t)h.index * 8 + 6];
+      m4 = s.prims[(size_t)h.index * 8 + 7];
+      if (m4.z <= 0.5f) {
+        need1 = true;
+        if (m4.x > 0.0f && c4.w == 1.0f) {
+          need2 = true;
+        } else if (c4.w < 1.0f && m4.x > 0.0f) {
+          mixed = true;
+          Rng t = rng;
+          rng_skip(t, 2);
+          need2 = rnd(t) > 0.5f;
+        }
+      }
+    }
+    f3 ray = mk(0.0f, 0.0f, 0.0f), rdir = ray;
+    rr_jobs(need1, need2, rng, mixed ? 3u : 2u, N, D, m4.x, m4.y, ray, rdir, s_own[wave], s_wl[wave], lane
+#ifdef MCPT_RR_STATS
+            , rrst
+#endif
+    );
 #endif
     if (ready && run) {
       if (p.variant != 0) {
@@ -1075,8 +1249,8 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
           res = mk(0.0f, 0.0f, 0.2f);
         } else {
           if (first) {
-            N = mk(s_pix[3][tid], s_pix[4][tid], s_pix[5][tid]);
-            P = mk(s_pix[6][tid], s_pix[7][tid], s_pix[8][tid]);
+            N = mk(s_pix[3][pslot], s_pix[4][pslot], s_pix[5][pslot]);
+            P = mk(s_pix[6][pslot], s_pix[7][pslot], s_pix[8][pslot]);
           }
           else geom_info<COUNT>(s, h, N, P, ev);
           ev.inc(EV_COLMAT);
@@ -1097,17 +1271,22 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
           res = add(total, mulv(att, gmix3(mk(0.5f, 0.5f, 0.9f), mk(1.0f, 1.0f, 0.8f), a)));
           done = true;
         } else {
+#if MCPT_RR_COMPACT
+          // part C: the rest of the shading with this lane's random_ray results
+          if (need1) rng_skip(rng, 2);   // the draws of `ray`
+#else
           if (first) {
-            N = mk(s_pix[3][tid], s_pix[4][tid], s_pix[5][tid]);
-            P = mk(s_pix[6][tid], s_pix[7][tid], s_pix[8][tid]);
+            N = mk(s_pix[3][pslot], s_pix[4][pslot], s_pix[5][pslot]);
+            P = mk(s_pix[6][pslot], s_pix[7][pslot], s_pix[8][pslot]);
           }
           else geom_info<COUNT>(s, h, N, P, ev);
           ev.inc(EV_COLMAT);
           const float4 c4 = s.prims[(size_t)h.index * 8 + 6];
           const float4 m4 = s.prims[(size_t)h.index * 8 + 7];
+          f3 ray = random_ray(rng, N, 1.0f - m4.y);
+#endif
           const f3 col = mk(c4.x, c4.y, c4.z);
           const float alpha = c4.w;
-          f3 ray = random_ray(rng, N, 1.0f - m4.y);
           float rs = schlick(ior, D, N);
           f3 R = greflect(neg(ray), N);
           f3 E = normalize3(sub(O, P));
@@ -1127,8 +1306,13 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
               O = sub(P, muls(N, kBIAS));
               D = grefract(D, N, ior);
             } else if (alpha < 1.0f && m4.x > 0.0f) {
+#if MCPT_RR_COMPACT
+              rng_skip(rng, 1);   // the coin, drawn in part A
+              if (need2) {
+#else
               float r = rnd(rng);
               if (r > 0.5f) {
+#endif
                 reflect_push = true;
               } else {
                 inner = true;
@@ -1143,7 +1327,12 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
             }
             if (reflect_push) {
               f3 na = add(base, mulv(muls(muls(muls(att, alpha), rs), spec), mx));
+#if MCPT_RR_COMPACT
+              rng_skip(rng, 2);   // the draws of the new direction (rr_jobs)
+              const f3 rd = rdir;
+#else
               f3 rd = random_ray(rng, greflect(D, N), 1.0f - m4.x * m4.y);
+#endif
               att = na;
               O = add(P, muls(N, kBIAS));
               D = rd;
@@ -1185,7 +1374,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
       pass++;
       next_chunk();
       rng = seed_for(((float)x + 0.5f) / (float)p.W, ((float)y + 0.5f) / (float)p.H, pass, p.date);   // = (u, v)
-      O = Ocam; D = mk(s_pix[0][tid], s_pix[1][tid], s_pix[2][tid]);
+      O = Ocam; D = mk(s_pix[0][pslot], s_pix[1][pslot], s_pix[2][pslot]);
       att = mk(0.8f, 0.8f, 0.8f); total = mk(0.0f, 0.0f, 0.0f);
       bounce = 0; phase = 0;
     }
@@ -1193,37 +1382,19 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
     st_s += __builtin_amdgcn_s_memtime();
 #endif
   }
-#ifdef MCPT_STAMPS
+#ifdef MCPT_RR_STATS
+  // the wave's counters are uniform per lane; lanes leave the loop at different rounds, so the
+  // last lane out holds the wave's totals (max over lanes)
   {
-    // wave totals = the last-finishing lane's sums (max over lanes); lane-iterations summed
-    unsigned long long vals[6] = {__builtin_amdgcn_s_memtime() - st_k0, st_p, st_t, st_s, st_it, ev.st_leaf};
-    unsigned long long it_sum = st_it, lit = ev.st_lit, wit = ev.st_wit;
-    unsigned long long nl = ev.st_nl, nw = ev.st_nw, ll = ev.st_ll, lw = ev.st_lw;
-    for (int off = 32; off > 0; off >>= 1) {
-      for (int k = 0; k < 6; ++k) { unsigned long long o = __shfl_xor(vals[k], off); vals[k] = vals[k] > o ? vals[k] : o; }
-      it_sum += __shfl_xor(it_sum, off);
-      lit += __shfl_xor(lit, off);
-      wit += __shfl_xor(wit, off);
-      nl += __shfl_xor(nl, off);
-      nw += __shfl_xor(nw, off);
-      ll += __shfl_xor(ll, off);
-      lw += __shfl_xor(lw, off);
-    }
-    if (lane == 0 && p.events) {
-      for (int k = 0; k < 5; ++k) atomicAdd(p.events + k, vals[k]);
-      atomicAdd(p.events + 5, it_sum);
+    unsigned long long v[6] = {rrst.calls, rrst.batches, rrst.jobs, rrst.active, rrst.over, rrst.jobs1};
+    for (int off = 32; off > 0; off >>= 1)
+      for (int k = 0; k < 6; ++k) { unsigned long long o = __shfl_xor(v[k], off); v[k] = v[k] > o ? v[k] : o; }
+    if ((int)__lane_id() == __builtin_ffsll((long long)__ballot(1)) - 1 && p.events) {
+      for (int k = 0; k < 6; ++k) atomicAdd(p.events + k, v[k]);
       atomicAdd(p.events + 6, 1ull);
-      atomicAdd(p.events + 7, vals[5]);
-      atomicAdd(p.events + 9, lit);
-      atomicAdd(p.events + 10, wit);
-      atomicAdd(p.events + 11, nl);
-      atomicAdd(p.events + 12, nw);
-      atomicAdd(p.events + 13, ll);
-      atomicAdd(p.events + 14, lw);
     }
   }
 #endif
-  flush_sum();
 
   if (COUNT) {
 #pragma unroll

@@ -217,6 +217,9 @@ __device__ __forceinline__ float rnd(Rng& s) {
   s.x += 11u; s.y += 43u; s.z += 67u;
   return f - 1.0f;
 }
+// the state after k draws: random_float only adds (11, 43, 67) to the seed per draw, so a
+// draw sequence can be entered at any position without computing the draws before it
+__device__ __forceinline__ void rng_skip(Rng& s, uint32_t k) { s.x += 11u * k; s.y += 43u * k; s.z += 67u * k; }
 // srand raytracer_func.frag:105-110
 __device__ __forceinline__ Rng seed_for(float tcx, float tcy, int np, float date) {
   float f = (float)(1 + np);
