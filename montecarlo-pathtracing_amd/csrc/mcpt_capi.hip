@@ -17,6 +17,7 @@
 
 #include "../../include/mcpt.h"
 #include "mcpt_internal.h"
+#include "mcpt_math.h"
 
 static thread_local char g_last_error[256] = "";
 
@@ -590,6 +591,14 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   p.seg_per_item = env_seg > 0 ? env_seg : cand_seg_per_item(cand);
   p.first_pass = first_pass; p.n_passes = n_passes; p.bounces = bounces; p.variant = variant;
   p.date = date; p.ior = refract_ind;
+  p.inv_ior = 1.0f / refract_ind;
+  {
+    float r0 = (refract_ind - 1.0f) / (refract_ind + 1.0f);   // schlick tp/montecarlo.frag:93-94
+    p.schlick_r0 = r0 * r0;
+    const float fmax = mcpt::kFLTMAX, nx = std::nextafter(fmax, INFINITY);   // cull_bound_sq(FLT_MAX)
+    const double m = ((double)fmax + (double)nx) * 0.5;
+    p.cull2_max = m * m;
+  }
   p.n_local_px = (long long)c->n_local_rows * c->W;
   // The call's pass range is cut at accumulation-chunk boundaries into sub-launches of at
   // most max_seg segments, so that the segment-sum buffer stays within partial_budget and

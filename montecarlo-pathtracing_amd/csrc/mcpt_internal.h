@@ -82,6 +82,11 @@ struct RenderParams {
   int leaf_batch;               // deep-BVH walk: run the leaf block once >= this many lanes wait
   int first_pass, n_passes, bounces, variant;
   float date, ior;
+  // wave-uniform constants computed on the host (same binary32/binary64 operations as the
+  // kernel would do) so that they live in SGPRs, not in spilled VGPRs: 1/ior (grefract of the
+  // inner exit), Schlick's ((ior-1)/(ior+1))^2, and cull_bound_sq(FLT_MAX) (walk start)
+  float inv_ior, schlick_r0;
+  double cull2_max;
 };
 
 // ray-query batch (mcpt_trace): per ray 3 ints (shape, prim, dir) and kTraceFloats floats

@@ -80,8 +80,11 @@ __device__ __forceinline__ float wsqrt(float x) { return __builtin_sqrtf(x); }
 __device__ __forceinline__ float wrcp(float x) { return 1.0f / x; }
 #endif
 
+// Closest-hit record.  The world-space hit point is not kept: it is xpoint(transform of
+// `index`, pl), recomputed by geom_info with the same operations accept_cand used (same bits),
+// which keeps 3 VGPRs out of the traversal's live state.
 struct Hit {
-  f3 pl, pg;
+  f3 pl;
   float dist;
   int index, shape, dir;
   double cull2;   // (midpoint between dist and the next float above)^2, exact in binary64
@@ -248,7 +251,7 @@ __device__ __forceinline__ void accept_cand(const SR& s, int index, int shape, i
   f3 Pg = xpoint(ld4<U>(s.prims, b + 3), ld4<U>(s.prims, b + 4), ld4<U>(s.prims, b + 5), Pl);
   float dist = wlength3(sub(Ol, Pg));
   if (dist < h.dist) {
-    h.dist = dist; h.pl = Pl; h.pg = Pg; h.index = index; h.shape = shape; h.dir = dir;
+    h.dist = dist; h.pl = Pl; h.index = index; h.shape = shape; h.dir = dir;
     h.cull2 = cull_bound_sq(dist);
   }
 }
@@ -279,7 +282,7 @@ __device__ __forceinline__ void tri_test(const SR& s, int tri_base, int t, int i
     const f3 Pg = xpoint(t0, t1, t2, Pl);
     const float dist = wlength3(sub(Ol, Pg));
     if (dist < h.dist) {
-      h.dist = dist; h.pl = Pl; h.pg = Pg; h.index = index; h.shape = CODE_MESH; h.dir = t;
+      h.dist = dist; h.pl = Pl; h.index = index; h.shape = CODE_MESH; h.dir = t;
       h.cull2 = cull_bound_sq(dist);
     }
   }
@@ -506,9 +509,11 @@ struct Walk {
 };
 
 template <bool COUNT, class SR>
-__device__ __forceinline__ void walk_begin(const SR& s, f3 D, Hit& h, Walk& w, Ev<COUNT>& ev) {
+__device__ __forceinline__ void walk_begin(const SR& s, f3 D, Hit& h, Walk& w, Ev<COUNT>& ev, double cull2_max) {
   ev.inc(EV_TRAV);
-  h.index = -1; h.dist = kFLTMAX; h.shape = -1; h.dir = -1; h.cull2 = cull_bound_sq(kFLTMAX);
+  // cull2_max = cull_bound_sq(kFLTMAX), a kernel argument (SGPRs) rather than a constant the
+  // register allocator keeps in (spilled) VGPRs across the render loop
+  h.index = -1; h.dist = kFLTMAX; h.shape = -1; h.dir = -1; h.cull2 = cull2_max;
   w.invD = mk(rcp_rn(D.x), rcp_rn(D.y), rcp_rn(D.z));
   w.node = 0; w.level = 0; w.pending = 0;
   if constexpr (SR::kMesh) w.mprim = -1;
@@ -763,7 +768,7 @@ __device__ __forceinline__ void geom_info(const SR& s, const Hit& h, f3& N, f3& 
   ev.inc(EV_GEOM);
   const float4* pr = s.prims + (size_t)h.index * 8;
   float4 t0 = pr[3], t1 = pr[4], t2 = pr[5];
-  P = h.pg;
+  P = xpoint(t0, t1, t2, h.pl);   // = the candidate's Pg (accept_cand / tri_test)
   f3 q;
   if (h.shape == CODE_SPHERE) {
     q = muls(h.pl, 2.0f);
@@ -826,9 +831,8 @@ __device__ __forceinline__ f3 random_ray(Rng& rng, f3 D, float roughness) {
   return normalize3(m);
 }
 
-__device__ __forceinline__ float schlick(float ior, f3 I, f3 N) {   // :91-98
-  float r0 = (ior - 1.0f) / (ior + 1.0f);
-  r0 *= r0;
+// r0 = ((ior-1)/(ior+1))^2 (:93-94), computed once on the host (RenderParams::schlick_r0)
+__device__ __forceinline__ float schlick(float r0, f3 I, f3 N) {   // :91-98
   float x = 1.0f - dot3(N, I);
   return gclamp(r0 + ((((1.0f - r0) * x) * x * x) * x) * x, 0.0f, 1.0f);
 }
@@ -1037,7 +1041,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
   f3 N = mk(0.0f, 0.0f, 0.0f), P = mk(0.0f, 0.0f, 0.0f);
   int bounce = 0, phase = 0;
   Hit h;
-  h.pl = mk(0.0f, 0.0f, 0.0f); h.pg = h.pl; h.dist = kFLTMAX; h.index = -1; h.shape = -1; h.dir = -1;
+  h.pl = mk(0.0f, 0.0f, 0.0f); h.dist = kFLTMAX; h.index = -1; h.shape = -1; h.dir = -1;
   h.cull2 = 0.0;
 
   // Primary-ray cache.  The camera ray of a pixel is the same in every pass (fixed
@@ -1067,7 +1071,11 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
 #endif
   // this segment's sum -> accumulator (one-segment launch) or its segment slot
   auto flush_sum = [&]() {
-    const size_t px = (size_t)lr * p.W + x;
+    // the pixel's address is recomputed at each flush (an empty asm makes the row opaque):
+    // hoisted out of the render loop, its 64-bit index and pointer were 4 spilled VGPRs
+    int lrow = lr;
+    asm volatile("" : "+v"(lrow));
+    const size_t px = (size_t)lrow * p.W + x;
     if (p.n_segments == 1) {
       float* accp = p.accum + px * 3;
       accp[0] = accp[0] + s_pix[12][tid]; accp[1] = accp[1] + s_pix[13][tid]; accp[2] = accp[2] + s_pix[14][tid];
@@ -1139,7 +1147,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
       } else if (WAVE) {
         traverse<COUNT, WAVE>(s, O, D, h, ev);
       } else {
-        if (!walking) { walk_begin<COUNT>(s, D, h, walk, ev); walking = true; }
+        if (!walking) { walk_begin<COUNT>(s, D, h, walk, ev, p.cull2_max); walking = true; }
         if constexpr (MESH) walking = !walk_run_mesh<COUNT, SUSPEND>(s, O, D, h, walk, ev, p.walk_exit);
         else walking = !walk_run<COUNT, SUSPEND>(s, O, D, h, walk, ev, p.walk_exit, p.leaf_batch);
         ready = !walking;
@@ -1287,7 +1295,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
 #endif
           const f3 col = mk(c4.x, c4.y, c4.z);
           const float alpha = c4.w;
-          float rs = schlick(ior, D, N);
+          float rs = schlick(p.schlick_r0, D, N);
           f3 R = greflect(neg(ray), N);
           f3 E = normalize3(sub(O, P));
           float se = gmix(100.0f, 2.0f, m4.y);
@@ -1360,7 +1368,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
           P = mk(s_pix[15][tid], s_pix[16][tid], s_pix[17][tid]);
         }
         O = add(P, muls(N, kBIAS));
-        D = grefract(D, neg(N), 1.0f / ior);
+        D = grefract(D, neg(N), p.inv_ior);
         phase = 0;
         bounce++;
         if (bounce >= B) done = true;
@@ -1434,7 +1442,7 @@ __global__ __launch_bounds__(256) void trace_kernel(TraceParams q) {
   const f3 O = mk(q.orig[3 * i], q.orig[3 * i + 1], q.orig[3 * i + 2]);
   const f3 D = mk(q.dir[3 * i], q.dir[3 * i + 1], q.dir[3 * i + 2]);
   Hit h;
-  h.pl = mk(0.0f, 0.0f, 0.0f); h.pg = h.pl; h.cull2 = 0.0;
+  h.pl = mk(0.0f, 0.0f, 0.0f); h.cull2 = 0.0;
   if (q.prim < 0) {
     traverse_lane<false, ANY>(s, O, D, h, ev);
   } else {                                       // intersect_one_prim / hit_one_prim
@@ -1446,12 +1454,15 @@ __global__ __launch_bounds__(256) void trace_kernel(TraceParams q) {
   oi[0] = h.shape; oi[1] = h.index; oi[2] = h.dir;
   f3 N = mk(0.0f, 0.0f, 0.0f), P = N;
   float4 col = make_float4(0.0f, 0.0f, 0.0f, 0.0f), mat = col;
+  f3 pg = h.pl;   // (0,0,0) on a miss
   if (h.shape >= 0) {
+    const size_t b = (size_t)h.index * 8;
+    pg = xpoint(s.prims[b + 3], s.prims[b + 4], s.prims[b + 5], h.pl);
     geom_info<false>(s, h, N, P, ev);
     col = s.prims[(size_t)h.index * 8 + 6];
     mat = s.prims[(size_t)h.index * 8 + 7];
   }
-  const float v[kTraceFloats] = {h.shape >= 0 ? h.dist : kFLTMAX, h.pl.x, h.pl.y, h.pl.z, h.pg.x, h.pg.y, h.pg.z,
+  const float v[kTraceFloats] = {h.shape >= 0 ? h.dist : kFLTMAX, h.pl.x, h.pl.y, h.pl.z, pg.x, pg.y, pg.z,
                                  N.x, N.y, N.z, P.x, P.y, P.z, col.x, col.y, col.z, col.w, mat.x, mat.y, mat.z, mat.w};
 #pragma unroll
   for (int k = 0; k < kTraceFloats; ++k) o[k] = v[k];
