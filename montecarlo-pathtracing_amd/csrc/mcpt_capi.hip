@@ -271,8 +271,8 @@ int mcpt_destroy(mcpt_ctx* c) {
 
 int mcpt_upload_scene(mcpt_ctx* c, const float* prims, int n_prims, const float* nodes, const int* leaves,
                       int depth, int nb_emissives) {
-  // n_prims < 2^28: the kernel packs a primitive index with its type code in one word
-  if (!c || !prims || !nodes || !leaves || n_prims <= 0 || n_prims >= (1 << 28) || depth < 0 || depth > 24)
+  // n_prims < 2^24: the kernel packs a hit's primitive index, shape and face in one word
+  if (!c || !prims || !nodes || !leaves || n_prims <= 0 || n_prims >= (1 << 24) || depth < 0 || depth > 24)
     return set_err(MCPT_ERR_INVALID_ARG, "mcpt_upload_scene: bad arguments");
   const int n_leaf = 1 << depth, n_node = 2 * n_leaf - 1;
   for (int i = 0; i < n_leaf; ++i)

@@ -83,12 +83,27 @@ __device__ __forceinline__ float wrcp(float x) { return 1.0f / x; }
 // Closest-hit record.  The world-space hit point is not kept: it is xpoint(transform of
 // `index`, pl), recomputed by geom_info with the same operations accept_cand used (same bits),
 // which keeps 3 VGPRs out of the traversal's live state.
+//
+// The hit's primitive, shape and face are one word, `code` = shape << 28 | face << 24 | index
+// (-1: no hit; index < 2^24, mcpt_upload_scene), so the record a walk carries is 7 VGPRs
+// (pl, dist, code, cull2).  A mesh hit's face is its mesh-local triangle (`tri`, mesh kernels
+// only; the reference's tri_index).
 struct Hit {
   f3 pl;
   float dist;
-  int index, shape, dir;
+  int code;
+  int tri;
   double cull2;   // (midpoint between dist and the next float above)^2, exact in binary64
+  __device__ __forceinline__ int shape() const { return code >> 28; }
+  __device__ __forceinline__ int index() const { return code & 0x00FFFFFF; }
+  __device__ __forceinline__ int face() const { return (code >> 24) & 15; }
+  __device__ __forceinline__ bool hit() const { return code >= 0; }
+  __device__ __forceinline__ void clear() { code = -1; }
+  __device__ __forceinline__ void set(int index, int shape, int face) { code = (shape << 28) | (face << 24) | index; }
 };
+// (shape, index) of the primary-hit cache: the same word with the face dropped (the cached
+// N, P make the face unnecessary)
+__device__ __forceinline__ int hit_key(const Hit& h) { return h.hit() ? (h.code & ~0x0F000000) : -1; }
 
 // The BVH cull `length(O - Pg) <= dist` (raytracer_func.frag:351) without the sqrt: for
 // binary32 d2 >= 0 and c >= 0, RN(sqrt(d2)) <= c  <=>  sqrt(d2) < m, m = the midpoint
@@ -251,7 +266,7 @@ __device__ __forceinline__ void accept_cand(const SR& s, int index, int shape, i
   f3 Pg = xpoint(ld4<U>(s.prims, b + 3), ld4<U>(s.prims, b + 4), ld4<U>(s.prims, b + 5), Pl);
   float dist = wlength3(sub(Ol, Pg));
   if (dist < h.dist) {
-    h.dist = dist; h.pl = Pl; h.index = index; h.shape = shape; h.dir = dir;
+    h.dist = dist; h.pl = Pl; h.set(index, shape, dir);
     h.cull2 = cull_bound_sq(dist);
   }
 }
@@ -282,7 +297,7 @@ __device__ __forceinline__ void tri_test(const SR& s, int tri_base, int t, int i
     const f3 Pg = xpoint(t0, t1, t2, Pl);
     const float dist = wlength3(sub(Ol, Pg));
     if (dist < h.dist) {
-      h.dist = dist; h.pl = Pl; h.index = index; h.shape = CODE_MESH; h.dir = t;
+      h.dist = dist; h.pl = Pl; h.set(index, CODE_MESH, 0); h.tri = t;
       h.cull2 = cull_bound_sq(dist);
     }
   }
@@ -309,7 +324,7 @@ __device__ __forceinline__ void mesh_test(const SR& s, int mesh, int index, f3 O
       const int t = s.mleaves[mi.y + node - leaf0];
       if (t >= 0) {
         tri_test<COUNT>(s, mi.w, t, index, O, D, Ol, t0, t1, t2, h, ev);
-        if (ANY && h.shape >= 0) return;   // hit_only (:664-665)
+        if (ANY && h.hit()) return;   // hit_only (:664-665)
       }
     } else {
       ev.inc(EV_NODE);
@@ -442,7 +457,7 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
 template <bool COUNT, bool ANY = false, class SR>
 __device__ __forceinline__ void traverse_lane(const SR& s, f3 O, f3 D, Hit& h, Ev<COUNT>& ev) {
   ev.inc(EV_TRAV);
-  h.index = -1; h.dist = kFLTMAX; h.shape = -1; h.dir = -1; h.cull2 = cull_bound_sq(kFLTMAX);
+  h.clear(); h.dist = kFLTMAX; h.cull2 = cull_bound_sq(kFLTMAX);
   const f3 invD = mk(rcp_rn(D.x), rcp_rn(D.y), rcp_rn(D.z));
   const int leaf0 = (1 << s.depth) - 1;
   int node = 0, level = 0;
@@ -457,7 +472,7 @@ __device__ __forceinline__ void traverse_lane(const SR& s, f3 O, f3 D, Hit& h, E
       ev.inc(EV_LEAF);
       int p = s.leaves[node - leaf0];
       if (p >= 0) prim_test<COUNT, false, ANY>(s, p, O, D, h, ev);
-      if (ANY && h.shape >= 0) break;
+      if (ANY && h.hit()) break;
     }
 #ifdef MCPT_STAMPS
     ev.st_leaf += __builtin_amdgcn_s_memtime() - t0;
@@ -513,7 +528,7 @@ __device__ __forceinline__ void walk_begin(const SR& s, f3 D, Hit& h, Walk& w, E
   ev.inc(EV_TRAV);
   // cull2_max = cull_bound_sq(kFLTMAX), a kernel argument (SGPRs) rather than a constant the
   // register allocator keeps in (spilled) VGPRs across the render loop
-  h.index = -1; h.dist = kFLTMAX; h.shape = -1; h.dir = -1; h.cull2 = cull2_max;
+  h.clear(); h.dist = kFLTMAX; h.cull2 = cull2_max;
   w.invD = mk(rcp_rn(D.x), rcp_rn(D.y), rcp_rn(D.z));
   w.node = 0; w.level = 0; w.pending = 0;
   if constexpr (SR::kMesh) w.mprim = -1;
@@ -707,7 +722,7 @@ __device__ __forceinline__ bool walk_run_mesh(const SR& s, f3 O, f3 D, Hit& h, W
 template <bool COUNT, class SR>
 __device__ __forceinline__ void traverse_wave(const SR& s, f3 O, f3 D, Hit& h, Ev<COUNT>& ev) {
   ev.inc(EV_TRAV);
-  h.index = -1; h.dist = kFLTMAX; h.shape = -1; h.dir = -1; h.cull2 = cull_bound_sq(kFLTMAX);
+  h.clear(); h.dist = kFLTMAX; h.cull2 = cull_bound_sq(kFLTMAX);
   const f3 invD = mk(rcp_rn(D.x), rcp_rn(D.y), rcp_rn(D.z));
   const int leaf0 = (1 << s.depth) - 1;
   uint32_t lpend = 0;    // bit L: this lane pushed the left child at level L of the cursor path
@@ -766,33 +781,34 @@ __device__ __forceinline__ void traverse(const SR& s, f3 O, f3 D, Hit& h, Ev<COU
 template <bool COUNT, class SR>
 __device__ __forceinline__ void geom_info(const SR& s, const Hit& h, f3& N, f3& P, Ev<COUNT>& ev) {
   ev.inc(EV_GEOM);
-  const float4* pr = s.prims + (size_t)h.index * 8;
+  const int shape = h.shape(), dir = h.face();
+  const float4* pr = s.prims + (size_t)h.index() * 8;
   float4 t0 = pr[3], t1 = pr[4], t2 = pr[5];
   P = xpoint(t0, t1, t2, h.pl);   // = the candidate's Pg (accept_cand / tri_test)
   f3 q;
-  if (h.shape == CODE_SPHERE) {
+  if (shape == CODE_SPHERE) {
     q = muls(h.pl, 2.0f);
-  } else if (h.shape == CODE_CUBE) {
-    float sg = (h.dir % 2 != 0) ? 1.0f : -1.0f;
-    int ax = h.dir / 2;
+  } else if (shape == CODE_CUBE) {
+    float sg = (dir % 2 != 0) ? 1.0f : -1.0f;
+    int ax = dir / 2;
     q = add(h.pl, mk(ax == 0 ? sg : 0.0f, ax == 1 ? sg : 0.0f, ax == 2 ? sg : 0.0f));
-  } else if (h.shape == CODE_CYLINDER) {
-    f3 No = (h.dir < 2) ? mk(0.0f, 0.0f, (h.dir % 2 != 0) ? 1.0f : -1.0f) : mk(h.pl.x, h.pl.y, 0.0f);
+  } else if (shape == CODE_CYLINDER) {
+    f3 No = (dir < 2) ? mk(0.0f, 0.0f, (dir % 2 != 0) ? 1.0f : -1.0f) : mk(h.pl.x, h.pl.y, 0.0f);
     q = add(h.pl, No);
-  } else if (h.shape == CODE_CONE) {
-    if (h.dir == 1) { N = mk(0.0f, 0.0f, 0.0f); return; }
-    if (h.dir == 0) q = mk(h.pl.x, h.pl.y, h.pl.z - 1.0f);
+  } else if (shape == CODE_CONE) {
+    if (dir == 1) { N = mk(0.0f, 0.0f, 0.0f); return; }
+    if (dir == 0) q = mk(h.pl.x, h.pl.y, h.pl.z - 1.0f);
     else {
       float lxy = sqrt_rn(__builtin_fmaf(h.pl.y, h.pl.y, h.pl.x * h.pl.x));
       q = add(h.pl, mk(h.pl.x, h.pl.y, lxy / 2.0f));
     }
-  } else if (h.shape == CODE_QUAD) {
+  } else if (shape == CODE_QUAD) {
     q = add(h.pl, mk(0.0f, 0.0f, 1.0f));
   } else {   // CODE_MESH: mesh_inter_geom_info :783-810 (smooth unless flat_face)
     if constexpr (SR::kMesh) {
       ev.inc(EV_MGEOM);
-      const int4 mi = s.minfo[s.ptype[h.index] >> 4];
-      const int4 vi = s.mtris[mi.w + h.dir];
+      const int4 mi = s.minfo[s.ptype[h.index()] >> 4];
+      const int4 vi = s.mtris[mi.w + h.tri];
       const float4 a4 = s.mverts[vi.x], b4 = s.mverts[vi.y], c4 = s.mverts[vi.z];
       const f3 A = mk(a4.x, a4.y, a4.z), Bv = mk(b4.x, b4.y, b4.z), C = mk(c4.x, c4.y, c4.z);
       if (s.flat_face) {
@@ -935,9 +951,11 @@ template <bool COUNT, bool WAVE, bool MESH, bool LDSS, bool SUSPEND>
 #define MCPT_MIN_WAVES_MESH 4
 #endif
 // per-lane walks over scenes read through L1/L2 (not LDS-staged: scenes 3, 5, 7, 8): 6 waves/SIMD
-// leave the walk more registers (profiles/r01_ab35_occupancy_v12.jsonl)
+// while their state spilled at 7 (profiles/r01_ab35_occupancy_v12.jsonl); with the packed hit
+// record they fit 72 VGPRs and 7 waves hide more of the dependent node loads (scene 8 +4 %,
+// scene 3 +5 %: profiles/r02_ab4_spill_free.jsonl)
 #ifndef MCPT_MIN_WAVES_L2
-#define MCPT_MIN_WAVES_L2 6
+#define MCPT_MIN_WAVES_L2 7
 #endif
 __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
                                            : (!WAVE && !LDSS ? MCPT_MIN_WAVES_L2 : MCPT_MIN_WAVES)) void render_kernel(
@@ -1041,7 +1059,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
   f3 N = mk(0.0f, 0.0f, 0.0f), P = mk(0.0f, 0.0f, 0.0f);
   int bounce = 0, phase = 0;
   Hit h;
-  h.pl = mk(0.0f, 0.0f, 0.0f); h.dist = kFLTMAX; h.index = -1; h.shape = -1; h.dir = -1;
+  h.pl = mk(0.0f, 0.0f, 0.0f); h.dist = kFLTMAX; h.clear(); h.tri = 0;
   h.cull2 = 0.0;
 
   // Primary-ray cache.  The camera ray of a pixel is the same in every pass (fixed
@@ -1050,7 +1068,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
   // traversal of every pass has one result per pixel: compute it once per segment.
   // Exact (same values); the counting build keeps the reference's per-pass traversal so
   // its events stay the reference's algorithmic model.
-  int shape0 = -1, idx0 = -1;
+  int key0 = -1;
   f3 N0 = N, P0 = P;   // only live until stored to LDS
   const bool run = !(p.variant == 0 && B <= 0);
 #ifdef MCPT_STAMPS
@@ -1059,12 +1077,12 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
 #endif
   if (!COUNT && run) {
     traverse<COUNT, WAVE>(s, Ocam, Dcam0, h, ev);
-    shape0 = h.shape; idx0 = h.index;
-    if (shape0 >= 0) geom_info<COUNT>(s, h, N0, P0, ev);
+    key0 = hit_key(h);
+    if (h.hit()) geom_info<COUNT>(s, h, N0, P0, ev);
   }
   s_pix[3][pslot] = N0.x; s_pix[4][pslot] = N0.y; s_pix[5][pslot] = N0.z;
   s_pix[6][pslot] = P0.x; s_pix[7][pslot] = P0.y; s_pix[8][pslot] = P0.z;
-  s_hit0[pslot] = shape0 < 0 ? -1 : (shape0 << 28) | idx0;   // idx0 < 2^28 (mcpt_upload_scene)
+  s_hit0[pslot] = key0;   // shape << 28 | index, -1: miss
 
 #ifdef MCPT_STAMPS
   const unsigned long long st_p = __builtin_amdgcn_s_memtime() - st_k0;
@@ -1073,9 +1091,9 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
   auto flush_sum = [&]() {
     // the pixel's address is recomputed at each flush (an empty asm makes the row opaque):
     // hoisted out of the render loop, its 64-bit index and pointer were 4 spilled VGPRs
-    int lrow = lr;
-    asm volatile("" : "+v"(lrow));
-    const size_t px = (size_t)lrow * p.W + x;
+    int lrow = lr, col = x;
+    asm volatile("" : "+v"(lrow), "+v"(col));
+    const size_t px = (size_t)lrow * p.W + col;
     if (p.n_segments == 1) {
       float* accp = p.accum + px * 3;
       accp[0] = accp[0] + s_pix[12][tid]; accp[1] = accp[1] + s_pix[13][tid]; accp[2] = accp[2] + s_pix[14][tid];
@@ -1141,9 +1159,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
       done = true;   // for(i=0; i<NB_BOUNCES ...) never runs: black
     } else {
       if (first) {
-        const int hv = s_hit0[pslot];
-        h.shape = hv < 0 ? -1 : hv >> 28;
-        h.index = hv < 0 ? -1 : hv & 0x0FFFFFFF;
+        h.code = s_hit0[pslot];
       } else if (WAVE) {
         traverse<COUNT, WAVE>(s, O, D, h, ev);
       } else {
@@ -1175,14 +1191,14 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
     bool fold_end = !COUNT && ready && run && p.variant == 0 && phase == 0 && !first;
     f3 fres = mk(0.0f, 0.0f, 0.0f);
     if (fold_end) {
-      if (h.shape < 0) {
+      if (!h.hit()) {
         const float a = gmax(0.0f, D.z);
         fres = add(total, mulv(att, gmix3(mk(0.5f, 0.5f, 0.9f), mk(1.0f, 1.0f, 0.8f), a)));
       } else {
 #if MCPT_FOLD_END
-        const float4 m4 = s.prims[(size_t)h.index * 8 + 7];
+        const float4 m4 = s.prims[(size_t)h.index() * 8 + 7];
         if (!(m4.z <= 0.5f)) {   // the shading block's emissive `else`, NaN included
-          const float4 c4 = s.prims[(size_t)h.index * 8 + 6];
+          const float4 c4 = s.prims[(size_t)h.index() * 8 + 6];
           fres = add(total, add(muls(mk(c4.x, c4.y, c4.z), 0.1f), muls(muls(muls(att, m4.z), 1.0f - m4.x), c4.w)));
         } else if (bounce < B - 1) {
           fold_end = false;
@@ -1204,9 +1220,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
         O = Ocam; D = mk(s_pix[0][pslot], s_pix[1][pslot], s_pix[2][pslot]);
         att = mk(0.8f, 0.8f, 0.8f); total = mk(0.0f, 0.0f, 0.0f);
         bounce = 0;
-        const int hv = s_hit0[pslot];
-        h.shape = hv < 0 ? -1 : hv >> 28;
-        h.index = hv < 0 ? -1 : hv & 0x0FFFFFFF;
+        h.code = s_hit0[pslot];
         first = true;
       } else {
         ready = false;   // unit finished: the lane claims another at the end of the round
@@ -1218,7 +1232,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
     // random_ray jobs of this round — `ray` for a non-emissive hit, and the reflect branch's
     // direction where the lane will take it (the mixed branch's coin is drawn ahead at its
     // place in the sequence, rng + 2)
-    const bool shade0 = ready && run && p.variant == 0 && phase == 0 && h.shape >= 0;
+    const bool shade0 = ready && run && p.variant == 0 && phase == 0 && h.hit();
     float4 c4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), m4 = c4;
     bool need1 = false, need2 = false, mixed = false;
     if (shade0) {
@@ -1229,8 +1243,8 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
         geom_info<COUNT>(s, h, N, P, ev);
       }
       ev.inc(EV_COLMAT);
-      c4 = s.prims[(size_t)h.index * 8 + 6];
-      m4 = s.prims[(size_t)h.index * 8 + 7];
+      c4 = s.prims[(size_t)h.index() * 8 + 6];
+      m4 = s.prims[(size_t)h.index() * 8 + 7];
       if (m4.z <= 0.5f) {
         need1 = true;
         if (m4.x > 0.0f && c4.w == 1.0f) {
@@ -1253,7 +1267,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
     if (ready && run) {
       if (p.variant != 0) {
         // tp/montecarlo_mat.frag:5-20 / montecarlo_mat_tr.frag:5-20
-        if (h.shape < 0) {
+        if (!h.hit()) {
           res = mk(0.0f, 0.0f, 0.2f);
         } else {
           if (first) {
@@ -1266,7 +1280,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
             float rx = rnd(rng), ry = rnd(rng), rz = rnd(rng);
             res = mk(__builtin_fabsf(N.x) * rx, __builtin_fabsf(N.y) * ry, __builtin_fabsf(N.z) * rz);
           } else {
-            float4 col = s.prims[(size_t)h.index * 8 + 6];
+            float4 col = s.prims[(size_t)h.index() * 8 + 6];
             float r = rnd(rng);
             res = mk(col.x * r, col.y * r, col.z * r);
           }
@@ -1274,7 +1288,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
         done = true;
       } else if (phase == 0) {
         // tp/montecarlo.frag:100-179, one bounce
-        if (h.shape < 0) {
+        if (!h.hit()) {
           float a = gmax(0.0f, D.z);
           res = add(total, mulv(att, gmix3(mk(0.5f, 0.5f, 0.9f), mk(1.0f, 1.0f, 0.8f), a)));
           done = true;
@@ -1289,8 +1303,8 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
           }
           else geom_info<COUNT>(s, h, N, P, ev);
           ev.inc(EV_COLMAT);
-          const float4 c4 = s.prims[(size_t)h.index * 8 + 6];
-          const float4 m4 = s.prims[(size_t)h.index * 8 + 7];
+          const float4 c4 = s.prims[(size_t)h.index() * 8 + 6];
+          const float4 m4 = s.prims[(size_t)h.index() * 8 + 7];
           f3 ray = random_ray(rng, N, 1.0f - m4.y);
 #endif
           const f3 col = mk(c4.x, c4.y, c4.z);
@@ -1361,7 +1375,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
         }
       } else {
         // inner traversal of the refraction branches (montecarlo.frag:148-152 / 162-165)
-        if (h.shape >= 0) {
+        if (h.hit()) {
           geom_info<COUNT>(s, h, N, P, ev);
         } else {
           N = mk(s_pix[9][tid], s_pix[10][tid], s_pix[11][tid]);
@@ -1446,23 +1460,25 @@ __global__ __launch_bounds__(256) void trace_kernel(TraceParams q) {
   if (q.prim < 0) {
     traverse_lane<false, ANY>(s, O, D, h, ev);
   } else {                                       // intersect_one_prim / hit_one_prim
-    h.index = -1; h.dist = kFLTMAX; h.shape = -1; h.dir = -1; h.cull2 = cull_bound_sq(kFLTMAX);
+    h.clear(); h.dist = kFLTMAX; h.cull2 = cull_bound_sq(kFLTMAX);
     prim_test<false, false, ANY>(s, q.prim, O, D, h, ev);
   }
   float* o = q.out + i * kTraceFloats;
   int* oi = q.out_i + i * 3;
-  oi[0] = h.shape; oi[1] = h.index; oi[2] = h.dir;
+  oi[0] = h.hit() ? h.shape() : -1;
+  oi[1] = h.hit() ? h.index() : -1;
+  oi[2] = !h.hit() ? -1 : (h.shape() == CODE_MESH ? h.tri : h.face());
   f3 N = mk(0.0f, 0.0f, 0.0f), P = N;
   float4 col = make_float4(0.0f, 0.0f, 0.0f, 0.0f), mat = col;
   f3 pg = h.pl;   // (0,0,0) on a miss
-  if (h.shape >= 0) {
-    const size_t b = (size_t)h.index * 8;
+  if (h.hit()) {
+    const size_t b = (size_t)h.index() * 8;
     pg = xpoint(s.prims[b + 3], s.prims[b + 4], s.prims[b + 5], h.pl);
     geom_info<false>(s, h, N, P, ev);
-    col = s.prims[(size_t)h.index * 8 + 6];
-    mat = s.prims[(size_t)h.index * 8 + 7];
+    col = s.prims[(size_t)h.index() * 8 + 6];
+    mat = s.prims[(size_t)h.index() * 8 + 7];
   }
-  const float v[kTraceFloats] = {h.shape >= 0 ? h.dist : kFLTMAX, h.pl.x, h.pl.y, h.pl.z, pg.x, pg.y, pg.z,
+  const float v[kTraceFloats] = {h.hit() ? h.dist : kFLTMAX, h.pl.x, h.pl.y, h.pl.z, pg.x, pg.y, pg.z,
                                  N.x, N.y, N.z, P.x, P.y, P.z, col.x, col.y, col.z, col.w, mat.x, mat.y, mat.z, mat.w};
 #pragma unroll
   for (int k = 0; k < kTraceFloats; ++k) o[k] = v[k];
