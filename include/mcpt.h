@@ -151,6 +151,17 @@ int mcpt_accum_device_ptr(mcpt_ctx* ctx, void** dev_ptr, size_t* bytes);
  * (e.g. a torch tensor that feeds the RCCL gather), ordered on the context's stream. */
 int mcpt_copy_accum_device(mcpt_ctx* ctx, void* dst_dev_ptr, size_t bytes);
 
+/* Multi-GPU frame assembly inside ONE process (the C++ host's N-GPU path: one context and
+ * host thread per device): copy every shard context's local rows into `frame`'s accumulator
+ * at their global rows, device to device (hipMemcpyPeerAsync over xGMI, one copy per run of
+ * consecutive global rows), ordered after the shards' queued renders and on `frame`'s stream.
+ * `frame` holds a full-frame target of the shards' W x H (mcpt_set_target(W, H, b, 1, 0));
+ * rows no shard holds keep their values; every shard must hold the same pass count, which
+ * becomes frame's.  Replaces montecarlo.cpp's single-FBO read (:59-70) for sharded renders.
+ * Multi-process (torch.distributed) callers gather mcpt_accum_device_ptr with RCCL instead.
+ * Asynchronous; mcpt_read_accum(frame) synchronizes. */
+int mcpt_gather_rows(mcpt_ctx* frame, mcpt_ctx* const* shards, int n_shards);
+
 /* Select the traversal strategy (mcpt_traversal) for later renders; default AUTO.
  * mcpt_get_traversal reports the strategy the next render uses (under AUTO: the trial mode
  * until both were timed, then the faster one).  Every strategy gives the same bits. */

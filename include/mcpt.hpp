@@ -359,6 +359,13 @@ class Renderer {
     return img;
   }
   float last_render_ms() const { float ms = 0; check(mcpt_last_render_ms(c_, &ms), "mcpt_last_render_ms"); return ms; }
+  // this (full-frame) renderer's accumulator <- the shards' rows (mcpt_gather_rows: peer copies
+  // over xGMI inside one process; asynchronous, read_accum / read_image synchronize)
+  void gather_rows(const std::vector<const Renderer*>& shards) {
+    std::vector<mcpt_ctx*> h;
+    for (const Renderer* r : shards) h.push_back(r->c_);
+    check(mcpt_gather_rows(c_, h.data(), (int)h.size()), "mcpt_gather_rows");
+  }
   void set_traversal(int mode) { check(mcpt_set_traversal(c_, mode), "mcpt_set_traversal"); }
   int width() const { return W_; }
   int height() const { return H_; }

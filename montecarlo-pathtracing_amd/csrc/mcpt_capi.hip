@@ -721,6 +721,55 @@ int mcpt_copy_accum_device(mcpt_ctx* c, void* dst, size_t bytes) {
   return MCPT_OK;
 }
 
+int mcpt_gather_rows(mcpt_ctx* frame, mcpt_ctx* const* shards, int n_shards) {
+  if (!frame || n_shards < 0 || (n_shards > 0 && !shards)) return set_err(MCPT_ERR_INVALID_ARG, "mcpt_gather_rows: bad arguments");
+  if (!frame->has_target) return set_err(MCPT_ERR_NO_TARGET, "mcpt_gather_rows: frame has no target");
+  if (frame->n_local_rows != frame->H) return set_err(MCPT_ERR_INVALID_ARG, "mcpt_gather_rows: frame target is a shard");
+  for (int k = 0; k < n_shards; ++k) {
+    const mcpt_ctx* s = shards[k];
+    if (!s || s == frame) return set_err(MCPT_ERR_INVALID_ARG, "mcpt_gather_rows: bad shard context");
+    if (!s->has_target) return set_err(MCPT_ERR_NO_TARGET, "mcpt_gather_rows: shard has no target");
+    if (s->W != frame->W || s->H != frame->H) return set_err(MCPT_ERR_INVALID_ARG, "mcpt_gather_rows: shard size differs");
+    if (s->pass_count != shards[0]->pass_count)
+      return set_err(MCPT_ERR_INVALID_ARG, "mcpt_gather_rows: shards hold different pass counts");
+  }
+  const size_t row_bytes = (size_t)frame->W * 3 * sizeof(float);
+  for (int k = 0; k < n_shards; ++k) {
+    mcpt_ctx* s = shards[k];
+    if (s->device != frame->device) {
+      int ok = 0;
+      HIP_OR_RETURN(hipDeviceCanAccessPeer(&ok, frame->device, s->device));
+      if (ok) {   // direct xGMI reads/writes between the two devices (once per process)
+        HIP_OR_RETURN(hipSetDevice(frame->device));
+        const hipError_t e = hipDeviceEnablePeerAccess(s->device, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return set_err(MCPT_ERR_HIP, "hipDeviceEnablePeerAccess", e);
+        (void)hipGetLastError();
+      }
+    }
+    // the frame's stream waits for the shard's queued work (its renders and combines)
+    hipEvent_t done = nullptr;
+    HIP_OR_RETURN(hipSetDevice(s->device));
+    HIP_OR_RETURN(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+    hipError_t e = hipEventRecord(done, s->stream);
+    if (e == hipSuccess) {
+      HIP_OR_RETURN(hipSetDevice(frame->device));
+      e = hipStreamWaitEvent(frame->stream, done, 0);
+    }
+    for (int i = 0; e == hipSuccess && i < s->n_local_rows;) {
+      int j = i + 1;   // run of consecutive global rows: one contiguous copy
+      while (j < s->n_local_rows && s->rows[(size_t)j] == s->rows[(size_t)j - 1] + 1) ++j;
+      e = hipMemcpyPeerAsync((char*)frame->d_accum + (size_t)s->rows[(size_t)i] * row_bytes, frame->device,
+                             (const char*)s->d_accum + (size_t)i * row_bytes, s->device, (size_t)(j - i) * row_bytes,
+                             frame->stream);
+      i = j;
+    }
+    (void)hipEventDestroy(done);   // released once the wait has been satisfied
+    if (e != hipSuccess) return set_err(MCPT_ERR_HIP, "mcpt_gather_rows: peer copy", e);
+  }
+  if (n_shards > 0) frame->pass_count = shards[0]->pass_count;
+  return MCPT_OK;
+}
+
 int mcpt_trace(mcpt_ctx* c, const float* origins, const float* dirs, int n, int any_hit, int prim, mcpt_hit* out) {
   if (!c || n < 0 || (n > 0 && (!origins || !dirs || !out))) return set_err(MCPT_ERR_INVALID_ARG, "mcpt_trace: bad arguments");
   if (!c->has_scene) return set_err(MCPT_ERR_NO_SCENE, "no scene uploaded");

@@ -90,6 +90,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "mcpt_clear_accum": (i, [_vp]),
         "mcpt_accum_device_ptr": (i, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(ctypes.c_size_t)]),
         "mcpt_copy_accum_device": (i, [_vp, _vp, ctypes.c_size_t]),
+        "mcpt_gather_rows": (i, [_vp, ctypes.POINTER(_vp), i]),
         "mcpt_set_traversal": (i, [_vp, i]),
         "mcpt_trace": (i, [_vp, fp, fp, i, i, i, _vp]),
         "mcpt_sample_hemisphere": (i, [_vp, fp, fp, f, i, i, fp]),
@@ -519,6 +520,12 @@ class Renderer:
         """D2D copy of the local accumulator into a device buffer (ordered on our stream)."""
         _check(lib().mcpt_copy_accum_device(self._h, _vp(dst_ptr), ctypes.c_size_t(nbytes)),
                "mcpt_copy_accum_device")
+
+    def gather_rows(self, shards) -> None:
+        """This full-frame renderer's accumulator <- the shard renderers' rows (mcpt_gather_rows:
+        device-to-device peer copies inside one process, ordered after the shards' renders)."""
+        hs = (_vp * max(len(shards), 1))(*[s._h for s in shards])
+        _check(lib().mcpt_gather_rows(self._h, hs, len(shards)), "mcpt_gather_rows")
 
     def trace(self, origins, dirs, any_hit: bool = False, prim: int = -1) -> np.ndarray:
         """Ray queries (traverse_all_bvh / just_hit_bvh, or one primitive) + intersection_info.

@@ -367,3 +367,39 @@ def test_empty_and_tiny_shards(mcpt_mod, renderer):
         part, n = renderer.read_accum()
         assert n == 2 and part.shape == (len(rows), W, 3)
         assert np.array_equal(part.view(np.uint32), full[rows].view(np.uint32))
+
+
+@pytest.mark.parametrize("world", [1, 3, 8])
+def test_gather_rows_assembles_frame(mcpt_mod, world):
+    """mcpt_gather_rows: shard contexts (balanced partition; one with its row list reversed)
+    copied into a full-frame context equal the one-context render bit for bit; the frame's
+    pass count is the shards'; bad arguments fail with a status, not silently."""
+    W, H, S, B = 37, 45, 3, 8
+    ipv, iv = mcpt_mod.camera_canonical(W, H)
+    sc = mcpt_mod.Scene.reference(6)
+    full = mcpt_mod.Renderer(0)
+    full.upload_scene(sc)
+    full.set_target(W, H)
+    full.render(ipv, iv, 1, S, 0.0, B, 1.0, 0)
+    ref, n_ref = full.read_accum()
+    shards = []
+    for rank in range(world):
+        r = mcpt_mod.Renderer(0)
+        r.upload_scene(sc)
+        from mcpt import dist
+        rows = [int(y) for y in np.nonzero(dist.balanced_owner(H, 8, world) == rank)[0]]
+        if rank == world - 1:
+            rows = rows[::-1]
+        r.set_target_rows(W, H, rows)
+        r.render(ipv, iv, 1, S, 0.0, B, 1.0, 0)
+        shards.append(r)
+    frame = mcpt_mod.Renderer(0)
+    frame.set_target(W, H)
+    frame.gather_rows(shards)
+    got, n = frame.read_accum()
+    assert n == n_ref == S
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    with pytest.raises(mcpt_mod.MCPTError):
+        shards[0].gather_rows(shards[1:] or [full])   # a shard is not a full-frame target
+    for r in shards + [frame, full]:
+        r.close()
