@@ -399,7 +399,12 @@ def test_gather_rows_assembles_frame(mcpt_mod, world):
     got, n = frame.read_accum()
     assert n == n_ref == S
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    if world > 1:
+        with pytest.raises(mcpt_mod.MCPTError):
+            shards[0].gather_rows(shards[1:])   # a shard is not a full-frame target
+    other = mcpt_mod.Renderer(0)
+    other.set_target(W + 1, H)
     with pytest.raises(mcpt_mod.MCPTError):
-        shards[0].gather_rows(shards[1:] or [full])   # a shard is not a full-frame target
-    for r in shards + [frame, full]:
+        other.gather_rows(shards)               # frame size differs from the shards'
+    for r in shards + [frame, full, other]:
         r.close()
