@@ -189,7 +189,7 @@ def main():
     sr = ShardedRenderer(W, H, args.band_rows, world, rank, local_rank)
     sr.upload_scene(scene)
     ipv, iv = mcpt.camera_canonical(W, H)
-    stream = torch.cuda.current_stream()   # the renderer's kernels and the gather run on it
+    stream = sr.stream   # the renderer's kernels, its D2D copy and the gather run on it
 
     def barrier():
         if world > 1:

@@ -130,9 +130,12 @@ class ShardedRenderer:
         import mcpt
         self.device = torch.device("cuda", local_rank)
         self.r = mcpt.Renderer(local_rank)
-        # kernels, D2D copy and the collective all run on torch's current stream of this device
-        with torch.cuda.device(self.device):
-            self.r.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
+        # The renderer's kernels, the D2D copy into the send buffer and the collective are
+        # ordered on ONE stream: a torch stream created here and handed to the library.  (Handing
+        # over torch's default stream, handle 0, would leave the library on its own non-blocking
+        # stream, and the gather would read the send buffer before the copy landed.)
+        self.stream = torch.cuda.Stream(self.device)
+        self.r.set_stream(self.stream.cuda_stream)
         if partition == "bands":
             self.r.set_target(W, H, band_rows, world, rank)
         else:
@@ -148,10 +151,17 @@ class ShardedRenderer:
         self.r.render(invPV, invV, first_pass, n_passes, date, bounces, refract_ind, variant)
 
     def gather(self) -> Optional[torch.Tensor]:
+        """Copy the local accumulator into the send buffer and gather the frame to rank 0, both
+        on `self.stream` after the queued renders; the caller's current stream is then made to
+        wait for it, so the returned frame is safe to use there."""
         n = self.g.n_local
-        if n:
-            self.r.copy_accum_device(self.g.send.data_ptr(), n * self.W * 3 * 4)
-        return self.g.gather(None)
+        caller = torch.cuda.current_stream(self.device)
+        with torch.cuda.stream(self.stream):
+            if n:
+                self.r.copy_accum_device(self.g.send.data_ptr(), n * self.W * 3 * 4)
+            frame = self.g.gather(None)
+        caller.wait_stream(self.stream)
+        return frame
 
     def close(self) -> None:
         self.r.close()
