@@ -199,7 +199,7 @@ def main():
     # AUTO times its candidate schedules (per-lane / wave-coherent walk, two or four pass
     # segments per work item) on the first sizeable launches of a scene: run those before the
     # warm-up so that every warm-up and timed step uses the pick
-    for k in range(4):
+    for k in range(mcpt.AUTO_TRIALS):
         sr.render(ipv, iv, 1, S, 0.0, B, args.ior, mcpt.MONTECARLO)
     sr.r.clear_accum()
     frame = None

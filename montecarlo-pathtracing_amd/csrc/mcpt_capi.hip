@@ -87,7 +87,8 @@ struct mcpt_ctx {
   long long tune_shape[2] = {0, 0};      // (local pixels, passes) of that launch
   long long meas_shape[2] = {0, 0};      // shape the measurements below were taken on
   int meas_segs = 0;                // pass segments of that shape (which candidates apply)
-  double tune_ns[5] = {0.0, 0.0, 0.0, 0.0, 0.0};   // ns per sample measured, by candidate (same shape)
+  double tune_ns[5] = {0.0, 0.0, 0.0, 0.0, 0.0};   // best ns per sample measured, by candidate (same shape)
+  int tune_cnt[5] = {0, 0, 0, 0, 0};                // trials of each candidate so far
   int tune_choice = 0;              // resolved candidate once all are measured
   int walk_exit = -1;               // mcpt_set_walk_exit; -1: by BVH depth
   int leaf_batch = -1;              // MCPT_LEAF_BATCH env (tuning); -1: default
@@ -149,13 +150,26 @@ static bool cand_applies(int cand, long long segs) {
 }
 static int cand_seg_per_item(int cand) { return cand == kCandLaneSeg2 ? 2 : cand == kCandLaneSeg4 ? 4 : 1; }
 
+// AUTO times every applicable candidate kTuneRounds times and keeps each one's best time:
+// round 1 in candidate order, round 2 in reverse, so that the clock ramp and cache warm-up of
+// the first launches after an upload do not favour the candidates tried last (one trial each
+// picked two- or four-segment items run to run on scene 6, 1-2.5 % apart)
+constexpr int kTuneRounds = 2;
+
 // schedule candidate of the next launch (`segs`: its pass segments)
 static int resolve_candidate(const mcpt_ctx* c, long long segs) {
   if (c->traversal != MCPT_TRAVERSAL_AUTO) return c->traversal;
   if (c->tune_choice) return c->tune_choice;
-  // next trial: the first applicable candidate not yet timed on the measured launch shape
+  // next trial: in the current round (the fewest trials of any applicable candidate), the
+  // first candidate of the round's order not yet timed that often on the measured shape
+  int round = kTuneRounds;
   for (int k = 1; k <= kCandLaneSeg4; ++k)
-    if (cand_applies(k, segs) && !(c->tune_ns[k] > 0.0)) return k;
+    if (cand_applies(k, segs)) round = std::min(round, c->tune_cnt[k]);
+  if (round >= kTuneRounds) return MCPT_TRAVERSAL_LANE;
+  for (int i = 0; i < kCandLaneSeg4; ++i) {
+    const int k = (round % 2 == 0) ? 1 + i : kCandLaneSeg4 - i;
+    if (cand_applies(k, segs) && c->tune_cnt[k] == round) return k;
+  }
   return MCPT_TRAVERSAL_LANE;
 }
 static int resolve_traversal(const mcpt_ctx* c) {
@@ -169,6 +183,7 @@ static void reset_tuning(mcpt_ctx* c) {
   c->tune_shape[0] = c->tune_shape[1] = c->meas_shape[0] = c->meas_shape[1] = 0;
   c->meas_segs = 0;
   for (double& t : c->tune_ns) t = 0.0;
+  for (int& n : c->tune_cnt) n = 0;
   c->tune_choice = 0;
 }
 
@@ -182,17 +197,21 @@ static hipError_t collect_tuning(mcpt_ctx* c) {
   // a launch of another shape restarts the comparison
   if (c->tune_shape[0] != c->meas_shape[0] || c->tune_shape[1] != c->meas_shape[1]) {
     for (double& t : c->tune_ns) t = 0.0;
+    for (int& n : c->tune_cnt) n = 0;
     c->meas_shape[0] = c->tune_shape[0];
     c->meas_shape[1] = c->tune_shape[1];
   }
-  c->tune_ns[c->tune_pending] = (double)ms * 1e6 / c->tune_samples;
+  const double ns = (double)ms * 1e6 / c->tune_samples;
+  const int k0 = c->tune_pending;
+  c->tune_ns[k0] = (c->tune_cnt[k0] == 0) ? ns : std::min(c->tune_ns[k0], ns);
+  c->tune_cnt[k0]++;
   c->tune_pending = 0;
   const double* t = c->tune_ns;
   bool all = true;
   int best = MCPT_TRAVERSAL_LANE;
   for (int k = 1; k <= kCandLaneSeg4; ++k) {
     if (!cand_applies(k, c->meas_segs)) continue;
-    if (!(t[k] > 0.0)) all = false;
+    if (c->tune_cnt[k] < kTuneRounds) all = false;
     else if (t[k] < t[best]) best = k;
   }
   if (all) c->tune_choice = best;

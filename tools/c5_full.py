@@ -44,7 +44,7 @@ def main():
     ipv, iv = mcpt.camera_canonical(W, H)
     r.set_target_rows(W, H, local_rows(H, BAND, WORLD, 0, "balanced"))
     # AUTO traversal trials on this launch shape first (same bits either way)
-    for _ in range(4):
+    for _ in range(mcpt.AUTO_TRIALS):
         r.render(ipv, iv, 1, 256, 0.0, B, 1.0, 0)
     shard_ms = []
     for rank in a.ranks:

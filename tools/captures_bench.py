@@ -29,12 +29,12 @@ def main():
     ipv, iv = mcpt.camera_canonical(W, H)
     for sid in (1, 2, 3, 4, 5, 6, 7, 8):
         r.upload_scene(mcpt.Scene.reference(sid, LIGHT))
-        for k in range(3):                        # warm-up incl. AUTO's two timing trials
+        for k in range(mcpt.AUTO_TRIALS):         # warm-up incl. AUTO's timing trials
             r.render(ipv, iv, 1 + 64 * k, 64, 0.0, B, 1.0, 0)
         r.synchronize()
         kms = 0.0
         for k in range(4):
-            r.render(ipv, iv, 193 + 64 * k, 64, 0.0, B, 1.0, 0)
+            r.render(ipv, iv, 1 + 64 * (mcpt.AUTO_TRIALS + k), 64, 0.0, B, 1.0, 0)
             kms += r.last_render_ms()
         rate = W * H * 256 / kms / 1e3
         frames = 50

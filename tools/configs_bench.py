@@ -50,7 +50,7 @@ def timed_render(r, ipv, iv, first, spp, B, ior, chunk=256):
 def tune(r, ipv, iv, B, ior, chunk=256):
     """AUTO schedule timing trials (after each scene upload), outside the measurements,
     on launches of the measured shape (timed_render's chunk)."""
-    for _ in range(4):
+    for _ in range(mcpt.AUTO_TRIALS):
         r.render(ipv, iv, 1, chunk, 0.0, B, ior, mcpt.MONTECARLO)
     r.clear_accum()
 
