@@ -220,6 +220,7 @@ def main():
         kernel_ms.append(sr.r.last_kernel_ms())   # HIP events of this launch (waits for its stop event)
     barrier()
     elapsed = time.perf_counter() - t0
+    sched = sr.r.schedule()   # what AUTO picked for this rank's timed launches
     stat_dev = sr.device if backend == "nccl" else torch.device("cpu")
     t = torch.tensor([elapsed], dtype=torch.float64, device=stat_dev)
     if world > 1:
@@ -313,7 +314,8 @@ def main():
             "kernel_ms": {"trace_avg": round(avg_trace_ms, 3), "combine_avg": round(avg_combine_ms, 3),
                           "gather_avg": round(gather_ms, 3),
                           "per_rank_trace_avg": [round(float(x), 3) for x in allstats[:, 1]],
-                          "per_rank_rows": [int(x) for x in allstats[:, 5]]},
+                          "per_rank_rows": [int(x) for x in allstats[:, 5]],
+                          "schedule_rank0": sched},
             "roofline": roof,
             "self_check": check,
         }

@@ -167,6 +167,10 @@ int mcpt_gather_rows(mcpt_ctx* frame, mcpt_ctx* const* shards, int n_shards);
  * until both were timed, then the faster one).  Every strategy gives the same bits. */
 int mcpt_set_traversal(mcpt_ctx* ctx, int mode);
 int mcpt_get_traversal(mcpt_ctx* ctx, int* resolved_mode);
+/* The whole schedule the next launch of the last launch shape uses: traversal mode, pass
+ * segments per work item (MCPT_SEG_PER_ITEM env overrides), and whether AUTO has finished its
+ * timing trials (1; always 1 for a fixed mode).  Any pointer may be NULL. */
+int mcpt_get_schedule(mcpt_ctx* ctx, int* traversal, int* seg_per_item, int* settled);
 
 /* Per-lane walks (MCPT_TRAVERSAL_LANE): the wave suspends its BVH walk loop once at most
  * `lanes` lanes are still walking, shades the finished lanes and resumes the rest with

@@ -900,6 +900,16 @@ int mcpt_get_traversal(mcpt_ctx* c, int* resolved) {
   return MCPT_OK;
 }
 
+int mcpt_get_schedule(mcpt_ctx* c, int* traversal, int* seg_per_item, int* settled) {
+  if (!c) return MCPT_ERR_INVALID_ARG;
+  const int cand = resolve_candidate(c, c->meas_segs);
+  if (traversal) *traversal = cand >= kCandLaneSeg2 ? MCPT_TRAVERSAL_LANE : cand;
+  const int env_seg = env_int("MCPT_SEG_PER_ITEM", 0);
+  if (seg_per_item) *seg_per_item = env_seg > 0 ? env_seg : cand_seg_per_item(cand);
+  if (settled) *settled = (c->traversal != MCPT_TRAVERSAL_AUTO || c->tune_choice != 0) ? 1 : 0;
+  return MCPT_OK;
+}
+
 int mcpt_set_stream(mcpt_ctx* c, void* s) {
   if (!c) return MCPT_ERR_INVALID_ARG;
   HIP_OR_RETURN(hipSetDevice(c->device));

@@ -98,6 +98,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "mcpt_trace": (i, [_vp, fp, fp, i, i, i, _vp]),
         "mcpt_sample_hemisphere": (i, [_vp, fp, fp, f, i, i, fp]),
         "mcpt_get_traversal": (i, [_vp, ip]),
+        "mcpt_get_schedule": (i, [_vp, ip, ip, ip]),
         "mcpt_set_walk_exit": (i, [_vp, i]),
         "mcpt_get_walk_exit": (i, [_vp, ip]),
         "mcpt_set_leaf_batch": (i, [_vp, i]),
@@ -590,6 +591,15 @@ class Renderer:
         m = ctypes.c_int()
         _check(lib().mcpt_get_traversal(self._h, ctypes.byref(m)), "mcpt_get_traversal")
         return m.value
+
+    def schedule(self) -> dict:
+        """The schedule of the next launch of the last launch shape (mcpt_get_schedule):
+        traversal ("lane"/"wave"), pass segments per work item, AUTO settled or not."""
+        t, k, s = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _check(lib().mcpt_get_schedule(self._h, ctypes.byref(t), ctypes.byref(k), ctypes.byref(s)),
+               "mcpt_get_schedule")
+        return {"traversal": {1: "lane", 2: "wave"}.get(t.value, str(t.value)), "seg_per_item": k.value,
+                "settled": bool(s.value)}
 
     def set_stream(self, hip_stream_ptr: int) -> None:
         _check(lib().mcpt_set_stream(self._h, _vp(hip_stream_ptr)), "mcpt_set_stream")
