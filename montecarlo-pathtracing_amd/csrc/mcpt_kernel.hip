@@ -1404,6 +1404,37 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
     st_s += __builtin_amdgcn_s_memtime();
 #endif
   }
+#ifdef MCPT_STAMPS
+  {
+    // diagnostic build (tools/stamps.py; frames whose tiles are all inside the image): wave
+    // totals = the last-finishing lane's sums (max over lanes), lane-iterations summed
+    unsigned long long vals[6] = {__builtin_amdgcn_s_memtime() - st_k0, st_p, st_t, st_s, st_it, ev.st_leaf};
+    unsigned long long it_sum = st_it, lit = ev.st_lit, wit = ev.st_wit;
+    unsigned long long nl = ev.st_nl, nw = ev.st_nw, ll = ev.st_ll, lw = ev.st_lw;
+    for (int off = 32; off > 0; off >>= 1) {
+      for (int k = 0; k < 6; ++k) { unsigned long long o = __shfl_xor(vals[k], off); vals[k] = vals[k] > o ? vals[k] : o; }
+      it_sum += __shfl_xor(it_sum, off);
+      lit += __shfl_xor(lit, off);
+      wit += __shfl_xor(wit, off);
+      nl += __shfl_xor(nl, off);
+      nw += __shfl_xor(nw, off);
+      ll += __shfl_xor(ll, off);
+      lw += __shfl_xor(lw, off);
+    }
+    if ((int)__lane_id() == __builtin_ffsll((long long)__ballot(1)) - 1 && p.events) {
+      for (int k = 0; k < 5; ++k) atomicAdd(p.events + k, vals[k]);
+      atomicAdd(p.events + 5, it_sum);
+      atomicAdd(p.events + 6, 1ull);
+      atomicAdd(p.events + 7, vals[5]);
+      atomicAdd(p.events + 9, lit);
+      atomicAdd(p.events + 10, wit);
+      atomicAdd(p.events + 11, nl);
+      atomicAdd(p.events + 12, nw);
+      atomicAdd(p.events + 13, ll);
+      atomicAdd(p.events + 14, lw);
+    }
+  }
+#endif
 #ifdef MCPT_RR_STATS
   // the wave's counters are uniform per lane; lanes leave the loop at different rounds, so the
   // last lane out holds the wave's totals (max over lanes)
