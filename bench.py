@@ -18,7 +18,8 @@ RCCL gather of the fp32 RGB shards to rank 0 inside the timed region.  Bit-ident
 rendering the same passes on one GPU; rank 0 checks that after the timed region (`self_check`:
 rows owned by every rank of the gathered frame against a single-rank render of those rows).
 ``--config c4`` (BASELINE configs[3]): scene 8, 1080p, 512 spp, B 12, the same frame split
-over N ranks — strong scaling.
+over N ranks — strong scaling.  ``--config c1`` (configs[0], the reference's CPU case): scene 1,
+256², 4 spp, B 3 — launch-bound on the GPU; its `cpu_baseline` times the whole config.
 
 Prints ONE JSON line (rank 0) with
 * `roofline` for the dominant kernel (the path-tracing kernel).  Its limiter is VALU issue,
@@ -61,7 +62,8 @@ VALU_PEAK_T = 78.64     # 256 CUs x 4 SIMD-32 x 32 lanes/clk x 2.4 GHz (a wave64
 METRIC = "Msamples/s (W×H×spp/s) + achieved HBM GB/s, 1080p scene6, 1/2/4/8 GPU"
 PMC_RECORDS = os.path.join(REPO, "profiles", "pmc_records.json")
 
-CONFIGS = {   # BASELINE.json configs[1] / configs[3]
+CONFIGS = {   # BASELINE.json configs[0] / configs[1] / configs[3]
+    "c1": dict(scene=1, width=256, height=256, spp=4, bounces=3, ior=1.0, scaling="weak"),
     "c2": dict(scene=6, width=1920, height=1080, spp=256, bounces=8, ior=1.0, scaling="weak"),
     "c4": dict(scene=8, width=1920, height=1080, spp=512, bounces=12, ior=1.0, scaling="strong"),
 }
@@ -117,7 +119,9 @@ def cpu_baseline(args, seconds: float):
     threads = max(1, min(threads, os.cpu_count() or threads))
     prims, nodes, leaves, depth, _ = orc.scene(args.scene, args.light)
     ipv, iv = orc.camera(args.width, args.height)
-    W, H, row_step = args.width, args.height, 2
+    # C1 (65,536 pixels x 4 passes) is timed whole; larger frames on every 2nd row
+    W, H = args.width, args.height
+    row_step = 1 if W * H <= (1 << 17) else 2
     rows = len(range(0, H, row_step))
     acc = np.zeros((H, W, 3), np.float32)
     samples, t0, p = 0, time.perf_counter(), 1
@@ -130,7 +134,8 @@ def cpu_baseline(args, seconds: float):
         if dt >= seconds or p > args.spp:
             break
     return {"value": round(samples / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/oracle.cpp, scene {args.scene} {W}x{H} every {row_step}nd row ({rows} rows), "
+            "sample": f"oracle/oracle.cpp, scene {args.scene} {W}x{H} "
+                      f"{'every row' if row_step == 1 else f'every {row_step}nd row'} ({rows} rows), "
                       f"passes 1..{p - 1} ({samples} samples, {dt:.1f} s), B={args.bounces}"}
 
 

@@ -22,10 +22,14 @@ cp $O/pmc_records.json profiles/pmc_records.json &&
 timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err && echo "bench ok" && cat $O/bench.json &&
 timeout -k 10 400 python bench.py --config c4 --no-cpu-baseline > $O/bench_c4.json 2> $O/bench_c4.err &&
 echo "bench c4 ok" && cat $O/bench_c4.json &&
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline > $O/prof_bench.json 2> $O/prof.err && echo "prof ok" || exit $?
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline > $O/prof_bench.json 2> $O/prof.err && echo "prof ok" &&
+timeout -k 10 200 python bench.py --config c1 > $O/bench_c1.json 2> $O/bench_c1.err && echo "bench c1 ok" || exit $?
 [ "${2:-}" = "full" ] || exit 0
 # N>1 path rehearsal on the one GPU: 2 ranks share cuda:0, gloo collectives (RCCL needs
 # one GPU per rank; the driver runs the real N>1 nccl bench on an 8-GPU node)
 MCPT_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
   --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 2 --warmup 1 --no-cpu-baseline \
   > $O/bench_gloo2.json 2> $O/bench_gloo2.err && echo "gloo2 ok" && cat $O/bench_gloo2.json
+MCPT_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
+  --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 4 --steps 2 --warmup 1 --no-cpu-baseline \
+  > $O/bench_gloo4.json 2> $O/bench_gloo4.err && echo "gloo4 ok"

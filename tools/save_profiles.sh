@@ -7,7 +7,9 @@ set -e
 V=$1; R=${2:-r02}; O=gpurun_out/$V; P=profiles/${R}_${V}
 cp $O/bench.json ${P}_bench.json
 [ -f $O/bench_c4.json ] && cp $O/bench_c4.json ${P}_bench_c4.json
-[ -f $O/bench_gloo2.json ] && cp $O/bench_gloo2.json ${P}_bench_gloo2_rehearsal.json
+[ -f $O/bench_gloo2.json ] && grep '^{' $O/bench_gloo2.json > ${P}_bench_gloo2_rehearsal.json
+[ -f $O/bench_gloo4.json ] && grep '^{' $O/bench_gloo4.json > ${P}_bench_gloo4_rehearsal.json
+[ -f $O/bench_c1.json ] && cp $O/bench_c1.json ${P}_bench_c1.json
 cp $O/prof/run_kernel_stats.csv ${P}_kernel_stats.csv
 python tools/trace_summary.py $O/prof/run_kernel_trace.csv \
   "$R $V: rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu-baseline" > ${P}_kernel_trace_summary.txt
