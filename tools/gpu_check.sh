@@ -29,7 +29,7 @@ timeout -k 10 200 python bench.py --config c1 > $O/bench_c1.json 2> $O/bench_c1.
 # one GPU per rank; the driver runs the real N>1 nccl bench on an 8-GPU node)
 MCPT_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
   --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 2 --warmup 1 --no-cpu-baseline \
-  > $O/bench_gloo2.json 2> $O/bench_gloo2.err && echo "gloo2 ok" && cat $O/bench_gloo2.json
+  > $O/bench_gloo2.json 2> $O/bench_gloo2.err && echo "gloo2 ok" &&
 MCPT_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
   --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 4 --steps 2 --warmup 1 --no-cpu-baseline \
   > $O/bench_gloo4.json 2> $O/bench_gloo4.err && echo "gloo4 ok"
