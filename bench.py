@@ -150,17 +150,19 @@ def check_rows(H: int, band_rows: int, world: int):
     return sorted(rows)
 
 
-def self_check(args, scene, ipv, iv, frame: torch.Tensor, passes_total: int, device: int):
-    """Single-rank render of `check_rows` for passes 1..passes_total (one call, chunk-aligned:
-    the accumulation contract makes it bit-equal to any chunk-aligned split)
-    against the same rows of the gathered frame."""
+def self_check(args, scene, ipv, iv, frame: torch.Tensor, n_calls: int, S: int, device: int):
+    """Single-rank render of `check_rows` with the run's own call sequence (passes [k·S+1,
+    (k+1)·S] for k < n_calls: a call that splits a 32-pass accumulation chunk adds its own
+    partial sum, DESIGN.md §3.3, so C1's 4-pass steps need the same split) against the same
+    rows of the gathered frame."""
     rows = check_rows(args.height, args.band_rows, max(args.world, 1))
     r = mcpt.Renderer(device)
     try:
         r.upload_scene(scene)
         r.set_target_rows(args.width, args.height, rows)
         r.set_traversal(mcpt.TRAVERSAL_LANE)   # no AUTO trials on this small target
-        r.render(ipv, iv, 1, passes_total, 0.0, args.bounces, args.ior, mcpt.MONTECARLO)
+        for k in range(n_calls):
+            r.render(ipv, iv, k * S + 1, S, 0.0, args.bounces, args.ior, mcpt.MONTECARLO)
         ref, n = r.read_accum()
     finally:
         r.close()
@@ -251,7 +253,7 @@ def main():
 
     check = None
     if rank == 0 and not args.no_check:
-        check = self_check(args, scene, ipv, iv, frame, (args.warmup + args.steps) * S, local_rank)
+        check = self_check(args, scene, ipv, iv, frame, args.warmup + args.steps, S, local_rank)
 
     if rank == 0:
         samples = float(W) * H * S * args.steps
