@@ -70,6 +70,11 @@ namespace mcpt {
 #ifndef MCPT_WALK_FAST_MATH
 #define MCPT_WALK_FAST_MATH 0
 #endif
+// which short sequences the L2-read kernels use (bits: 1 normalize, 2 length, 4 sqrt, 8 rcp);
+// the LDS-scene kernels use all of them
+#ifndef MCPT_L2_FAST
+#define MCPT_L2_FAST (MCPT_WALK_FAST_MATH ? 15 : 0)
+#endif
 template <bool FAST>
 __device__ __forceinline__ f3 wnormalize3(f3 a) {
   if constexpr (FAST) return normalize3(a); else return normalize3_g(a);
@@ -137,7 +142,9 @@ template <bool MESH, bool LDS = false>
 struct SceneT {
   static constexpr bool kMesh = MESH;
   static constexpr bool kLds = LDS;
-  static constexpr bool kFastMath = LDS || MCPT_WALK_FAST_MATH;   // walk-loop math (wsqrt, ...)
+  // walk-loop math (wnormalize3, wlength3, wsqrt, wrcp): short exact sequences or generic
+  static constexpr int kFast = LDS ? 15 : MCPT_L2_FAST;
+  static constexpr bool kFastNorm = kFast & 1, kFastLen = kFast & 2, kFastSqrt = kFast & 4, kFastRcp = kFast & 8;
   const float4* __restrict__ nodes;   // 3 per node: (c, has-prim) (w, 0) (1/w, 0)
   const int* __restrict__ leaves;
   const int* __restrict__ ptype;      // type code | mesh id << 4
@@ -272,7 +279,7 @@ __device__ __forceinline__ void accept_cand(const SR& s, int index, int shape, i
   const size_t b = (size_t)index * 8;
   constexpr bool U = UNI && !SR::kLds;
   f3 Pg = xpoint(ld4<U>(s.prims, b + 3), ld4<U>(s.prims, b + 4), ld4<U>(s.prims, b + 5), Pl);
-  float dist = wlength3<SR::kFastMath>(sub(Ol, Pg));
+  float dist = wlength3<SR::kFastLen>(sub(Ol, Pg));
   if (dist < h.dist) {
     h.dist = dist; h.pl = Pl; h.set(index, shape, dir);
     h.cull2 = cull_bound_sq(dist);
@@ -292,7 +299,7 @@ __device__ __forceinline__ void tri_test(const SR& s, int tri_base, int t, int i
   const f3 hv = cross3(D, edge2);
   const float det = dot3(edge1, hv);
   if (__builtin_fabsf(det) < kEPS) return;
-  const float invdet = wrcp<SR::kFastMath>(det);
+  const float invdet = wrcp<SR::kFastRcp>(det);
   const f3 sv = sub(O, vA);
   const float u = dot3(sv, hv) * invdet;
   if (u < 0.0f || u > 1.0f) return;
@@ -303,7 +310,7 @@ __device__ __forceinline__ void tri_test(const SR& s, int tri_base, int t, int i
   if (a > kEPS) {
     const f3 Pl = add(O, muls(D, a));
     const f3 Pg = xpoint(t0, t1, t2, Pl);
-    const float dist = wlength3<SR::kFastMath>(sub(Ol, Pg));
+    const float dist = wlength3<SR::kFastLen>(sub(Ol, Pg));
     if (dist < h.dist) {
       h.dist = dist; h.pl = Pl; h.set(index, CODE_MESH, 0); h.tri = t;
       h.cull2 = cull_bound_sq(dist);
@@ -371,12 +378,12 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
   const size_t b = (size_t)i * 8;
   float4 r0 = ld4<U>(s.prims, b), r1 = ld4<U>(s.prims, b + 1), r2 = ld4<U>(s.prims, b + 2);
   f3 O = xpoint(r0, r1, r2, Ow);
-  f3 D = wnormalize3<SR::kFastMath>(xdir(r0, r1, r2, Dw));
+  f3 D = wnormalize3<SR::kFastNorm>(xdir(r0, r1, r2, Dw));
   if (t == CODE_SPHERE) {
     float OO = dot3(O, O), OD = dot3(O, D), D2 = dot3(D, D);
     float delta4 = OD * OD - D2 * (OO - 1.0f);
     if (delta4 > 0.0f) {
-      float sq = wsqrt<SR::kFastMath>(delta4);
+      float sq = wsqrt<SR::kFastSqrt>(delta4);
       float a = -(OD + sq) / D2;
       if (a > kEPS) accept_cand<COUNT, UNI>(s, i, CODE_SPHERE, 0, add(O, muls(D, a)), Ow, h, ev);
       a = -(OD - sq) / D2;
@@ -421,7 +428,7 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
     float D2 = __builtin_fmaf(D.y, D.y, D.x * D.x);
     float delta4 = OD * OD - D2 * (O2 - 1.0f);
     if (delta4 > 0.0f) {
-      float a = -(OD + wsqrt<SR::kFastMath>(delta4)) / D2;
+      float a = -(OD + wsqrt<SR::kFastSqrt>(delta4)) / D2;
       if ((a > kEPS) && (a < al)) {
         float z = O.z + a * D.z;
         if (__builtin_fabsf(z) < 1.0f) { cl = 2; al = a; }
@@ -443,7 +450,7 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
     float cc = co.z * co.z - dot3(co, co) * 0.8f;
     float det = b * b - (4.0f * a) * cc;
     if (det > 0.0f) {
-      det = wsqrt<SR::kFastMath>(det);
+      det = wsqrt<SR::kFastSqrt>(det);
       float t1 = (-b - det) / (2.0f * a);
       if (__builtin_fabsf(O.z + t1 * D.z) > 1.0f) t1 = kFLTMAX;
       float t2 = (-b + det) / (2.0f * a);
@@ -678,7 +685,7 @@ __device__ __forceinline__ bool walk_run_mesh(const SR& s, f3 O, f3 D, Hit& h, W
           const size_t b = (size_t)p * 8;
           const float4 r0 = s.prims[b], r1 = s.prims[b + 1], r2 = s.prims[b + 2];
           w.Om = xpoint(r0, r1, r2, O);
-          w.Dm = wnormalize3<SR::kFastMath>(xdir(r0, r1, r2, D));
+          w.Dm = wnormalize3<SR::kFastNorm>(xdir(r0, r1, r2, D));
           w.invDm = mk(rcp_rn(w.Dm.x), rcp_rn(w.Dm.y), rcp_rn(w.Dm.z));
           w.mprim = p; w.mi = s.minfo[pt >> 4];
           w.t0 = s.prims[b + 3]; w.t1 = s.prims[b + 4]; w.t2 = s.prims[b + 5];
