@@ -71,9 +71,10 @@ namespace mcpt {
 #define MCPT_WALK_FAST_MATH 0
 #endif
 // which short sequences the L2-read kernels use (bits: 1 normalize, 2 length, 4 sqrt, 8 rcp);
-// the LDS-scene kernels use all of them
+// the LDS-scene kernels use all of them.  Default: normalize only (scenes 3/5/7/8 +1.2..+5 %;
+// sqrt alone +-0; normalize + sqrt -9..-15 %: profiles/r02_ab12_l2_fast_math.jsonl)
 #ifndef MCPT_L2_FAST
-#define MCPT_L2_FAST (MCPT_WALK_FAST_MATH ? 15 : 0)
+#define MCPT_L2_FAST (MCPT_WALK_FAST_MATH ? 15 : 1)
 #endif
 template <bool FAST>
 __device__ __forceinline__ f3 wnormalize3(f3 a) {
