@@ -408,3 +408,32 @@ def test_gather_rows_assembles_frame(mcpt_mod, world):
         other.gather_rows(shards)               # frame size differs from the shards'
     for r in shards + [frame, full, other]:
         r.close()
+
+
+def test_auto_two_round_trials_settle(mcpt_mod, renderer):
+    """AUTO times each applicable candidate twice (candidate order, then reverse) on launches of
+    one shape and then settles (mcpt_get_schedule reports it); mcpt.AUTO_TRIALS launches are
+    enough; the image equals a fixed per-lane render of the same launches."""
+    W, H, S = 1920, 1080, 256   # 8 pass segments: all four candidates apply
+    ipv, iv = mcpt_mod.camera_canonical(W, H)
+
+    def run(mode, n):
+        renderer.set_traversal(mode)
+        renderer.upload_scene(mcpt_mod.Scene.reference(6))
+        renderer.set_target(W, H)
+        sched = []
+        for k in range(n):
+            renderer.render(ipv, iv, 1 + S * k, S, 0.0, 3, 1.0, 0)
+            sched.append(renderer.schedule())
+        acc, cnt = renderer.read_accum()
+        return acc, cnt, sched
+
+    auto, n_a, sched = run(0, mcpt_mod.AUTO_TRIALS + 1)
+    assert not any(s["settled"] for s in sched[:mcpt_mod.AUTO_TRIALS - 1]), sched
+    assert sched[-1]["settled"] and sched[-1]["seg_per_item"] in (1, 2, 4), sched
+    assert sched[-1]["traversal"] in ("lane", "wave")
+    lane, n_l, fixed = run(1, mcpt_mod.AUTO_TRIALS + 1)
+    renderer.set_traversal(0)
+    assert all(s["settled"] and s["traversal"] == "lane" for s in fixed)
+    assert n_a == n_l
+    assert np.array_equal(auto.view(np.uint32), lane.view(np.uint32))
