@@ -8,9 +8,9 @@
    (double product + TwoSum + midpoint fix-up), so the vectors are bit-exact.
 2. img_s{scene}_v{variant}.npy — small accumulator images rendered by the C++ oracle
    (regression pins for the oracle and direct fixtures for the GPU tests).
-3. paths.npz (`python gen_golden.py paths`) — 320 whole samples of the integrator
-   ((pixel, pass) at 1080p on scenes 1, 6 at IOR 1.0 and 1.5, 8, and a scene with the pure
-   refraction branch) from the same independent numpy restatement extended to the camera
+3. paths.npz (`python gen_golden.py paths`) — 592 whole samples of the integrator
+   ((pixel, pass) at 1080p on all eight reference scenes, 6 and 5 also at IOR 1.5, and a scene
+   with the pure refraction branch) from the same independent numpy restatement extended to the camera
    ray, the BVH DFS, intersection_info and random_path, with the branch sequence each took.
 
 The reference itself cannot run here (no GL 4.3 / Eigen / GLFW / assimp):
@@ -742,16 +742,22 @@ PATH_CASES = [  # (scene id or 0 = pure_refraction_scene, light, ior, bounces, s
     (1, 1.2, 1.0, 3, 64), (6, 1.2, 1.0, 8, 64), (6, 0.443, 1.5, 8, 64), (8, 1.2, 1.0, 12, 64),
     (0, 1.2, 1.5, 8, 64),
 ]
+# the other reference scenes (second RNG stream, appended after the cases above so those stay
+# bit-identical): box of balls, Menger sponges, open box, material grid (IOR 1.5 too)
+PATH_CASES_2 = [
+    (2, 1.2, 1.0, 8, 48), (3, 1.2, 1.0, 8, 48), (4, 1.2, 1.0, 8, 48), (5, 1.2, 1.0, 8, 48),
+    (5, 1.2, 1.5, 8, 32), (7, 1.2, 1.0, 8, 48),
+]
 
 
-def make_path_kat(orc, rng):
+def make_path_kat(orc, rng, cases=PATH_CASES, rng2=None, cases2=()):
     """Whole samples of the integrator (pixel, pass) at 1920×1080 with the numpy restatement
     above: the oracle must reproduce every one bit for bit (tests/test_oracle_paths.py)."""
     W, H = 1920, 1080
     ipv, iv = orc.camera(W, H)
     out = {k: [] for k in ("scene", "light", "ior", "bounces", "x", "y", "npass", "rgb", "trace")}
     custom = pure_refraction_scene(orc)
-    for scene_id, li, ior, B, n in PATH_CASES:
+    for scene_id, li, ior, B, n, rng in [c + (rng,) for c in cases] + [c + (rng2,) for c in cases2]:
         prims, nodes, leaves, depth, _ = custom if scene_id == 0 else orc.scene(scene_id, li)
         for k in range(n):
             # pixels near the image centre (objects) or anywhere; every 8th sample is drawn
@@ -783,7 +789,8 @@ def make_path_kat(orc, rng):
 def main():
     from oracle import oracle as orc
     if len(sys.argv) > 1 and sys.argv[1] == "paths":   # paths.npz only (round-2 addition)
-        kat = make_path_kat(orc, np.random.default_rng(20250216))
+        kat = make_path_kat(orc, np.random.default_rng(20250216), PATH_CASES,
+                            np.random.default_rng(20251016), PATH_CASES_2)
         np.savez_compressed(os.path.join(HERE, "paths.npz"), **kat)
         codes = "".join(kat["path_trace"].tolist())
         print("wrote paths.npz:", len(kat["path_x"]), "samples; branch counts",

@@ -1,5 +1,5 @@
 """The HIP kernel against the independent integrator restatement (tests/golden/paths.npz, see
-tests/test_oracle_paths.py): every one of the 320 (pixel, pass) samples at 1080p, rendered as a
+tests/test_oracle_paths.py): every one of the 592 (pixel, pass) samples at 1080p, rendered as a
 one-pass launch of the sample's row through the C ABI, must equal the restatement bit for bit,
 under both BVH walks."""
 import numpy as np

@@ -1,12 +1,13 @@
 """The oracle's integrator pinned to an independent restatement, sample by sample.
 
-tests/golden/paths.npz holds 320 whole samples ((pixel, pass) at 1920×1080) of
+tests/golden/paths.npz holds 592 whole samples ((pixel, pass) at 1920×1080) of
 tp/montecarlo.frag:100-179 computed by the numpy float32 restatement in
 tests/golden/gen_golden.py (camera ray, intersect_bvh's literal stack DFS, intersect_bv,
 the primitive tests, intersection_info, random_path with all four material branches, the
 inner traversal and the exhausted-budget black), written from the GLSL text and the
-arithmetic contract of DESIGN.md §3, not from oracle.cpp.  The cases cover scenes 1, 6 (IOR
-1.0 and 1.5), 8 and a scene with the pure-refraction branch no reference scene reaches; each
+arithmetic contract of DESIGN.md §3, not from oracle.cpp.  The cases cover all eight reference
+scenes (6 and 5 also at IOR 1.5) and a scene with the pure-refraction branch no reference scene
+reaches; each
 case records the branch sequence its path took.  The oracle (and, in test_gpu_paths.py, the
 HIP kernel) must reproduce every sample bit for bit.
 """
@@ -36,8 +37,8 @@ def test_branch_coverage(paths):
     # exhausted budget, inner traversal missing (N, P kept)
     for c in "SERTMmFXI":
         assert codes.count(c) > 0, f"branch {c} not covered"
-    assert set(paths["path_scene"].tolist()) == {0, 1, 6, 8}
-    assert len(paths["path_x"]) == 320
+    assert set(paths["path_scene"].tolist()) == {0, 1, 2, 3, 4, 5, 6, 7, 8}
+    assert len(paths["path_x"]) == 592
 
 
 def test_oracle_matches_independent_paths(oracle_mod, paths):
