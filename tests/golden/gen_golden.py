@@ -8,9 +8,10 @@
    (double product + TwoSum + midpoint fix-up), so the vectors are bit-exact.
 2. img_s{scene}_v{variant}.npy — small accumulator images rendered by the C++ oracle
    (regression pins for the oracle and direct fixtures for the GPU tests).
-3. paths.npz (`python gen_golden.py paths`) — 592 whole samples of the integrator
+3. paths.npz (`python gen_golden.py paths`) — 688 whole samples of the integrator
    ((pixel, pass) at 1080p on all eight reference scenes, 6 and 5 also at IOR 1.5, and a scene
-   with the pure refraction branch) from the same independent numpy restatement extended to the camera
+   with the pure refraction branch; 96 of them run montecarlo_mat / montecarlo_mat_tr) from the
+   same independent numpy restatement extended to the camera
    ray, the BVH DFS, intersection_info and random_path, with the branch sequence each took.
 
 The reference itself cannot run here (no GL 4.3 / Eigen / GLFW / assimp):
@@ -559,10 +560,29 @@ def random_path(prims, boxes, leaves, depth, seed, D, O, B, ior):
     return [f32(0.0)] * 3, trace
 
 
-def sample(prims, nodes, leaves, depth, invPV, invV, W, H, x, y, npass, B, ior, date=0.0):
-    """One (pixel, pass) sample of montecarlo.frag: srand at screen_tc, then random_path."""
+def variant_path(prims, boxes, leaves, depth, seed, D, O, variant):
+    """tp/montecarlo_mat.frag:5-20 (variant 1) / tp/montecarlo_mat_tr.frag:5-20 (variant 2): one
+    traversal; a miss is (0, 0, 0.2); a hit returns abs(N) * random_vec3() (three draws, x then
+    y then z: GLSL evaluates constructor arguments left to right) or col.rgb * random_float()."""
+    hit = intersect_bvh(prims, boxes, leaves, depth, O, D)
+    if hit["shape"] < 0:
+        return [f32(0.0), f32(0.0), f32(0.2)], ["S"]
+    N, _ = intersection_info(prims, hit)
+    col = prims[hit["index"]][52:56]
+    if variant == 1:
+        r = [random_float(seed) for _ in range(3)]
+        return [f32(f32(abs(N[k])) * r[k]) for k in range(3)], ["V"]
+    r = random_float(seed)
+    return [f32(col[k] * r) for k in range(3)], ["V"]
+
+
+def sample(prims, nodes, leaves, depth, invPV, invV, W, H, x, y, npass, B, ior, date=0.0, variant=0):
+    """One (pixel, pass) sample of montecarlo.frag (or a variant): srand at screen_tc, then
+    random_path."""
     Ori, D, u, v = camera_dir(invPV, invV, W, H, x, y)
     seed = srand(u, v, npass, f32(date))
+    if variant:
+        return variant_path(prims, node_boxes(nodes), leaves, depth, seed, D, Ori, variant)
     return random_path(prims, node_boxes(nodes), leaves, depth, seed, D, Ori, B, ior)
 
 
@@ -750,14 +770,21 @@ PATH_CASES_2 = [
 ]
 
 
-def make_path_kat(orc, rng, cases=PATH_CASES, rng2=None, cases2=()):
+# the two other tp/ programs (variant 1 = montecarlo_mat.frag, 2 = montecarlo_mat_tr.frag), third
+# RNG stream, appended last: (scene, light, ior, bounces, samples, variant)
+VARIANT_CASES = [(1, 1.2, 1.0, 8, 16, 1), (6, 1.2, 1.0, 8, 16, 1), (8, 1.2, 1.0, 12, 16, 1),
+                 (1, 1.2, 1.0, 8, 16, 2), (6, 1.2, 1.0, 8, 16, 2), (8, 1.2, 1.0, 12, 16, 2)]
+
+
+def make_path_kat(orc, rng, cases=PATH_CASES, rng2=None, cases2=(), rng3=None, cases3=()):
     """Whole samples of the integrator (pixel, pass) at 1920×1080 with the numpy restatement
     above: the oracle must reproduce every one bit for bit (tests/test_oracle_paths.py)."""
     W, H = 1920, 1080
     ipv, iv = orc.camera(W, H)
-    out = {k: [] for k in ("scene", "light", "ior", "bounces", "x", "y", "npass", "rgb", "trace")}
+    out = {k: [] for k in ("scene", "light", "ior", "bounces", "x", "y", "npass", "rgb", "trace", "variant")}
     custom = pure_refraction_scene(orc)
-    for scene_id, li, ior, B, n, rng in [c + (rng,) for c in cases] + [c + (rng2,) for c in cases2]:
+    for scene_id, li, ior, B, n, variant, rng in ([c + (0, rng) for c in cases] + [c + (0, rng2) for c in cases2] +
+                                                  [c + (rng3,) for c in cases3]):
         prims, nodes, leaves, depth, _ = custom if scene_id == 0 else orc.scene(scene_id, li)
         for k in range(n):
             # pixels near the image centre (objects) or anywhere; every 8th sample is drawn
@@ -769,11 +796,11 @@ def make_path_kat(orc, rng, cases=PATH_CASES, rng2=None, cases2=()):
                 else:
                     x, y = int(rng.integers(0, W)), int(rng.integers(0, H))
                 npass = int(rng.integers(1, 84001)) if k % 3 else int(rng.integers(1, 33))
-                rgb, tr = sample(prims, nodes, leaves, depth, ipv, iv, W, H, x, y, npass, B, ior)
-                if tr[-1] == "E":
+                rgb, tr = sample(prims, nodes, leaves, depth, ipv, iv, W, H, x, y, npass, B, ior, variant=variant)
+                if tr[-1] == "E" or variant:
                     break
             for key, val in (("scene", scene_id), ("light", li), ("ior", ior), ("bounces", B), ("x", x), ("y", y),
-                             ("npass", npass), ("rgb", rgb), ("trace", "".join(tr))):
+                             ("npass", npass), ("rgb", rgb), ("trace", "".join(tr)), ("variant", variant)):
                 out[key].append(val)
     kat = {"path_" + k: np.array(v) for k, v in out.items()}
     kat["path_rgb"] = np.array(out["rgb"], np.float32)
@@ -790,11 +817,12 @@ def main():
     from oracle import oracle as orc
     if len(sys.argv) > 1 and sys.argv[1] == "paths":   # paths.npz only (round-2 addition)
         kat = make_path_kat(orc, np.random.default_rng(20250216), PATH_CASES,
-                            np.random.default_rng(20251016), PATH_CASES_2)
+                            np.random.default_rng(20251016), PATH_CASES_2,
+                            np.random.default_rng(20251017), VARIANT_CASES)
         np.savez_compressed(os.path.join(HERE, "paths.npz"), **kat)
         codes = "".join(kat["path_trace"].tolist())
         print("wrote paths.npz:", len(kat["path_x"]), "samples; branch counts",
-              {c: codes.count(c) for c in "SERTMmFXI"})
+              {c: codes.count(c) for c in "SERTMmFXIV"})
         return
     rng = np.random.default_rng(20241008)
     kat = make_kat(rng)

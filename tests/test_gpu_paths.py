@@ -1,5 +1,5 @@
 """The HIP kernel against the independent integrator restatement (tests/golden/paths.npz, see
-tests/test_oracle_paths.py): every one of the 592 (pixel, pass) samples at 1080p, rendered as a
+tests/test_oracle_paths.py): every one of the 688 (pixel, pass) samples (all three tp/ programs) at 1080p, rendered as a
 one-pass launch of the sample's row through the C ABI, must equal the restatement bit for bit,
 under both BVH walks."""
 import numpy as np
@@ -33,7 +33,7 @@ def test_gpu_matches_independent_paths(mcpt_mod, traversal):
             x, y = int(kat["path_x"][i]), int(kat["path_y"][i])
             r.set_target_rows(W, H, [y])
             r.render(ipv, iv, int(kat["path_npass"][i]), 1, 0.0, int(kat["path_bounces"][i]),
-                     float(kat["path_ior"][i]), mcpt_mod.MONTECARLO)
+                     float(kat["path_ior"][i]), int(kat["path_variant"][i]))
             acc, n = r.read_accum()
             assert n == 1
             got, want = acc[0, x], kat["path_rgb"][i]
