@@ -169,7 +169,8 @@ int mcpt_set_traversal(mcpt_ctx* ctx, int mode);
 int mcpt_get_traversal(mcpt_ctx* ctx, int* resolved_mode);
 /* The whole schedule the next launch of the last launch shape uses: traversal mode, pass
  * segments per work item (MCPT_SEG_PER_ITEM env overrides), and whether AUTO has finished its
- * timing trials (1; always 1 for a fixed mode).  Any pointer may be NULL. */
+ * timing trials (1; always 1 for a fixed mode).  Any pointer may be NULL.  No reference
+ * equivalent (the fragment shader has one fixed schedule). */
 int mcpt_get_schedule(mcpt_ctx* ctx, int* traversal, int* seg_per_item, int* settled);
 
 /* Per-lane walks (MCPT_TRAVERSAL_LANE): the wave suspends its BVH walk loop once at most
