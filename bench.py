@@ -136,7 +136,7 @@ def cpu_baseline(args, seconds: float):
     return {"value": round(samples / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
             "sample": f"oracle/oracle.cpp, scene {args.scene} {W}x{H} "
                       f"{'every row' if row_step == 1 else f'every {row_step}nd row'} ({rows} rows), "
-                      f"passes 1..{p - 1} ({samples} samples, {dt:.1f} s), B={args.bounces}"}
+                      f"passes 1..{p - 1} ({samples} samples, {dt:.3g} s), B={args.bounces}"}
 
 
 def check_rows(H: int, band_rows: int, world: int):
