@@ -143,6 +143,8 @@ class ShardedRenderer:
         self.W, self.H, self.band_rows, self.world, self.rank = W, H, band_rows, world, rank
         self.partition = partition
         self.g = FrameGather(H, W, band_rows, world, rank, self.device, group=group, partition=partition)
+        # the gather buffers were allocated (and zero-filled) on the caller's stream
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
 
     def upload_scene(self, scene) -> None:
         self.r.upload_scene(scene)
