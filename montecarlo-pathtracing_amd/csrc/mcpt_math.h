@@ -177,6 +177,34 @@ __device__ __forceinline__ float mc_log(float x) {
   return __builtin_fmaf(ef, 0.693359375f, r);
 }
 
+// mc_log for x in [2^-23, 1] (sample_hemisphere's log(1 - random_float()): random_float is a
+// multiple of 2^-23 in [0, 1 - 2^-23], so 1 - u is exact, normal and positive): the same
+// operations as mc_log with its zero / negative / inf / subnormal cases dropped, none of which
+// that domain reaches — same bits
+__device__ __forceinline__ float mc_log_unit(float x) {
+  const uint32_t b = fbits(x);
+  int e = (int)(b >> 23) - 127;
+  float m = bitsf((b & 0x007FFFFFu) | 0x3F800000u);
+  if (m > 1.41421353816986084f) { m = m * 0.5f; e += 1; }
+  float f = m - 1.0f;
+  float z = f * f;
+  float p = 7.0376836292e-2f;
+  p = __builtin_fmaf(p, f, -1.1514610310e-1f);
+  p = __builtin_fmaf(p, f, 1.1676998740e-1f);
+  p = __builtin_fmaf(p, f, -1.2420140846e-1f);
+  p = __builtin_fmaf(p, f, 1.4249322787e-1f);
+  p = __builtin_fmaf(p, f, -1.6668057665e-1f);
+  p = __builtin_fmaf(p, f, 2.0000714765e-1f);
+  p = __builtin_fmaf(p, f, -2.4999993993e-1f);
+  p = __builtin_fmaf(p, f, 3.3333331174e-1f);
+  float ef = (float)e;
+  float y = (f * z) * p;
+  y = __builtin_fmaf(ef, -2.12194440e-4f, y);
+  y = __builtin_fmaf(-0.5f, z, y);
+  float r = f + y;
+  return __builtin_fmaf(ef, 0.693359375f, r);
+}
+
 __device__ __forceinline__ float mc_exp2(float x) {
   if (x != x) return x;
   if (x >= 128.0f) return __builtin_inff();
