@@ -1350,7 +1350,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
           f3 R = greflect(neg(ray), N);
           f3 E = normalize3(sub(O, P));
           float se = gmix(100.0f, 2.0f, m4.y);
-          float spec = mc_pow(gmax(0.0f, dot3(E, R)), se);
+          float spec = mc_pow_le1(gmax(0.0f, dot3(E, R)), se);   // E, R unit: dot <= 1 + ulps
           total = add(total, add(muls(col, 0.1f), muls(muls(muls(att, m4.z), 1.0f - m4.x), alpha)));
           if (m4.z <= 0.5f) {
             const f3 mx = gmix3(att, col, m4.x);

@@ -105,7 +105,9 @@ __device__ __forceinline__ f3 grefract(f3 I, f3 N, float eta) {
   float d = dot3(N, I);
   float k = 1.0f - (eta * eta) * (1.0f - d * d);
   if (k < 0.0f) return mk(0.0f, 0.0f, 0.0f);
-  return sub(muls(I, eta), muls(N, eta * d + sqrt_rn(k)));
+  // k >= 0 here is 0 or >= 2^-24 (1 - y for a float y < 1 is exact: y <= 1 - 2^-24, or
+  // k > 0.5 when y < 0.5), or +inf / NaN: never in sqrt_core's inexact range (0, 2^-96)
+  return sub(muls(I, eta), muls(N, eta * d + sqrt_core(k)));
 }
 
 // 3x4 affine rows (row r = (m[r], m[4+r], m[8+r], m[12+r]) of a column-major mat4)
@@ -148,13 +150,9 @@ __device__ __forceinline__ void mc_sincos(float x, float& s_out, float& c_out) {
   c_out = ((qq + 1) & 2) ? -b : b;
 }
 
-// natural log (x > 0 finite expected; 0 -> -inf, <0/NaN -> NaN)
-__device__ __forceinline__ float mc_log(float x) {
-  if (!(x > 0.0f)) return (x == 0.0f) ? -__builtin_inff() : __builtin_nanf("");
-  if (x == __builtin_inff()) return x;
-  uint32_t b = fbits(x);
-  int e = 0;
-  if (b < 0x00800000u) { x = x * 8388608.0f; b = fbits(x); e = -23; }
+// natural log, normal positive finite x with bits b and exponent offset e (the polynomial
+// shared by mc_log and its domain-restricted forms below)
+__device__ __forceinline__ float mc_log_core(uint32_t b, int e) {
   e += (int)(b >> 23) - 127;
   float m = bitsf((b & 0x007FFFFFu) | 0x3F800000u);
   if (m > 1.41421353816986084f) { m = m * 0.5f; e += 1; }
@@ -176,34 +174,20 @@ __device__ __forceinline__ float mc_log(float x) {
   float r = f + y;
   return __builtin_fmaf(ef, 0.693359375f, r);
 }
-
-// mc_log for x in [2^-23, 1] (sample_hemisphere's log(1 - random_float()): random_float is a
-// multiple of 2^-23 in [0, 1 - 2^-23], so 1 - u is exact, normal and positive): the same
-// operations as mc_log with its zero / negative / inf / subnormal cases dropped, none of which
-// that domain reaches — same bits
-__device__ __forceinline__ float mc_log_unit(float x) {
-  const uint32_t b = fbits(x);
-  int e = (int)(b >> 23) - 127;
-  float m = bitsf((b & 0x007FFFFFu) | 0x3F800000u);
-  if (m > 1.41421353816986084f) { m = m * 0.5f; e += 1; }
-  float f = m - 1.0f;
-  float z = f * f;
-  float p = 7.0376836292e-2f;
-  p = __builtin_fmaf(p, f, -1.1514610310e-1f);
-  p = __builtin_fmaf(p, f, 1.1676998740e-1f);
-  p = __builtin_fmaf(p, f, -1.2420140846e-1f);
-  p = __builtin_fmaf(p, f, 1.4249322787e-1f);
-  p = __builtin_fmaf(p, f, -1.6668057665e-1f);
-  p = __builtin_fmaf(p, f, 2.0000714765e-1f);
-  p = __builtin_fmaf(p, f, -2.4999993993e-1f);
-  p = __builtin_fmaf(p, f, 3.3333331174e-1f);
-  float ef = (float)e;
-  float y = (f * z) * p;
-  y = __builtin_fmaf(ef, -2.12194440e-4f, y);
-  y = __builtin_fmaf(-0.5f, z, y);
-  float r = f + y;
-  return __builtin_fmaf(ef, 0.693359375f, r);
+// natural log (x > 0 finite expected; 0 -> -inf, <0/NaN -> NaN)
+__device__ __forceinline__ float mc_log(float x) {
+  if (!(x > 0.0f)) return (x == 0.0f) ? -__builtin_inff() : __builtin_nanf("");
+  if (x == __builtin_inff()) return x;
+  uint32_t b = fbits(x);
+  int e = 0;
+  if (b < 0x00800000u) { x = x * 8388608.0f; b = fbits(x); e = -23; }
+  return mc_log_core(b, e);
 }
+// mc_log for x in [2^-23, 1] (sample_hemisphere's log(1 - random_float()): random_float is a
+// multiple of 2^-23 in [0, 1 - 2^-23], so 1 - u is exact, normal and positive): mc_log with
+// its zero / negative / inf / subnormal cases dropped, none of which that domain reaches —
+// same bits
+__device__ __forceinline__ float mc_log_unit(float x) { return mc_log_core(fbits(x), 0); }
 
 __device__ __forceinline__ float mc_exp2(float x) {
   if (x != x) return x;
@@ -223,6 +207,19 @@ __device__ __forceinline__ float mc_exp2(float x) {
   return (r * bitsf((uint32_t)(k + 127 + 64) << 23)) * 5.42101086242752217e-20f;
 }
 
+// pow for x in [0, 1 + a few ulp] (the specular term: max(0, dot) of unit vectors, NaN -> 0):
+// mc_log's inf test is unreachable there; same bits as mc_pow
+__device__ __forceinline__ float mc_pow_le1(float x, float y) {
+  float l;
+  if (!(x > 0.0f)) l = (x == 0.0f) ? -__builtin_inff() : __builtin_nanf("");
+  else {
+    uint32_t b = fbits(x);
+    int e = 0;
+    if (b < 0x00800000u) { x = x * 8388608.0f; b = fbits(x); e = -23; }
+    l = mc_log_core(b, e);
+  }
+  return mc_exp2(y * (l * 1.44269502162933350f));
+}
 __device__ __forceinline__ float mc_pow(float x, float y) {
   return mc_exp2(y * (mc_log(x) * 1.44269502162933350f));
 }
