@@ -7,19 +7,38 @@ montecarlo.frag.  A *step* = one full C2 frame: passes [k·256+1, (k+1)·256] ac
 into the device framebuffer, then the frame gathered to rank 0 (RCCL gather for N>1).
 Scene buffers and the framebuffer are resident in HBM before the timed region.
 
-    python bench.py [--gpus N --steps K --warmup W] [--config c2|c4]
+    python bench.py [--gpus N --steps K --warmup W] [--config c1|c2|c3|c4|c5] [--rough R]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
-Multi-GPU, C2: weak scaling — per-GPU work fixed at one C2 frame's worth of samples: at N GPUs
-a step accumulates 256·N passes of the 1080p frame (progressive accumulation, as configs
-C4/C5 do), the frame split into balanced row shards across ranks (mcpt_balanced_rows:
-rotated 8-row bands; each rank H/N rows × 256·N passes = one C2 frame of samples), then one
-RCCL gather of the fp32 RGB shards to rank 0 inside the timed region.  Bit-identical to
-rendering the same passes on one GPU; rank 0 checks that after the timed region (`self_check`:
-rows owned by every rank of the gathered frame against a single-rank render of those rows).
-``--config c4`` (BASELINE configs[3]): scene 8, 1080p, 512 spp, B 12, the same frame split
-over N ranks — strong scaling.  ``--config c1`` (configs[0], the reference's CPU case): scene 1,
-256², 4 spp, B 3 — launch-bound on the GPU; its `cpu_baseline` times the whole config.
+Launch: with ``--gpus N > 1`` and no launcher (``WORLD_SIZE`` unset) the process starts N
+child ranks itself (one process per GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set, rendezvous
+on 127.0.0.1) before touching the GPU, waits for them, and prints rank 0's line after checking
+that it reports N GPUs; a failed rank stops the others and the run exits non-zero with no
+line.  A rank whose world size differs from ``--gpus``, or that sees fewer GPUs than ranks
+(RCCL), exits non-zero before rendering.  ``MCPT_DIST_BACKEND=gloo`` rehearses the N>1 path
+with ranks sharing the visible GPUs (host-staged gloo gather; the line says so).
+
+Configs (BASELINE.json ``configs``):
+* c2 (configs[1], default) — weak scaling: per-GPU work fixed at one C2 frame's worth of
+  samples: at N GPUs a step accumulates 256·N passes of the 1080p frame (progressive
+  accumulation), the frame split into balanced row shards across ranks (mcpt_balanced_rows:
+  rotated 8-row bands; each rank H/N rows × 256·N passes = one C2 frame of samples), then one
+  RCCL gather of the fp32 RGB shards to rank 0 inside the timed region.  Bit-identical to
+  rendering the same passes on one GPU; rank 0 checks that after the timed region
+  (`self_check`: rows owned by every rank of the gathered frame against a single-rank render
+  of those rows).
+* c3 (configs[2]) — scene 6, 1080p, 1024 spp per step, B 8, IOR 1.5, roughness sweep: the
+  roughness (material .y) of every non-emissive primitive set to each of 0, 0.5, 0.9, 0.99, 1
+  (SURVEY §8d), one measurement per point (``--rough R`` runs one point); `value` = the
+  sweep's samples ÷ its timed seconds, each point listed under ``config.roughness_points``.  Weak
+  scaling like c2.
+* c4 (configs[3]) — scene 8, 1080p, 512 spp, B 12, the same frame split over N ranks: strong.
+* c5 (configs[4]) — scene 6, 3840×2160, B 8, progressive accumulation toward 84,000 spp: a
+  step = 1,024 passes (a bounded slice of the target), the 4K frame split over N ranks
+  (strong); ``config.time_to_target_s`` extrapolates the measured rate to 84,000 spp (labelled
+  as an extrapolation, not a measured run of the whole target).
+* c1 (configs[0], the reference's CPU case) — scene 1, 256², 4 spp, B 3: launch-bound on the
+  GPU; its `cpu_baseline` times the whole config.
 
 Prints ONE JSON line (rank 0) with
 * `roofline` for the dominant kernel (the path-tracing kernel).  Its limiter is VALU issue,
@@ -34,8 +53,8 @@ Prints ONE JSON line (rank 0) with
   is the SURVEY §8d texel-fetch model of the reference (counted exactly by the counting build
   of the same kernel): reference-equivalent work, not HBM traffic, and never divided by the
   HBM peak.
-* `cpu_baseline` (the C++ oracle on a bounded row/pass sample of the same workload, host
-  threads stated).
+* `cpu_baseline` (the C++ oracle on a bounded row/pass sample of the same workload; threads
+  used, the host's CPU count and CPU model stated).
 """
 from __future__ import annotations
 
@@ -43,7 +62,11 @@ import argparse
 import hashlib
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
+import threading
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
@@ -51,44 +74,192 @@ sys.path.insert(0, os.path.join(REPO, "montecarlo-pathtracing_amd"))
 sys.path.insert(0, REPO)
 
 import numpy as np  # noqa: E402
-import torch  # noqa: E402  (loads the HIP runtime first; libmcpt binds to the same one)
+import torch  # noqa: E402  (loads the HIP runtime library; no HIP call until a rank runs)
 import torch.distributed as dist  # noqa: E402
 
-import mcpt  # noqa: E402
+import mcpt  # noqa: E402  (libmcpt.so is loaded lazily, on the first call)
 from mcpt.dist import ShardedRenderer, local_rows  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 VALU_PEAK_T = 78.64     # 256 CUs x 4 SIMD-32 x 32 lanes/clk x 2.4 GHz (a wave64 VALU op = 2 clk)
 METRIC = "Msamples/s (W×H×spp/s) + achieved HBM GB/s, 1080p scene6, 1/2/4/8 GPU"
 PMC_RECORDS = os.path.join(REPO, "profiles", "pmc_records.json")
+C3_ROUGHNESS = (0.0, 0.5, 0.9, 0.99, 1.0)
+C5_TARGET_SPP = 84000
 
-CONFIGS = {   # BASELINE.json configs[0] / configs[1] / configs[3]
+CONFIGS = {   # BASELINE.json configs[0..4]
     "c1": dict(scene=1, width=256, height=256, spp=4, bounces=3, ior=1.0, scaling="weak"),
     "c2": dict(scene=6, width=1920, height=1080, spp=256, bounces=8, ior=1.0, scaling="weak"),
+    "c3": dict(scene=6, width=1920, height=1080, spp=1024, bounces=8, ior=1.5, scaling="weak",
+               rough_sweep=C3_ROUGHNESS),
     "c4": dict(scene=8, width=1920, height=1080, spp=512, bounces=12, ior=1.0, scaling="strong"),
+    "c5": dict(scene=6, width=3840, height=2160, spp=1024, bounces=8, ior=1.0, scaling="strong",
+               target_spp=C5_TARGET_SPP),
 }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="c2")
+    ap.add_argument("--rough", type=float, default=None, help="c3: one roughness point instead of the sweep")
     ap.add_argument("--light", type=float, default=1.2)
     ap.add_argument("--band-rows", type=int, default=8)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (s)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-count", action="store_true", help="skip the reference-byte counting launch")
     ap.add_argument("--no-check", action="store_true", help="skip rank 0's post-run self check")
-    a = ap.parse_args()
+    a = ap.parse_args(argv)
+    if a.gpus < 1:
+        ap.error("--gpus must be >= 1")
     for k, v in CONFIGS[a.config].items():
         setattr(a, k, v)
+    if not hasattr(a, "target_spp"):
+        a.target_spp = None
+    if a.config == "c3":
+        a.rough_points = (a.rough,) if a.rough is not None else tuple(a.rough_sweep)
+    else:
+        if a.rough is not None:
+            ap.error("--rough applies to --config c3 only")
+        a.rough_points = (None,)
     return a
 
 
-def workload_key(args, passes_per_step: int) -> str:
-    return f"scene{args.scene}_{args.width}x{args.height}_{passes_per_step}spp_B{args.bounces}"
+# ------------------------------------------------------------------------------------------
+# launcher: `python bench.py --gpus N` without torchrun starts its own N ranks
+# ------------------------------------------------------------------------------------------
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_env(base: dict, rank: int, world: int, port: int) -> dict:
+    env = dict(base)
+    env.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+               GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    return env
+
+
+def spawn_ranks(cmd, world: int, base_env=None, poll_s: float = 0.2, grace_s: float = 10.0):
+    """Run `cmd` as `world` child processes (rank r gets RANK/LOCAL_RANK = r, WORLD_SIZE = world,
+    MASTER_ADDR 127.0.0.1 and a free port).  Rank 0's stdout is captured; the others' stdout
+    and every stderr pass through.  As soon as one rank exits non-zero the others are stopped
+    (SIGTERM, then SIGKILL after `grace_s`), since they would block in a collective.
+    Returns (exit status: 0, or the first failing rank's non-zero status; rank 0's stdout)."""
+    base = dict(os.environ if base_env is None else base_env)
+    port = free_port()
+    procs, out0 = [], []
+
+    def stop_all():
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        t_end = time.time() + grace_s
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, t_end - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+
+    def on_term(signum, _frame):   # the parent being stopped stops its ranks too
+        stop_all()
+        sys.exit(128 + signum)
+
+    old = signal.signal(signal.SIGTERM, on_term) if threading.current_thread() is threading.main_thread() else None
+    try:
+        for r in range(world):
+            procs.append(subprocess.Popen(cmd, env=rank_env(base, r, world, port),
+                                          stdout=subprocess.PIPE if r == 0 else None, text=True))
+        reader = threading.Thread(target=lambda: out0.append(procs[0].stdout.read()), daemon=True)
+        reader.start()
+        status = 0
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                status = bad[0]
+                break
+            if all(c == 0 for c in codes):
+                break
+            time.sleep(poll_s)
+        if status:
+            stop_all()
+        reader.join(timeout=grace_s)
+    finally:
+        if old is not None:
+            signal.signal(signal.SIGTERM, old)
+    return status, (out0[0] if out0 else "")
+
+
+def rank0_line(stdout: str, world: int):
+    """Rank 0's JSON line if it reports `world` GPUs, else None."""
+    for ln in reversed(stdout.strip().splitlines()):
+        ln = ln.strip()
+        if ln.startswith("{"):
+            try:
+                d = json.loads(ln)
+            except ValueError:
+                return None
+            return ln if d.get("n_gpus") == world else None
+    return None
+
+
+def launch(args) -> int:
+    """Parent of a plain `python bench.py --gpus N` (N > 1).  No HIP call happens here: the
+    children are fresh processes, and this process only waits and relays rank 0's line."""
+    cmd = [sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"bench: starting {args.gpus} ranks (one process per GPU)", file=sys.stderr, flush=True)
+    status, out = spawn_ranks(cmd, args.gpus)
+    if status:
+        print(f"bench: a rank failed (exit {status}); no result", file=sys.stderr, flush=True)
+        return status if status > 0 else 1
+    line = rank0_line(out, args.gpus)
+    if line is None:
+        print(f"bench: rank 0 did not report a {args.gpus}-GPU result:\n{out}", file=sys.stderr, flush=True)
+        return 1
+    print(line, flush=True)
+    return 0
+
+
+def check_world(gpus: int, world: int, backend: str, n_devices: int, local_world: int):
+    """Why this rank must not run (str), or None.  Every rank of an N-GPU run must see the
+    --gpus N it was asked for, and with RCCL one GPU of its own."""
+    if world != gpus:
+        return f"--gpus {gpus} but {world} rank(s) joined (WORLD_SIZE)"
+    if backend == "nccl" and n_devices < local_world:
+        return f"{local_world} ranks on this node but only {n_devices} visible GPU(s)"
+    if n_devices < 1:
+        return "no visible GPU"
+    return None
+
+
+# ------------------------------------------------------------------------------------------
+# workload
+# ------------------------------------------------------------------------------------------
+def workload_key(args, passes_per_step: int, rough=None) -> str:
+    k = f"scene{args.scene}_{args.width}x{args.height}_{passes_per_step}spp_B{args.bounces}"
+    if getattr(args, "ior", 1.0) != 1.0:
+        k += f"_ior{args.ior:g}"
+    if rough is not None:
+        k += f"_rough{rough:g}"
+    return k
+
+
+def build_scene(args, rough=None) -> "mcpt.Scene":
+    """The reference scene; for a C3 point, every non-emissive primitive's roughness = rough."""
+    sc = mcpt.Scene.reference(args.scene, args.light)
+    if rough is not None:
+        prims, _, _ = sc.buffers()
+        for i in range(sc.nb_prim()):
+            rec = prims[i]
+            if rec[58] > 0:   # emissive (material .z): untouched
+                continue
+            sc.set_material(i, np.concatenate([rec[52:56], [rec[56], rough, rec[58]]]).astype(np.float32))
+    return sc
 
 
 def lib_sha256() -> str:
@@ -109,17 +280,40 @@ def pmc_record(workload: str, sha: str):
     return None
 
 
-def cpu_baseline(args, seconds: float):
-    """Oracle (C++ restatement, same arithmetic) on a bounded sample of the workload:
-    every 2nd row of the frame, 1-pass launches of increasing pass number (1..spp) until
-    the budget is spent (≈10 s on the box's 16 host threads).  Threads = the host share of
-    one GPU on the box (OMP_NUM_THREADS, 16 there), else nproc."""
+def host_cpu():
+    """(logical CPUs of the host, CPU model string)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return os.cpu_count() or 1, model
+
+
+def cpu_threads() -> int:
+    """Threads for the CPU baseline: the host share of one GPU where the box sets it
+    (OMP_NUM_THREADS, 16 on the GPU box), else every logical CPU."""
+    n = os.cpu_count() or 1
+    t = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or n
+    return max(1, min(t, n))
+
+
+def cpu_baseline(args, seconds: float, rough=None):
+    """Oracle (C++ restatement, same arithmetic) on a bounded sample of the workload: every
+    2nd row of the frame (every row for C1), 1-pass launches of increasing pass number
+    (1..spp) until the budget is spent (≈10 s), std::thread over rows."""
     from oracle import oracle as orc
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    threads = max(1, min(threads, os.cpu_count() or threads))
+    threads = cpu_threads()
+    nproc, model = host_cpu()
     prims, nodes, leaves, depth, _ = orc.scene(args.scene, args.light)
+    if rough is not None:   # build_scene's override: material .y of every non-emissive record
+        prims = np.array(prims, copy=True)
+        prims[~(prims[:, 58] > 0), 57] = rough
     ipv, iv = orc.camera(args.width, args.height)
-    # C1 (65,536 pixels x 4 passes) is timed whole; larger frames on every 2nd row
     W, H = args.width, args.height
     row_step = 1 if W * H <= (1 << 17) else 2
     rows = len(range(0, H, row_step))
@@ -134,9 +328,14 @@ def cpu_baseline(args, seconds: float):
         if dt >= seconds or p > args.spp:
             break
     return {"value": round(samples / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "host_logical_cpus": nproc, "cpu_model": model,
+            "threads_note": "std::thread workers = OMP_NUM_THREADS (the host share of one GPU on the box) "
+                            "capped at the host's logical CPUs",
             "sample": f"oracle/oracle.cpp, scene {args.scene} {W}x{H} "
                       f"{'every row' if row_step == 1 else f'every {row_step}nd row'} ({rows} rows), "
-                      f"passes 1..{p - 1} ({samples} samples, {dt:.3g} s), B={args.bounces}"}
+                      f"passes 1..{p - 1} ({samples} samples, {dt:.3g} s), B={args.bounces}, IOR {args.ior:g}"
+                      + (f", roughness {rough:g}" if rough is not None else "")
+                      + ("" if row_step == 1 and p > args.spp else "; extrapolated rate, not the whole config")}
 
 
 def check_rows(H: int, band_rows: int, world: int):
@@ -171,42 +370,56 @@ def self_check(args, scene, ipv, iv, frame: torch.Tensor, n_calls: int, S: int, 
     return {"rows": len(rows), "passes": int(n), "bit_equal": diff == 0, "channels_differing": diff}
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    args.world = world
-    if os.environ.get("MCPT_DIST_BACKEND") == "gloo":
-        local_rank = local_rank % max(torch.cuda.device_count(), 1)   # ranks may share a GPU
-    if world != args.gpus and not (world == 1 and args.gpus == 1):
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
-    torch.cuda.set_device(local_rank)
-    backend = os.environ.get("MCPT_DIST_BACKEND", "nccl")   # "gloo": N>1 rehearsal on one GPU
-    if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        else:
-            dist.init_process_group(backend)
+def roofline(workload: str, sha: str, avg_trace_ms: float, ref_bytes: float, bytes_per_sample: float, world: int):
+    rec = pmc_record(workload, sha) if world == 1 else None
+    t_s = avg_trace_ms / 1e3
+    roof = {"bound": "valu", "achieved": None, "peak": VALU_PEAK_T, "unit": "T lane-instr/s", "frac": None,
+            "lane_utilisation": None, "useful_frac": None, "traffic": None,
+            "hbm": {"achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None},
+            "kernel_ms": round(avg_trace_ms, 3),
+            "pmc": {"workload": workload, "lib_sha256": sha, "matched": rec is not None,
+                    "source": rec.get("source") if rec else None,
+                    "note": None if rec else ("no rocprofv3 PMC record of this workload for this libmcpt.so "
+                                              "build (profiles/pmc_records.json): PMC fields left null"
+                                              if world == 1 else "PMC records are single-GPU measurements")}}
+    if rec is not None and t_s > 0:
+        c = rec["counters_per_launch"]
+        ach = c["SQ_INSTS_VALU"] * 64 / t_s / 1e12
+        roof["achieved"] = round(ach, 3)
+        roof["frac"] = round(ach / VALU_PEAK_T, 4)
+        lu = rec.get("valu_lane_utilisation")
+        if lu is not None:
+            roof["lane_utilisation"] = round(lu, 4)
+            roof["useful_frac"] = round(ach / VALU_PEAK_T * lu, 4)
+        roof["valu_instructions_per_launch"] = c["SQ_INSTS_VALU"]
+        traffic = rec.get("hbm_bytes_per_launch")
+        roof["traffic"] = traffic
+        if traffic is not None:
+            gbs = traffic / t_s / 1e9
+            roof["hbm"].update(achieved=round(gbs, 2), frac=round(gbs / HBM_PEAK_GBS, 5))
+        if rec.get("wave_cycle_split"):
+            roof["wave_cycle_split"] = {k: round(v, 4) for k, v in rec["wave_cycle_split"].items()}
+    roof["reference_equivalent_bytes"] = {
+        "per_launch": ref_bytes, "per_sample": round(float(bytes_per_sample), 2),
+        "rate_GBs": round(ref_bytes / t_s / 1e9, 1) if t_s > 0 else None,
+        "note": ("SURVEY §8d texel-fetch model: the bytes the reference's shader would fetch for the "
+                 "same work (event counts of the counting build). Scene records are served from "
+                 "LDS/L1/L2 here, so this is NOT HBM traffic and is never divided by the HBM peak")}
+    return roof
 
+
+def run_point(args, sr, rough, S, world, barrier, stat_dev):
+    """Upload the point's scene, AUTO trials, warm-up, K timed steps (render + gather), the
+    counting launch and rank 0's self check.  Returns this rank's figures."""
     W, H, B = args.width, args.height, args.bounces
-    # passes per step: weak (C2) = one frame of samples per GPU; strong (C4) = one frame in total
-    S = args.spp * world if args.scaling == "weak" else args.spp
-    scene = mcpt.Scene.reference(args.scene, args.light)
-    sr = ShardedRenderer(W, H, args.band_rows, world, rank, local_rank)
+    scene = build_scene(args, rough)
     sr.upload_scene(scene)
     ipv, iv = mcpt.camera_canonical(W, H)
     stream = sr.stream   # the renderer's kernels, its D2D copy and the gather run on it
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-
     # AUTO times its candidate schedules (per-lane / wave-coherent walk, two or four pass
     # segments per work item) on the first sizeable launches of a scene: run those before the
     # warm-up so that every warm-up and timed step uses the pick
-    for k in range(mcpt.AUTO_TRIALS):
+    for _ in range(mcpt.AUTO_TRIALS):
         sr.render(ipv, iv, 1, S, 0.0, B, args.ior, mcpt.MONTECARLO)
     sr.r.clear_accum()
     frame = None
@@ -228,7 +441,6 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     sched = sr.r.schedule()   # what AUTO picked for this rank's timed launches
-    stat_dev = sr.device if backend == "nccl" else torch.device("cpu")
     t = torch.tensor([elapsed], dtype=torch.float64, device=stat_dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -250,51 +462,95 @@ def main():
         allstats = torch.stack(allstats).cpu().numpy()
     else:
         allstats = stats.cpu().numpy()[None]
-
     check = None
-    if rank == 0 and not args.no_check:
-        check = self_check(args, scene, ipv, iv, frame, args.warmup + args.steps, S, local_rank)
+    if args.rank == 0 and not args.no_check:
+        check = self_check(args, scene, ipv, iv, frame, args.warmup + args.steps, S, args.local_rank)
+    return dict(rough=rough, elapsed=elapsed, sched=sched, gather_ms=gather_ms, avg_trace_ms=avg_trace_ms,
+                avg_combine_ms=avg_combine_ms, allstats=allstats, check=check)
+
+
+def main():
+    args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch(args))   # this process never touches the GPU
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    backend = os.environ.get("MCPT_DIST_BACKEND", "nccl")   # "gloo": N>1 rehearsal sharing GPUs
+    n_dev = torch.cuda.device_count()
+    why = check_world(args.gpus, world, backend, n_dev, local_world)
+    if why:
+        print(f"bench rank {rank}: {why}; not running", file=sys.stderr, flush=True)
+        sys.exit(3)
+    shared = backend != "nccl" and n_dev < local_world
+    if backend != "nccl":
+        local_rank = local_rank % n_dev   # ranks may share a GPU
+    args.world, args.rank, args.local_rank = world, rank, local_rank
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
+        if dist.get_world_size() != args.gpus:
+            print(f"bench rank {rank}: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}",
+                  file=sys.stderr, flush=True)
+            sys.exit(3)
+
+    W, H, B = args.width, args.height, args.bounces
+    # passes per step: weak (C2/C3) = one frame of samples per GPU; strong (C4/C5) = one frame in total
+    S = args.spp * world if args.scaling == "weak" else args.spp
+    sr = ShardedRenderer(W, H, args.band_rows, world, rank, local_rank)
+    stat_dev = sr.device if backend == "nccl" else torch.device("cpu")
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    points = [run_point(args, sr, rough, S, world, barrier, stat_dev) for rough in args.rough_points]
 
     if rank == 0:
-        samples = float(W) * H * S * args.steps
-        value = samples / elapsed / 1e6
-        workload = workload_key(args, S)
         sha = lib_sha256()
-        rec = pmc_record(workload, sha) if world == 1 else None
-        t_s = avg_trace_ms / 1e3
-        ref_bytes = allstats[0, 0]
-        bytes_per_sample = allstats[:, 0].sum() / max(allstats[:, 3].sum(), 1.0)
-        roof = {"bound": "valu", "achieved": None, "peak": VALU_PEAK_T, "unit": "T lane-instr/s", "frac": None,
-                "lane_utilisation": None, "useful_frac": None, "traffic": None,
-                "hbm": {"achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None},
-                "kernel_ms": round(avg_trace_ms, 3),
-                "pmc": {"lib_sha256": sha, "matched": rec is not None,
-                        "source": rec.get("source") if rec else None,
-                        "note": None if rec else "no rocprofv3 PMC record of this workload for this libmcpt.so "
-                                                 "build (profiles/pmc_records.json): PMC fields left null"}}
-        if rec is not None and t_s > 0:
-            c = rec["counters_per_launch"]
-            ach = c["SQ_INSTS_VALU"] * 64 / t_s / 1e12
-            roof["achieved"] = round(ach, 3)
-            roof["frac"] = round(ach / VALU_PEAK_T, 4)
-            lu = rec.get("valu_lane_utilisation")
-            if lu is not None:
-                roof["lane_utilisation"] = round(lu, 4)
-                roof["useful_frac"] = round(ach / VALU_PEAK_T * lu, 4)
-            roof["valu_instructions_per_launch"] = c["SQ_INSTS_VALU"]
-            traffic = rec.get("hbm_bytes_per_launch")
-            roof["traffic"] = traffic
-            if traffic is not None:
-                gbs = traffic / t_s / 1e9
-                roof["hbm"].update(achieved=round(gbs, 2), frac=round(gbs / HBM_PEAK_GBS, 5))
-            if rec.get("wave_cycle_split"):
-                roof["wave_cycle_split"] = {k: round(v, 4) for k, v in rec["wave_cycle_split"].items()}
-        roof["reference_equivalent_bytes"] = {
-            "per_launch": ref_bytes, "per_sample": round(float(bytes_per_sample), 2),
-            "rate_GBs": round(ref_bytes / t_s / 1e9, 1) if t_s > 0 else None,
-            "note": ("SURVEY §8d texel-fetch model: the bytes the reference's shader would fetch for the "
-                     "same work (event counts of the counting build). Scene records are served from "
-                     "LDS/L1/L2 here, so this is NOT HBM traffic and is never divided by the HBM peak")}
+        samples_per_step = float(W) * H * S
+        total_s = sum(pt["elapsed"] for pt in points)
+        n_steps = args.steps * len(points)
+        value = samples_per_step * n_steps / total_s / 1e6
+        main_pt = max(points, key=lambda pt: pt["avg_trace_ms"])   # the dominant kernel
+        for pt in points:
+            a = pt["allstats"]
+            pt["roof"] = roofline(workload_key(args, S, pt["rough"]), sha, pt["avg_trace_ms"], float(a[0, 0]),
+                                  float(a[:, 0].sum() / max(a[:, 3].sum(), 1.0)), world)
+        config = {
+            "workload": workload_key(args, S, main_pt["rough"] if len(points) == 1 else None)
+                        + ("_rough-sweep" if len(points) > 1 else ""),
+            "baseline_config": args.config.upper(),
+            "scene": args.scene, "width": W, "height": H, "spp_per_step": S,
+            "spp_per_gpu_step": S // world if args.scaling == "weak" else S, "bounces": B,
+            "ior": args.ior, "light_intensity": args.light, "variant": "montecarlo.frag",
+            "parallelism": (f"balanced row shards ({args.band_rows}-row bands) x{world} + "
+                            f"{'RCCL' if backend == 'nccl' else backend} gather") if world > 1 else "single GPU",
+        }
+        if world > 1:
+            config["backend"] = backend
+            if shared:
+                config["rehearsal"] = f"{world} ranks sharing {n_dev} GPU(s): checks the N>1 code path, not scaling"
+        if args.config == "c3":
+            config["roughness_points"] = [
+                {"roughness": pt["rough"], "value": round(samples_per_step * args.steps / pt["elapsed"] / 1e6, 2),
+                 "ms_per_step": round(pt["elapsed"] / args.steps * 1e3, 3),
+                 "kernel_ms": round(pt["avg_trace_ms"], 3), "schedule_rank0": pt["sched"],
+                 "roofline_frac": pt["roof"]["frac"], "self_check": pt["check"]} for pt in points]
+        if args.target_spp:
+            t_step = total_s / n_steps
+            config["target_spp"] = args.target_spp
+            config["time_to_target_s"] = round(args.target_spp / S * t_step, 3)
+            config["time_to_target_note"] = (f"extrapolated: {args.target_spp} spp / {S} spp per step x the measured "
+                                             f"{t_step * 1e3:.1f} ms per step (render + gather); not a measured run "
+                                             "of the whole target")
+        a = main_pt["allstats"]
+        checks = [pt["check"] for pt in points if pt["check"] is not None]
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -302,32 +558,29 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "ms_per_step": round(total_s / n_steps * 1e3, 3),
             "higher_is_better": True,
             "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f32",
             "data": f"synthetic (reference scene {args.scene} built by the C++ scene producer; "
                     "deterministic RNG seeds)",
-            "config": {
-                "workload": workload,
-                "baseline_config": args.config.upper(),
-                "scene": args.scene, "width": W, "height": H, "spp_per_step": S,
-                "spp_per_gpu_step": S // world if args.scaling == "weak" else S, "bounces": B,
-                "ior": args.ior, "light_intensity": args.light, "variant": "montecarlo.frag",
-                "parallelism": f"balanced row shards ({args.band_rows}-row bands) x{world} + RCCL gather"
-                               if world > 1 else "single GPU",
-            },
-            "kernel_ms": {"trace_avg": round(avg_trace_ms, 3), "combine_avg": round(avg_combine_ms, 3),
-                          "gather_avg": round(gather_ms, 3),
-                          "per_rank_trace_avg": [round(float(x), 3) for x in allstats[:, 1]],
-                          "per_rank_rows": [int(x) for x in allstats[:, 5]],
-                          "schedule_rank0": sched},
-            "roofline": roof,
-            "self_check": check,
+            "config": config,
+            "kernel_ms": {"trace_avg": round(main_pt["avg_trace_ms"], 3),
+                          "combine_avg": round(main_pt["avg_combine_ms"], 3),
+                          "gather_avg": round(main_pt["gather_ms"], 3),
+                          "per_rank_trace_avg": [round(float(x), 3) for x in a[:, 1]],
+                          "per_rank_rows": [int(x) for x in a[:, 5]],
+                          "schedule_rank0": main_pt["sched"]},
+            "roofline": main_pt["roof"],
+            "self_check": (None if not checks else
+                           {"rows": checks[0]["rows"], "passes": checks[0]["passes"],
+                            "bit_equal": all(c["bit_equal"] for c in checks),
+                            "channels_differing": sum(c["channels_differing"] for c in checks),
+                            "points": len(checks)}),
         }
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds, main_pt["rough"])
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
@@ -335,8 +588,9 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-    if check is not None and not check["bit_equal"]:
-        sys.exit(f"self check failed: {check}")
+    bad = [pt["check"] for pt in points if pt["check"] is not None and not pt["check"]["bit_equal"]]
+    if bad:
+        sys.exit(f"self check failed: {bad}")
 
 
 if __name__ == "__main__":

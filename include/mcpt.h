@@ -45,9 +45,9 @@ enum mcpt_variant {
 
 /* BVH traversal strategy of the kernel (same results, different speed) */
 enum mcpt_traversal {
-  MCPT_TRAVERSAL_AUTO = 0,   /* measured: after a scene upload, launches of >= 2^24 samples try
-                                LANE and WAVE once each on launches of the same shape (pixels,
-                                passes); later launches use the faster */
+  MCPT_TRAVERSAL_AUTO = 0,   /* measured: after a scene upload, launches of >= 2^24 samples time
+                                the schedule candidates twice each (see mcpt_set_traversal);
+                                later launches of that shape use the fastest */
   MCPT_TRAVERSAL_LANE = 1,   /* each lane walks its own DFS (divergent, vector loads) */
   MCPT_TRAVERSAL_WAVE = 2,   /* the wave walks the union of its lanes' DFS orders (scalar loads) */
 };
@@ -78,7 +78,10 @@ int mcpt_destroy(mcpt_ctx* ctx);
  *   leaves : 2^depth i32 (prim index or -1)                   — tex_ind, gpu_bvh_scene.cpp:143-144
  * Replaces BVH_GPU_Scene::finalize's Texture2D uploads (gpu_bvh_scene.cpp:143-160) and
  * the uniforms nb_prims(1), bvh_depth(2), nb_emissives(20).  Transforms must be affine
- * (row 3 = 0,0,0,1: the shader only uses .xyz).  Synchronous. */
+ * (row 3 = 0,0,0,1: the shader only uses .xyz).  Limit: n_prims < 2^24 (MCPT_ERR_INVALID_ARG
+ * otherwise) — the kernel packs a hit's primitive index, shape and face into one 32-bit word
+ * (shape << 28 | face << 24 | index), which keeps the walk's hit record in 7 registers.
+ * Synchronous. */
 int mcpt_upload_scene(mcpt_ctx* ctx, const float* prims, int n_prims, const float* nodes,
                       const int* leaves, int depth, int nb_emissives);
 
@@ -154,7 +157,10 @@ int mcpt_copy_accum_device(mcpt_ctx* ctx, void* dst_dev_ptr, size_t bytes);
 /* Multi-GPU frame assembly inside ONE process (the C++ host's N-GPU path: one context and
  * host thread per device): copy every shard context's local rows into `frame`'s accumulator
  * at their global rows, device to device (hipMemcpyPeerAsync over xGMI, one copy per run of
- * consecutive global rows), ordered after the shards' queued renders and on `frame`'s stream.
+ * consecutive global rows), ordered after the shards' queued renders and on `frame`'s stream;
+ * each shard's stream in turn waits for the copies that read its accumulator, so a
+ * progressive caller may render into a shard again right after the call (its next passes
+ * cannot reach rows still being copied).
  * `frame` holds a full-frame target of the shards' W x H (mcpt_set_target(W, H, b, 1, 0));
  * rows no shard holds keep their values; every shard must hold the same pass count, which
  * becomes frame's.  Replaces montecarlo.cpp's single-FBO read (:59-70) for sharded renders.
@@ -162,9 +168,14 @@ int mcpt_copy_accum_device(mcpt_ctx* ctx, void* dst_dev_ptr, size_t bytes);
  * Asynchronous; mcpt_read_accum(frame) synchronizes. */
 int mcpt_gather_rows(mcpt_ctx* frame, mcpt_ctx* const* shards, int n_shards);
 
-/* Select the traversal strategy (mcpt_traversal) for later renders; default AUTO.
- * mcpt_get_traversal reports the strategy the next render uses (under AUTO: the trial mode
- * until both were timed, then the faster one).  Every strategy gives the same bits. */
+/* Select the traversal strategy (mcpt_traversal) for later renders; default AUTO.  AUTO times
+ * its schedule candidates (per-lane walk, wave-coherent walk, per-lane walk with two and with
+ * four pass segments per work item, where the launch has that many segments) on the first
+ * launches of >= 2^24 samples after a scene upload: two rounds, forward then reverse order,
+ * each candidate's best time per sample kept, compared only between launches of the same shape
+ * — 8 launches in all (mcpt.AUTO_TRIALS); later launches of that shape use the fastest.
+ * mcpt_get_traversal reports the strategy the next render uses (a trial candidate until AUTO
+ * has settled: see mcpt_get_schedule's `settled`).  Every strategy gives the same bits. */
 int mcpt_set_traversal(mcpt_ctx* ctx, int mode);
 int mcpt_get_traversal(mcpt_ctx* ctx, int* resolved_mode);
 /* The whole schedule the next launch of the last launch shape uses: traversal mode, pass

@@ -752,6 +752,18 @@ int mcpt_gather_rows(mcpt_ctx* frame, mcpt_ctx* const* shards, int n_shards) {
     if (s->pass_count != shards[0]->pass_count)
       return set_err(MCPT_ERR_INVALID_ARG, "mcpt_gather_rows: shards hold different pass counts");
   }
+  // the calling thread's current device is restored on every return path
+  struct DeviceGuard {
+    int prev = -1;
+    DeviceGuard() { if (hipGetDevice(&prev) != hipSuccess) prev = -1; }
+    ~DeviceGuard() { if (prev >= 0) (void)hipSetDevice(prev); }
+  } device_guard;
+  // an event created here is destroyed on every return path (it is released by HIP once the
+  // waits recorded against it have been satisfied)
+  struct EventGuard {
+    hipEvent_t e = nullptr;
+    ~EventGuard() { if (e) (void)hipEventDestroy(e); }
+  };
   const size_t row_bytes = (size_t)frame->W * 3 * sizeof(float);
   for (int k = 0; k < n_shards; ++k) {
     mcpt_ctx* s = shards[k];
@@ -765,15 +777,14 @@ int mcpt_gather_rows(mcpt_ctx* frame, mcpt_ctx* const* shards, int n_shards) {
         (void)hipGetLastError();
       }
     }
-    // the frame's stream waits for the shard's queued work (its renders and combines)
-    hipEvent_t done = nullptr;
+    // (1) the frame's stream waits for the shard's queued work (its renders and combines)
+    EventGuard done;
     HIP_OR_RETURN(hipSetDevice(s->device));
-    HIP_OR_RETURN(hipEventCreateWithFlags(&done, hipEventDisableTiming));
-    hipError_t e = hipEventRecord(done, s->stream);
-    if (e == hipSuccess) {
-      HIP_OR_RETURN(hipSetDevice(frame->device));
-      e = hipStreamWaitEvent(frame->stream, done, 0);
-    }
+    HIP_OR_RETURN(hipEventCreateWithFlags(&done.e, hipEventDisableTiming));
+    HIP_OR_RETURN(hipEventRecord(done.e, s->stream));
+    HIP_OR_RETURN(hipSetDevice(frame->device));
+    HIP_OR_RETURN(hipStreamWaitEvent(frame->stream, done.e, 0));
+    hipError_t e = hipSuccess;
     for (int i = 0; e == hipSuccess && i < s->n_local_rows;) {
       int j = i + 1;   // run of consecutive global rows: one contiguous copy
       while (j < s->n_local_rows && s->rows[(size_t)j] == s->rows[(size_t)j - 1] + 1) ++j;
@@ -782,8 +793,14 @@ int mcpt_gather_rows(mcpt_ctx* frame, mcpt_ctx* const* shards, int n_shards) {
                              frame->stream);
       i = j;
     }
-    (void)hipEventDestroy(done);   // released once the wait has been satisfied
     if (e != hipSuccess) return set_err(MCPT_ERR_HIP, "mcpt_gather_rows: peer copy", e);
+    // (2) the shard's later work (a progressive caller's next render adds into d_accum in
+    // place) waits for the copies that read its accumulator
+    EventGuard copied;
+    HIP_OR_RETURN(hipEventCreateWithFlags(&copied.e, hipEventDisableTiming));
+    HIP_OR_RETURN(hipEventRecord(copied.e, frame->stream));
+    HIP_OR_RETURN(hipSetDevice(s->device));
+    HIP_OR_RETURN(hipStreamWaitEvent(s->stream, copied.e, 0));
   }
   if (n_shards > 0) frame->pass_count = shards[0]->pass_count;
   return MCPT_OK;

@@ -155,9 +155,17 @@ class ShardedRenderer:
     def gather(self) -> Optional[torch.Tensor]:
         """Copy the local accumulator into the send buffer and gather the frame to rank 0, both
         on `self.stream` after the queued renders; the caller's current stream is then made to
-        wait for it, so the returned frame is safe to use there."""
+        wait for it, so the returned frame is safe to use there.
+
+        The returned tensor is a buffer this renderer reuses (the frame on rank 0, the send
+        buffer at world 1): the next gather overwrites it.  That gather's writes are ordered
+        after everything the caller has queued on its current stream by then (the private
+        stream waits for it first), so work the caller queued that reads the previous frame
+        completes before the buffer changes; keep a copy (``frame.clone()``) to hold a frame
+        across gathers."""
         n = self.g.n_local
         caller = torch.cuda.current_stream(self.device)
+        self.stream.wait_stream(caller)   # the caller's reads of the previous frame come first
         with torch.cuda.stream(self.stream):
             if n:
                 self.r.copy_accum_device(self.g.send.data_ptr(), n * self.W * 3 * 4)

@@ -410,6 +410,46 @@ def test_gather_rows_assembles_frame(mcpt_mod, world):
         r.close()
 
 
+@pytest.mark.gpu
+def test_gather_rows_then_render_again(mcpt_mod):
+    """A progressive caller: render, gather_rows, render again at once, then read the frame.
+    The shards' next renders add into their accumulators in place; they must wait for the peer
+    copies of the gather (mcpt_gather_rows orders each shard's stream after them), so the frame
+    holds exactly the first pass range (= a one-context render of it) and its pass count."""
+    W, H, S1, S2, B = 640, 360, 32, 1024, 8
+    ipv, iv = mcpt_mod.camera_canonical(W, H)
+    sc = mcpt_mod.Scene.reference(6)
+    full = mcpt_mod.Renderer(0)
+    full.upload_scene(sc)
+    full.set_target(W, H)
+    full.set_traversal(mcpt_mod.TRAVERSAL_LANE)
+    full.render(ipv, iv, 1, S1, 0.0, B, 1.0, 0)
+    ref, n_ref = full.read_accum()
+    from mcpt import dist
+    shards = []
+    for rank in range(2):
+        r = mcpt_mod.Renderer(0)
+        r.upload_scene(sc)
+        r.set_traversal(mcpt_mod.TRAVERSAL_LANE)
+        r.set_target_rows(W, H, [int(y) for y in np.nonzero(dist.balanced_owner(H, 8, 2) == rank)[0]])
+        shards.append(r)
+    frame = mcpt_mod.Renderer(0)
+    frame.set_target(W, H)
+    for r in shards:
+        r.render(ipv, iv, 1, S1, 0.0, B, 1.0, 0)
+    frame.gather_rows(shards)
+    for r in shards:   # queued right after the gather: must not reach the rows being copied
+        r.render(ipv, iv, S1 + 1, S2, 0.0, B, 1.0, 0)
+    got, n = frame.read_accum()
+    assert n == n_ref == S1
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    for r in shards:
+        _, ns = r.read_accum()
+        assert ns == S1 + S2
+    for r in shards + [frame, full]:
+        r.close()
+
+
 def test_auto_two_round_trials_settle(mcpt_mod, renderer):
     """AUTO times each applicable candidate twice (candidate order, then reverse) on launches of
     one shape and then settles (mcpt_get_schedule reports it); mcpt.AUTO_TRIALS launches are

@@ -4,12 +4,16 @@
 # The PMC records (keyed by libmcpt.so's sha256) become profiles/pmc_records.json, which
 # bench.py's roofline reads.
 set -e
-V=$1; R=${2:-r02}; O=gpurun_out/$V; P=profiles/${R}_${V}
+V=$1; R=${2:-r03}; O=gpurun_out/$V; P=profiles/${R}_${V}
 cp $O/bench.json ${P}_bench.json
 [ -f $O/bench_c4.json ] && cp $O/bench_c4.json ${P}_bench_c4.json
 [ -f $O/bench_gloo2.json ] && grep '^{' $O/bench_gloo2.json > ${P}_bench_gloo2_rehearsal.json
 [ -f $O/bench_gloo4.json ] && grep '^{' $O/bench_gloo4.json > ${P}_bench_gloo4_rehearsal.json
 [ -f $O/bench_c1.json ] && cp $O/bench_c1.json ${P}_bench_c1.json
+[ -f $O/bench_c3.json ] && cp $O/bench_c3.json ${P}_bench_c3.json
+[ -f $O/bench_c5.json ] && cp $O/bench_c5.json ${P}_bench_c5.json
+[ -f $O/bench_gloo2_c4.json ] && grep '^{' $O/bench_gloo2_c4.json > ${P}_bench_gloo2_c4_rehearsal.json
+[ -f $O/bench_nccl2_1gpu.err ] && cp $O/bench_nccl2_1gpu.err ${P}_bench_nccl2_on_1gpu_refused.txt
 cp $O/prof/run_kernel_stats.csv ${P}_kernel_stats.csv
 python tools/trace_summary.py $O/prof/run_kernel_trace.csv \
   "$R $V: rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu-baseline" > ${P}_kernel_trace_summary.txt
