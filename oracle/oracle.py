@@ -66,6 +66,7 @@ def lib() -> ctypes.CDLL:
             "orc_mesh_view_free": (None, [_vp]),
             "orc_mesh_bvh": (i, [_fp, _ip, i, _fp, _ip]),
             "orc_sample_hemisphere": (None, [_fp, _fp, f, i, i, _fp]),
+            "orc_set_deviation": (i, [i]),
         }
         for name, (res, args) in sigs.items():
             fn = getattr(L, name)
@@ -73,6 +74,25 @@ def lib() -> ctypes.CDLL:
             fn.argtypes = args
         _L = L
     return _L
+
+
+# deviations from the arithmetic contract (oracle.cpp DEV_*): measurement of what the pieces the
+# reference leaves to the GL driver / Eigen would change (tests/test_oracle_variants.py only)
+DEV_TC_UP, DEV_TC_DOWN, DEV_LIBM, DEV_DIV, DEV_INV_F32 = 1, 2, 4, 8, 16
+
+
+class deviation:
+    """``with deviation(flags): ...`` renders/builds with the given DEV_* flags, then restores."""
+
+    def __init__(self, flags: int):
+        self.flags = int(flags)
+
+    def __enter__(self):
+        self.old = lib().orc_set_deviation(self.flags)
+        return self
+
+    def __exit__(self, *exc):
+        lib().orc_set_deviation(self.old)
 
 
 def P(a: np.ndarray, t=_fp):
