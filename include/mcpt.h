@@ -50,6 +50,13 @@ enum mcpt_traversal {
                                 later launches of that shape use the fastest */
   MCPT_TRAVERSAL_LANE = 1,   /* each lane walks its own DFS (divergent, vector loads) */
   MCPT_TRAVERSAL_WAVE = 2,   /* the wave walks the union of its lanes' DFS orders (scalar loads) */
+  MCPT_TRAVERSAL_STREAM = 3, /* wavefront schedule: a pool of path slots in HBM, iterations of one
+                                trace kernel (persistent waves, a lane takes the next queued ray as
+                                soon as its walk ends) and one shade kernel.
+                                Variant montecarlo.frag, scenes without meshes, bounces > 0; other
+                                renders run the per-lane walk.  mcpt_render returns once the
+                                iterations have been issued (it waits on the device while it issues
+                                them, to know when the slots are done) */
 };
 
 /* algorithmic-byte event counters, index order */
@@ -191,6 +198,15 @@ int mcpt_get_schedule(mcpt_ctx* ctx, int* traversal, int* seg_per_item, int* set
  * results for every value; a scheduling knob.  mcpt_get_walk_exit reports the value used. */
 int mcpt_set_walk_exit(mcpt_ctx* ctx, int lanes);
 int mcpt_get_walk_exit(mcpt_ctx* ctx, int* resolved_lanes);
+
+/* Stream schedule (MCPT_TRAVERSAL_STREAM) knobs: path slots of the pool (0 = default 4 Mi;
+ * never more than the launch's (pixel, pass segment) units; 160 B of device state per slot)
+ * and the trace kernel's refill threshold (a wave takes new rays for its idle lanes once at
+ * most `refill` lanes still walk; 0 = only when all are done; -1 = default 56).  Same results
+ * for every value.  mcpt_stream_iterations: trace + shade iterations of the last stream launch
+ * (0 if it did not use the stream schedule).  No reference equivalent. */
+int mcpt_set_stream_pool(mcpt_ctx* ctx, int slots, int refill);
+int mcpt_stream_iterations(mcpt_ctx* ctx, long long* iterations);
 
 /* Per-lane walks: run the primitive-test block only once at least `lanes` lanes wait on a
  * leaf (or no lane can take a node step); others wait (0 = off: node and leaf blocks every

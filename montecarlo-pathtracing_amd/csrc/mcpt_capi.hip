@@ -77,21 +77,33 @@ struct mcpt_ctx {
   bool timed = false;
   size_t partial_budget = kDefaultPartialBudget;
   int traversal = MCPT_TRAVERSAL_AUTO;
-  // AUTO schedule: the first sizeable launches after a scene upload run each candidate once
+  // AUTO schedule: the first sizeable launches after a scene upload run each candidate twice
   // (kernel time per sample from the launch events), later launches use the fastest (results
-  // are identical either way).  Candidates: 1 = per-lane walk, 2 = wave-coherent walk, and
-  // per-lane walks with 2 (3, on launches of >= 2 pass segments) or 4 (4, >= 4 segments) pass
-  // segments per work item.
+  // are identical either way).  Candidates: 1 = per-lane walk, 2 = wave-coherent walk, 3 = the
+  // stream schedule (deep BVHs, montecarlo.frag, no meshes), and per-lane walks with 2 (4, on
+  // launches of >= 2 pass segments) or 4 (5, >= 4 segments) pass segments per work item.
   int tune_pending = 0;             // candidate of the launch whose timing is not collected yet
   double tune_samples = 0.0;        // samples of that launch
   long long tune_shape[2] = {0, 0};      // (local pixels, passes) of that launch
   long long meas_shape[2] = {0, 0};      // shape the measurements below were taken on
   int meas_segs = 0;                // pass segments of that shape (which candidates apply)
-  double tune_ns[5] = {0.0, 0.0, 0.0, 0.0, 0.0};   // best ns per sample measured, by candidate (same shape)
-  int tune_cnt[5] = {0, 0, 0, 0, 0};                // trials of each candidate so far
+  double tune_ns[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};   // best ns per sample measured, by candidate (same shape)
+  int tune_cnt[6] = {0, 0, 0, 0, 0, 0};                  // trials of each candidate so far
+  bool stream_auto = false;         // the stream candidate applies to the current launch
   int tune_choice = 0;              // resolved candidate once all are measured
   int walk_exit = -1;               // mcpt_set_walk_exit; -1: by BVH depth
   int leaf_batch = -1;              // MCPT_LEAF_BATCH env (tuning); -1: default
+  // stream schedule (MCPT_TRAVERSAL_STREAM): slot pool, ray queues, counters
+  int n_cu = 0;                     // compute units of the device (persistent grids)
+  float* d_slots = nullptr;         // SF_COUNT x slot capacity
+  int* d_queue = nullptr;           // 2 x slot capacity
+  unsigned* d_sctr = nullptr;       // SC_COUNT counters
+  int slot_cap = 0;
+  unsigned* h_cnt = nullptr;        // pinned: queue counts read back after each batch (2)
+  hipEvent_t batch_ev[2] = {nullptr, nullptr};
+  int stream_slots = 0;             // MCPT_STREAM_SLOTS env: pool size (0: default)
+  int stream_refill = -1;           // MCPT_STREAM_REFILL env: refill threshold (-1: default)
+  long long stream_iters = 0;       // iterations of the last stream render (diagnostics)
 };
 
 // events of sub-launch k: start / mid / stop
@@ -143,10 +155,14 @@ static int resolve_leaf_batch(const mcpt_ctx* c) {
   return c->depth >= 8 ? 8 : 0;
 }
 
-constexpr int kCandLaneSeg2 = 3, kCandLaneSeg4 = 4;
+constexpr int kCandStream = MCPT_TRAVERSAL_STREAM, kCandLaneSeg2 = 4, kCandLaneSeg4 = 5;
+// BVH depth from which AUTO also times the stream schedule (its pool and two launches per
+// iteration only pay where walks are long)
+constexpr int kStreamAutoDepth = 8;
 // the candidates that apply to a launch of `segs` pass segments
-static bool cand_applies(int cand, long long segs) {
-  return cand <= 2 || (cand == kCandLaneSeg2 && segs >= 2) || (cand == kCandLaneSeg4 && segs >= 4);
+static bool cand_applies(const mcpt_ctx* c, int cand, long long segs) {
+  return cand <= 2 || (cand == kCandStream && c->stream_auto) || (cand == kCandLaneSeg2 && segs >= 2) ||
+         (cand == kCandLaneSeg4 && segs >= 4);
 }
 static int cand_seg_per_item(int cand) { return cand == kCandLaneSeg2 ? 2 : cand == kCandLaneSeg4 ? 4 : 1; }
 
@@ -164,18 +180,16 @@ static int resolve_candidate(const mcpt_ctx* c, long long segs) {
   // first candidate of the round's order not yet timed that often on the measured shape
   int round = kTuneRounds;
   for (int k = 1; k <= kCandLaneSeg4; ++k)
-    if (cand_applies(k, segs)) round = std::min(round, c->tune_cnt[k]);
+    if (cand_applies(c, k, segs)) round = std::min(round, c->tune_cnt[k]);
   if (round >= kTuneRounds) return MCPT_TRAVERSAL_LANE;
   for (int i = 0; i < kCandLaneSeg4; ++i) {
     const int k = (round % 2 == 0) ? 1 + i : kCandLaneSeg4 - i;
-    if (cand_applies(k, segs) && c->tune_cnt[k] == round) return k;
+    if (cand_applies(c, k, segs) && c->tune_cnt[k] == round) return k;
   }
   return MCPT_TRAVERSAL_LANE;
 }
-static int resolve_traversal(const mcpt_ctx* c) {
-  const int cand = resolve_candidate(c, c->meas_segs);
-  return cand >= kCandLaneSeg2 ? MCPT_TRAVERSAL_LANE : cand;
-}
+static int cand_traversal(int cand) { return cand >= kCandLaneSeg2 ? MCPT_TRAVERSAL_LANE : cand; }
+static int resolve_traversal(const mcpt_ctx* c) { return cand_traversal(resolve_candidate(c, c->meas_segs)); }
 
 static void reset_tuning(mcpt_ctx* c) {
   c->tune_pending = 0;
@@ -210,7 +224,7 @@ static hipError_t collect_tuning(mcpt_ctx* c) {
   bool all = true;
   int best = MCPT_TRAVERSAL_LANE;
   for (int k = 1; k <= kCandLaneSeg4; ++k) {
-    if (!cand_applies(k, c->meas_segs)) continue;
+    if (!cand_applies(c, k, c->meas_segs)) continue;
     if (c->tune_cnt[k] < kTuneRounds) all = false;
     else if (t[k] < t[best]) best = k;
   }
@@ -246,7 +260,12 @@ int mcpt_create(int device_ordinal, mcpt_ctx** out) {
   mcpt_ctx* c = new (std::nothrow) mcpt_ctx();
   if (!c) return MCPT_ERR_INVALID_ARG;
   c->leaf_batch = env_int("MCPT_LEAF_BATCH", -1);   // tuning hook (same results for any value)
+  c->stream_slots = env_int("MCPT_STREAM_SLOTS", 0);
+  c->stream_refill = env_int("MCPT_STREAM_REFILL", -1);
   c->device = device_ordinal;
+  if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device_ordinal) != hipSuccess ||
+      c->n_cu <= 0)
+    c->n_cu = 256;
   hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = ensure_events(c, 1);
   if (const char* pb = std::getenv("MCPT_PARTIAL_BYTES")) c->partial_budget = (size_t)std::strtoull(pb, nullptr, 10);
@@ -282,6 +301,11 @@ int mcpt_destroy(mcpt_ctx* c) {
   (void)hipFree(c->d_rows);
   (void)hipFree(c->d_events);
   (void)hipFree(c->d_partial);
+  (void)hipFree(c->d_slots);
+  (void)hipFree(c->d_queue);
+  (void)hipFree(c->d_sctr);
+  if (c->h_cnt) (void)hipHostFree(c->h_cnt);
+  for (hipEvent_t e : c->batch_ev) if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->evs) (void)hipEventDestroy(e);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
@@ -562,6 +586,78 @@ static void corner_rays(const float* invPV, const float* invV, mcpt::RenderParam
   }
 }
 
+// stream schedule defaults: 4 M path slots (160 B of state each: 640 MB) keep every trace
+// kernel of an iteration long against its tail (the last walks of the iteration); a wave refills
+// its lanes once 8 of them have finished their walks
+constexpr int kStreamSlotsDefault = 1 << 22;
+constexpr int kStreamRefillDefault = 56;
+constexpr int kStreamBatch = 8;   // iterations issued between two checks of the queue count
+
+static bool stream_applies(const mcpt_ctx* c, int variant, int bounces, bool count) {
+  return !count && variant == 0 && bounces > 0 && c->n_meshes == 0;
+}
+
+// One sub-launch (one pass range of <= max_seg segments) with the stream schedule: slots set up,
+// then iterations (trace + shade) in batches until the ray queue is empty.  The host reads the
+// queue count of batch b-1 while batch b runs, so the device never waits for the host.
+static int stream_run(mcpt_ctx* c, const mcpt::RenderParams& p) {
+  const unsigned long long n_units = (unsigned long long)p.n_local_px * (unsigned long long)p.n_segments;
+  if (n_units == 0) return MCPT_OK;
+  if (n_units >= (1ULL << 31) || p.n_local_px >= (1LL << 31))
+    return set_err(MCPT_ERR_INVALID_ARG, "stream schedule: too many units in one launch");
+  // the kernels address the pool through one buffer resource: below 2 GiB
+  const int max_slots = (int)(((1ULL << 31) - 1) / (mcpt::SF_COUNT * sizeof(float)));
+  const int want = std::min(c->stream_slots > 0 ? c->stream_slots : kStreamSlotsDefault, max_slots);
+  const int n_slots = (int)std::min<unsigned long long>(n_units, (unsigned long long)want);
+  if (n_slots > c->slot_cap) {
+    HIP_OR_RETURN(hipStreamSynchronize(c->stream));
+    (void)hipFree(c->d_slots); (void)hipFree(c->d_queue);
+    c->d_slots = nullptr; c->d_queue = nullptr; c->slot_cap = 0;
+    HIP_OR_RETURN(hipMalloc(&c->d_slots, (size_t)mcpt::SF_COUNT * n_slots * sizeof(float)));
+    HIP_OR_RETURN(hipMalloc(&c->d_queue, (size_t)2 * n_slots * sizeof(int)));
+    c->slot_cap = n_slots;
+  }
+  if (!c->d_sctr) HIP_OR_RETURN(hipMalloc(&c->d_sctr, mcpt::SC_COUNT * sizeof(unsigned)));
+  if (!c->h_cnt) HIP_OR_RETURN(hipHostMalloc(&c->h_cnt, 2 * sizeof(unsigned), hipHostMallocDefault));
+  for (hipEvent_t& e : c->batch_ev)
+    if (!e) HIP_OR_RETURN(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  mcpt::StreamParams q;
+  q.r = p;
+  q.st = c->d_slots;
+  // slot field f of slot i at st[f * n_slots + i]: the pool is laid out for this launch's slot count
+  q.queue[0] = c->d_queue;
+  q.queue[1] = c->d_queue + n_slots;
+  q.ctr = c->d_sctr;
+  q.n_slots = n_slots;
+  q.n_units = (unsigned)n_units;
+  q.parity = 0;
+  q.refill = c->stream_refill >= 0 ? c->stream_refill : kStreamRefillDefault;
+  HIP_OR_RETURN(mcpt_launch_stream_init(q, c->stream));
+  // every iteration advances each live slot by one traversal; a unit needs at most
+  // (passes) x (2 B + 1) + 1 of them, and a slot runs ceil(units / slots) units
+  const long long per_unit = (long long)mcpt::kPassChunk * (2LL * p.bounces + 1) + 1;
+  const long long cap = ((long long)((n_units + n_slots - 1) / n_slots) + 1) * per_unit + 2 * kStreamBatch;
+  const int blocks = c->n_cu * 8;   // persistent waves: 8 workgroups of 4 waves per CU
+  long long it = 0;
+  for (int b = 0;; ++b) {
+    for (int k = 0; k < kStreamBatch; ++k, ++it) {
+      q.parity = (int)(it & 1);
+      HIP_OR_RETURN(mcpt_launch_stream_iter(q, blocks, c->stream));
+    }
+    // queue count the next iteration will read
+    HIP_OR_RETURN(hipMemcpyAsync(c->h_cnt + (b & 1), c->d_sctr + mcpt::SC_CNT + (it & 1), sizeof(unsigned),
+                                 hipMemcpyDeviceToHost, c->stream));
+    HIP_OR_RETURN(hipEventRecord(c->batch_ev[b & 1], c->stream));
+    if (b >= 1) {
+      HIP_OR_RETURN(hipEventSynchronize(c->batch_ev[(b - 1) & 1]));
+      if (c->h_cnt[(b - 1) & 1] == 0u) break;   // batch b found nothing to do
+    }
+    if (it > cap) return set_err(MCPT_ERR_HIP, "stream schedule did not drain its queue");
+  }
+  c->stream_iters += it;
+  return MCPT_OK;
+}
+
 static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_pass, int n_passes, float date,
                   int bounces, float refract_ind, int variant, bool count, unsigned long long* events) {
   if (!c || !invPV || !invV || n_passes < 0 || variant < 0 || variant > 2)
@@ -599,9 +695,12 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   // segment groups need segments to group; whether longer items pay (the lanes' pass-count
   // tails average out) or cost (longer grid tail) depends on the scene and the launch: timed,
   // not guessed (profiles/r01_ab44_seg_per_item.jsonl, r01_ab49_seg_groups_tail.jsonl)
+  c->stream_auto = stream_applies(c, variant, bounces, false) && c->depth >= kStreamAutoDepth;
   const int cand = count ? (c->traversal == MCPT_TRAVERSAL_AUTO ? MCPT_TRAVERSAL_LANE : c->traversal)
                          : resolve_candidate(c, total_seg);
-  const int mode = cand >= kCandLaneSeg2 ? MCPT_TRAVERSAL_LANE : cand;
+  const bool stream = cand == kCandStream && stream_applies(c, variant, bounces, count);
+  c->stream_iters = 0;
+  const int mode = (cand >= kCandLaneSeg2 || cand == kCandStream) ? MCPT_TRAVERSAL_LANE : cand;
   p.wave_traversal = (mode == MCPT_TRAVERSAL_WAVE) ? 1 : 0;
   p.walk_exit = resolve_walk_exit(c);
   p.leaf_batch = resolve_leaf_batch(c);
@@ -668,7 +767,12 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
     p.n_passes = (int)(hi - lo);
     p.n_segments = fdiv((int)(hi - 2), mcpt::kPassChunk) - (int)c0 + 1;
     HIP_OR_RETURN(hipEventRecord(ev_start(c, (int)k), c->stream));
-    HIP_OR_RETURN(mcpt_launch_render(p, count, c->stream));
+    if (stream) {
+      const int st = stream_run(c, p);
+      if (st != MCPT_OK) return st;
+    } else {
+      HIP_OR_RETURN(mcpt_launch_render(p, count, c->stream));
+    }
     HIP_OR_RETURN(hipEventRecord(ev_mid(c, (int)k), c->stream));
     HIP_OR_RETURN(mcpt_launch_combine(p, c->stream));
     HIP_OR_RETURN(hipEventRecord(ev_stop(c, (int)k), c->stream));
@@ -868,7 +972,7 @@ int mcpt_sample_hemisphere(mcpt_ctx* c, const float* normal3, const float* fseed
 }
 
 int mcpt_set_traversal(mcpt_ctx* c, int mode) {
-  if (!c || mode < MCPT_TRAVERSAL_AUTO || mode > MCPT_TRAVERSAL_WAVE)
+  if (!c || mode < MCPT_TRAVERSAL_AUTO || mode > MCPT_TRAVERSAL_STREAM)
     return set_err(MCPT_ERR_INVALID_ARG, "mcpt_set_traversal: bad mode");
   c->traversal = mode;
   reset_tuning(c);
@@ -878,6 +982,19 @@ int mcpt_set_traversal(mcpt_ctx* c, int mode) {
 int mcpt_set_walk_exit(mcpt_ctx* c, int lanes) {
   if (!c || lanes < -1 || lanes > 64) return set_err(MCPT_ERR_INVALID_ARG, "mcpt_set_walk_exit: bad lane count");
   c->walk_exit = lanes;
+  return MCPT_OK;
+}
+
+int mcpt_set_stream_pool(mcpt_ctx* c, int slots, int refill) {
+  if (!c || slots < 0 || refill < -1 || refill > 64) return set_err(MCPT_ERR_INVALID_ARG, "mcpt_set_stream_pool: bad arguments");
+  c->stream_slots = slots;
+  c->stream_refill = refill;
+  return MCPT_OK;
+}
+
+int mcpt_stream_iterations(mcpt_ctx* c, long long* iterations) {
+  if (!c || !iterations) return MCPT_ERR_INVALID_ARG;
+  *iterations = c->stream_iters;
   return MCPT_OK;
 }
 
@@ -920,7 +1037,7 @@ int mcpt_get_traversal(mcpt_ctx* c, int* resolved) {
 int mcpt_get_schedule(mcpt_ctx* c, int* traversal, int* seg_per_item, int* settled) {
   if (!c) return MCPT_ERR_INVALID_ARG;
   const int cand = resolve_candidate(c, c->meas_segs);
-  if (traversal) *traversal = cand >= kCandLaneSeg2 ? MCPT_TRAVERSAL_LANE : cand;
+  if (traversal) *traversal = cand_traversal(cand);
   const int env_seg = env_int("MCPT_SEG_PER_ITEM", 0);
   if (seg_per_item) *seg_per_item = env_seg > 0 ? env_seg : cand_seg_per_item(cand);
   if (settled) *settled = (c->traversal != MCPT_TRAVERSAL_AUTO || c->tune_choice != 0) ? 1 : 0;

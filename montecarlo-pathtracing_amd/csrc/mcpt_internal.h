@@ -89,6 +89,34 @@ struct RenderParams {
   double cull2_max;
 };
 
+// Stream schedule (MCPT_TRAVERSAL_STREAM): wavefront path tracing in two
+// kernels per iteration over a pool of path slots.  Slot state is SoA, field f of slot i at
+// st[f * n_slots + i].
+enum StreamField {
+  SF_OX, SF_OY, SF_OZ, SF_DX, SF_DY, SF_DZ,   // the ray the next traversal walks
+  SF_AX, SF_AY, SF_AZ, SF_TX, SF_TY, SF_TZ,   // att, total
+  SF_RX, SF_RY, SF_RZ,                        // RNG state (u32 bits)
+  SF_STATE,                                   // bounce | phase << 8 (u32 bits)
+  SF_PASS, SF_UNIT,                           // current pass, unit = segment * n_local_px + px
+  SF_SX, SF_SY, SF_SZ,                        // the unit's sum (passes in order, from 0)
+  SF_N0X, SF_N0Y, SF_N0Z, SF_P0X, SF_P0Y, SF_P0Z, SF_KEY0,   // the unit's cached primary hit
+  SF_NSX, SF_NSY, SF_NSZ, SF_PSX, SF_PSY, SF_PSZ,            // N, P kept across an inner walk
+  SF_HX, SF_HY, SF_HZ, SF_HDIST, SF_HCODE,    // the traversal's hit record (pl, dist, code)
+  SF_COUNT
+};
+// ctr[]: queue counts [0..1], trace-kernel fetch counters [2..3], next unit [4]
+enum { SC_CNT = 0, SC_FETCH = 2, SC_UNIT = 4, SC_COUNT = 8 };
+struct StreamParams {
+  RenderParams r;               // scene, target, the sub-launch's pass range and constants
+  float* st;                    // SF_COUNT x n_slots
+  int* queue[2];                // slots whose ray waits for a traversal (ping-pong by parity)
+  unsigned* ctr;                // SC_* counters
+  int n_slots;
+  unsigned n_units;             // n_segments x n_local_px
+  int parity;                   // iteration & 1: queue[parity] is this iteration's input
+  int refill;                   // trace kernel: refill a wave's idle lanes once <= this many still walk
+};
+
 // ray-query batch (mcpt_trace): per ray 3 ints (shape, prim, dir) and kTraceFloats floats
 // (dist, pl.xyz, pg.xyz, N.xyz, P.xyz, colour rgba, material rgba) — the mcpt_hit layout
 constexpr int kTraceFloats = 21;
@@ -128,3 +156,7 @@ hipError_t mcpt_launch_trace(const mcpt::TraceParams& q, bool any_hit, hipStream
 hipError_t mcpt_launch_sample(const mcpt::SampleParams& q, hipStream_t stream);
 hipError_t mcpt_launch_render(const mcpt::RenderParams& p, bool count, hipStream_t stream);
 hipError_t mcpt_launch_combine(const mcpt::RenderParams& p, hipStream_t stream);
+// stream schedule: slot set-up (queue[0] = every slot with a unit), then one iteration = the
+// trace kernel over queue[parity] + the shade kernel appending to queue[parity ^ 1]
+hipError_t mcpt_launch_stream_init(const mcpt::StreamParams& q, hipStream_t stream);
+hipError_t mcpt_launch_stream_iter(const mcpt::StreamParams& q, int persistent_blocks, hipStream_t stream);

@@ -969,6 +969,22 @@ __device__ __forceinline__ void rr_jobs(bool need1, bool need2, const Rng& rng, 
 // ------------------------------------------------------------------------------------
 __device__ __forceinline__ int floordiv(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
 
+// raytracer.vert:9-22: the camera ray of screen position (u, v) — the 4 corner rays
+// interpolated over the strip triangles (v0,v1,v2) / (v1,v3,v2), normalized
+__device__ __forceinline__ f3 camera_dir(const RenderParams& p, float u, float v) {
+  const f3 d0 = mk(p.cd[0], p.cd[1], p.cd[2]), d1 = mk(p.cd[3], p.cd[4], p.cd[5]);
+  const f3 d2 = mk(p.cd[6], p.cd[7], p.cd[8]), d3 = mk(p.cd[9], p.cd[10], p.cd[11]);
+  f3 dir;
+  if (u + v <= 1.0f) {
+    float w0 = (1.0f - u) - v;
+    dir = add(add(muls(d0, w0), muls(d1, u)), muls(d2, v));
+  } else {
+    float w1 = 1.0f - v, w3 = (u + v) - 1.0f, w2 = 1.0f - u;
+    dir = add(add(muls(d1, w1), muls(d3, w3)), muls(d2, w2));
+  }
+  return normalize3(dir);
+}
+
 // Work item = (32x8 pixel tile of four 8x8 waves, group of seg_per_item pass segments).  A
 // segment is the part of the launch's pass range inside one accumulation chunk of kPassChunk
 // absolute passes: segments of one pixel are independent (strong-scaling
@@ -1049,21 +1065,8 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
   ev.init();
   if (!live) return;
 
-  // raytracer.vert:9-22 corner rays, interpolated over the strip (v0,v1,v2) / (v1,v3,v2)
   const float u = ((float)x + 0.5f) / (float)p.W;
   const float v = ((float)y + 0.5f) / (float)p.H;
-  f3 dir;
-  {
-    const f3 d0 = mk(p.cd[0], p.cd[1], p.cd[2]), d1 = mk(p.cd[3], p.cd[4], p.cd[5]);
-    const f3 d2 = mk(p.cd[6], p.cd[7], p.cd[8]), d3 = mk(p.cd[9], p.cd[10], p.cd[11]);
-    if (u + v <= 1.0f) {
-      float w0 = (1.0f - u) - v;
-      dir = add(add(muls(d0, w0), muls(d1, u)), muls(d2, v));
-    } else {
-      float w1 = 1.0f - v, w3 = (u + v) - 1.0f, w2 = 1.0f - u;
-      dir = add(add(muls(d1, w1), muls(d3, w3)), muls(d2, w2));
-    }
-  }
   // Per-pixel constants live in LDS (SoA by thread: conflict-free), not in VGPRs: the
   // camera direction and the cached primary hit are read once per pass, and keeping them
   // out of the register file is what lets 7 waves/SIMD fit.  rows: 0-2 Dcam, 3-5 N0, 6-8 P0
@@ -1078,7 +1081,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
 #if MCPT_RR_COMPACT
   __shared__ unsigned char s_own[kTileThreads / 64][128], s_wl[kTileThreads / 64][64];   // rr_jobs
 #endif
-  const f3 Dcam0 = normalize3(dir);
+  const f3 Dcam0 = camera_dir(p, u, v);
   s_pix[0][pslot] = Dcam0.x; s_pix[1][pslot] = Dcam0.y; s_pix[2][pslot] = Dcam0.z;
   s_pix[12][tid] = 0.0f; s_pix[13][tid] = 0.0f; s_pix[14][tid] = 0.0f;   // this segment's sum
 #if MCPT_UNIT_POOL
@@ -1510,6 +1513,353 @@ __global__ __launch_bounds__(256) void combine_kernel(float* __restrict__ accum,
 }
 
 // ------------------------------------------------------------------------------------
+// stream schedule (MCPT_TRAVERSAL_STREAM): wavefront path tracing for deep
+// BVHs.  A pool of path slots (SoA in HBM, StreamField) each runs one (pixel, pass segment)
+// unit at a time, its passes in order (the unit's sum is the megakernel's segment sum, so the
+// bits are the same); an iteration is
+//   stream_trace_kernel: persistent waves walk the queued slots' rays, a lane taking the next
+//     queued ray as soon as its walk ends (no lane waits for the wave's longest walk);
+//   stream_shade_kernel: one lane per queued slot shades the hit (tp/montecarlo.frag:100-179),
+//     ends passes / units, takes new units, and queues the slot's next ray.
+// Each slot's sequence of operations is the megakernel's (same traversal, same shading, same
+// RNG draws, same sums), only the interleaving across slots changes.
+// ------------------------------------------------------------------------------------
+constexpr uint32_t kPhaseInner = 1, kPhasePrimary = 2, kSlotDead = 0xFFFFFFFFu;
+#ifndef MCPT_MIN_WAVES_STREAM
+#define MCPT_MIN_WAVES_STREAM 8
+#endif
+// the shade kernel streams slot state from HBM: occupancy over registers
+#ifndef MCPT_MIN_WAVES_SHADE
+#define MCPT_MIN_WAVES_SHADE 5
+#endif
+
+// Slot i's fields through a buffer resource over the pool: the field's column offset is a
+// wave-uniform scalar (soffset) and the lane's offset one 32-bit VGPR shared by every field, so
+// no 64-bit per-lane address is formed or kept per field (with plain pointers the compiler
+// strength-reduced the field columns into ~40 live 64-bit addresses and spilled them).
+// Pools are < 2 GiB (host check).  0x00020000: the gfx9 raw-buffer descriptor word 3.
+struct SlotRef {
+  __amdgpu_buffer_rsrc_t rs;
+  uint32_t col_bytes;   // n_slots * 4: one field column
+  uint32_t off;         // slot * 4
+  __device__ __forceinline__ uint32_t ldu(int f) const {
+    return __builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, (int)((uint32_t)f * col_bytes), 0);
+  }
+  __device__ __forceinline__ float ld(int f) const { return __uint_as_float(ldu(f)); }
+  __device__ __forceinline__ void setu(int f, uint32_t v) const {
+    __builtin_amdgcn_raw_buffer_store_b32(v, rs, (int)off, (int)((uint32_t)f * col_bytes), 0);
+  }
+  __device__ __forceinline__ void set(int f, float v) const { setu(f, __float_as_uint(v)); }
+  __device__ __forceinline__ f3 ld3(int f) const { return mk(ld(f), ld(f + 1), ld(f + 2)); }
+  __device__ __forceinline__ void set3(int f, f3 v) const { set(f, v.x); set(f + 1, v.y); set(f + 2, v.z); }
+};
+__device__ __forceinline__ SlotRef slot_ref(const StreamParams& q, uint32_t i) {
+  SlotRef r;
+  r.col_bytes = (uint32_t)q.n_slots * 4u;
+  r.rs = __builtin_amdgcn_make_buffer_rsrc(q.st, 0, (int)((uint32_t)SF_COUNT * r.col_bytes), 0x00020000);
+  r.off = i * 4u;
+  return r;
+}
+
+// a unit = (pass segment, local pixel): its pixel and its pass range in this launch
+struct UnitGeom { int x, y, px, seg, pass_begin, pass_end; };
+__device__ __forceinline__ UnitGeom unit_geom(const RenderParams& p, uint32_t unit) {
+  UnitGeom g;
+  const uint32_t npx = (uint32_t)p.n_local_px;
+  g.seg = (int)(unit / npx);
+  g.px = (int)(unit - (uint32_t)g.seg * npx);
+  const int lr = g.px / p.W;
+  g.x = g.px - lr * p.W;
+  g.y = p.rows[lr];
+  const int c = floordiv(p.first_pass - 1, kPassChunk) + g.seg;
+  g.pass_begin = max(p.first_pass, c * kPassChunk + 1);
+  g.pass_end = min(p.first_pass + p.n_passes, (c + 1) * kPassChunk + 1);
+  return g;
+}
+
+// a slot starts `unit`: its camera ray is queued for the primary traversal
+__device__ __forceinline__ void stream_start_unit(const RenderParams& p, const SlotRef& sl, uint32_t unit) {
+  const UnitGeom g = unit_geom(p, unit);
+  const f3 D = camera_dir(p, ((float)g.x + 0.5f) / (float)p.W, ((float)g.y + 0.5f) / (float)p.H);
+  sl.set3(SF_OX, mk(p.ox, p.oy, p.oz));
+  sl.set3(SF_DX, D);
+  sl.setu(SF_STATE, kPhasePrimary << 8);
+  sl.setu(SF_PASS, (uint32_t)g.pass_begin);
+  sl.setu(SF_UNIT, unit);
+  sl.set3(SF_SX, mk(0.0f, 0.0f, 0.0f));
+}
+
+__global__ __launch_bounds__(256) void stream_init_kernel(StreamParams q) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i == 0) {
+    const unsigned n0 = (unsigned)q.n_slots < q.n_units ? (unsigned)q.n_slots : q.n_units;
+    q.ctr[SC_CNT] = n0;
+    q.ctr[SC_CNT + 1] = 0u;
+    q.ctr[SC_FETCH] = 0u;
+    q.ctr[SC_FETCH + 1] = 0u;
+    q.ctr[SC_UNIT] = n0;
+  }
+  if (i >= q.n_slots) return;
+  const SlotRef sl = slot_ref(q, (uint32_t)i);
+  if ((unsigned)i < q.n_units) {
+    stream_start_unit(q.r, sl, (uint32_t)i);
+    q.queue[0][i] = i;
+  } else {
+    sl.setu(SF_STATE, kSlotDead);
+  }
+}
+
+// The traversal half of an iteration: every queued slot's ray walked with the per-lane DFS of
+// walk_run (right child first, cull at push time, batched leaf visits) and its hit record
+// stored.  Persistent waves; a lane whose walk ended takes the next queued ray when the wave
+// leaves walk_run (at <= q.refill walking lanes), through one atomic per wave.
+__global__ __launch_bounds__(256, MCPT_MIN_WAVES_STREAM) void stream_trace_kernel(StreamParams q) {
+  const RenderParams& p = q.r;
+  const SceneT<false, false> s{p.nodes, p.leaves, p.ptype, p.prims, p.depth, p.minfo, p.mnodes, p.mleaves,
+                               p.mtris, p.mverts, p.mnorms, p.flat_face};
+  const int par = q.parity;
+  const unsigned n = q.ctr[SC_CNT + par];
+  if (blockIdx.x == 0 && threadIdx.x == 0) q.ctr[SC_CNT + (par ^ 1)] = 0u;   // the shade kernel's output count
+  const int* in = q.queue[par];
+  unsigned* fetch = q.ctr + SC_FETCH + par;
+  const int lane = threadIdx.x & 63;
+  Ev<false> ev;
+  ev.init();
+  int r = -1;
+  bool more = true;
+  f3 O = mk(0.0f, 0.0f, 0.0f), D = O;
+  Hit h;
+  h.pl = O; h.dist = kFLTMAX; h.clear(); h.tri = 0; h.cull2 = 0.0;
+  Walk w;
+  w.invD = O; w.node = 0; w.level = 0; w.pending = 0;
+  for (;;) {
+    const bool need = r < 0 && more;
+    const uint64_t m = __ballot(need);
+    if (m) {
+      const int leader = __builtin_ffsll((long long)m) - 1;
+      unsigned b = 0;
+      if (lane == leader) b = atomicAdd(fetch, (unsigned)__builtin_popcountll(m));
+      b = (unsigned)__shfl((int)b, leader);
+      if (need) {
+        const unsigned idx = b + (unsigned)mbcnt64(m);
+        if (idx < n) {
+          r = in[idx];
+          const SlotRef sl = slot_ref(q, (uint32_t)r);
+          O = sl.ld3(SF_OX);
+          D = sl.ld3(SF_DX);
+          walk_begin<false>(s, D, h, w, ev, p.cull2_max);
+        } else {
+          more = false;
+        }
+      }
+    }
+    if (__ballot(r >= 0) == 0) break;
+    if (r >= 0) {
+      if (walk_run<false, true>(s, O, D, h, w, ev, q.refill, p.leaf_batch)) {
+        const SlotRef sl = slot_ref(q, (uint32_t)r);
+        sl.set3(SF_HX, h.pl);
+        sl.setu(SF_HCODE, (uint32_t)h.code);
+        r = -1;
+      }
+    }
+  }
+}
+
+// The shading half: slot i's hit through tp/montecarlo.frag:100-179 (the megakernel's shading
+// block, variant montecarlo.frag).  A path that ends adds its result to the unit's sum in pass
+// order and the slot goes on with the unit's next pass, whose camera ray is the cached primary
+// hit (shaded at once, no traversal); a unit that ends writes its sum and the slot takes the
+// next unit.  Returns true when the slot's next ray must be traversed.
+__device__ __forceinline__ bool stream_shade(const StreamParams& q, int i) {
+  const RenderParams& p = q.r;
+  const SceneT<false, false> s{p.nodes, p.leaves, p.ptype, p.prims, p.depth, p.minfo, p.mnodes, p.mleaves,
+                               p.mtris, p.mverts, p.mnorms, p.flat_face};
+  Ev<false> ev;
+  ev.init();
+  const SlotRef sl = slot_ref(q, (uint32_t)i);
+  uint32_t unit = sl.ldu(SF_UNIT);
+  UnitGeom g = unit_geom(p, unit);
+  const uint32_t sw = sl.ldu(SF_STATE);
+  int bounce = (int)(sw & 255u);
+  uint32_t phase = sw >> 8;
+  int pass = (int)sl.ldu(SF_PASS);
+  const int B = p.bounces;
+  const f3 Ocam = mk(p.ox, p.oy, p.oz);
+  Hit h;
+  h.pl = sl.ld3(SF_HX); h.code = (int)sl.ldu(SF_HCODE); h.dist = 0.0f; h.tri = 0; h.cull2 = 0.0;
+  f3 O, D, att, total, N = mk(0.0f, 0.0f, 0.0f), P = N;
+  Rng rng;
+  bool first = false;
+  f3 sum = sl.ld3(SF_SX);
+  if (phase == kPhasePrimary) {
+    // the unit's camera-ray hit, computed once and reused by all its passes (exact: the camera
+    // ray has no jitter and traversal / intersection_info draw no random numbers)
+    const int key0 = hit_key(h);
+    f3 N0 = mk(0.0f, 0.0f, 0.0f), P0 = N0;
+    if (h.hit()) geom_info<false>(s, h, N0, P0, ev);
+    sl.set3(SF_N0X, N0); sl.set3(SF_P0X, P0); sl.setu(SF_KEY0, (uint32_t)key0);
+    phase = 0;
+    first = true;
+    N = N0; P = P0;
+    h.code = key0;
+  } else {
+    O = sl.ld3(SF_OX); D = sl.ld3(SF_DX);
+    att = sl.ld3(SF_AX); total = sl.ld3(SF_TX);
+    rng.x = sl.ldu(SF_RX); rng.y = sl.ldu(SF_RY); rng.z = sl.ldu(SF_RZ);
+  }
+  float u = ((float)g.x + 0.5f) / (float)p.W, v = ((float)g.y + 0.5f) / (float)p.H;
+  if (first) {   // pass `pass` of the unit starts
+    rng = seed_for(u, v, pass, p.date);
+    O = Ocam; D = camera_dir(p, u, v);
+    att = mk(0.8f, 0.8f, 0.8f); total = mk(0.0f, 0.0f, 0.0f);
+    bounce = 0;
+  }
+  for (;;) {
+    bool done = false;
+    f3 res = mk(0.0f, 0.0f, 0.0f);
+    if (phase == 0) {
+      if (!h.hit()) {
+        const float a = gmax(0.0f, D.z);
+        res = add(total, mulv(att, gmix3(mk(0.5f, 0.5f, 0.9f), mk(1.0f, 1.0f, 0.8f), a)));
+        done = true;
+      } else {
+        if (!first) geom_info<false>(s, h, N, P, ev);
+        const float4 c4 = s.prims[(size_t)h.index() * 8 + 6];
+        const float4 m4 = s.prims[(size_t)h.index() * 8 + 7];
+        if (!(m4.z <= 0.5f)) {   // emissive: the path ends with its emission (no draw, no ray)
+          res = add(total, add(muls(mk(c4.x, c4.y, c4.z), 0.1f), muls(muls(muls(att, m4.z), 1.0f - m4.x), c4.w)));
+          done = true;
+        } else if (bounce >= B - 1) {   // every branch reaches the budget: black (MCPT_FOLD_END)
+          done = true;
+        } else {
+          f3 ray = random_ray(rng, N, 1.0f - m4.y);
+          const f3 col = mk(c4.x, c4.y, c4.z);
+          const float alpha = c4.w;
+          const float rs = schlick(p.schlick_r0, D, N);
+          const f3 R = greflect(neg(ray), N);
+          const f3 E = normalize3(sub(O, P));
+          const float se = gmix(100.0f, 2.0f, m4.y);
+          const float spec = mc_pow_le1(gmax(0.0f, dot3(E, R)), se);
+          total = add(total, add(muls(col, 0.1f), muls(muls(muls(att, m4.z), 1.0f - m4.x), alpha)));
+          const f3 mx = gmix3(att, col, m4.x);
+          const f3 base = mulv(col, att);
+          bool reflect_push = false, inner = false;
+          if (m4.x > 0.0f && alpha == 1.0f) {
+            reflect_push = true;
+          } else if (alpha < 1.0f && m4.x == 0.0f) {
+            inner = true;
+            att = add(base, mulv(muls(muls(muls(att, 1.0f - alpha), 1.0f - rs), spec), mx));
+            O = sub(P, muls(N, kBIAS));
+            D = grefract(D, N, p.ior);
+          } else if (alpha < 1.0f && m4.x > 0.0f) {
+            const float rc = rnd(rng);
+            if (rc > 0.5f) {
+              reflect_push = true;
+            } else {
+              inner = true;
+              att = add(base, mulv(muls(muls(muls(att, 1.0f - alpha), 1.0f - rs), spec), mx));
+              O = sub(P, muls(N, kBIAS));
+            }
+          } else {   // diffuse
+            att = add(base, mulv(muls(att, spec), mx));
+            O = add(P, muls(N, kBIAS));
+            D = ray;
+            bounce++;
+          }
+          if (reflect_push) {
+            const f3 na = add(base, mulv(muls(muls(muls(att, alpha), rs), spec), mx));
+            const f3 rd = random_ray(rng, greflect(D, N), 1.0f - m4.x * m4.y);
+            att = na;
+            O = add(P, muls(N, kBIAS));
+            D = rd;
+            bounce++;
+          }
+          if (inner) {   // intersection_info leaves N, P untouched on a miss: kept for the inner hit
+            phase = kPhaseInner;
+            sl.set3(SF_NSX, N); sl.set3(SF_PSX, P);
+          }
+        }
+      }
+    } else {
+      // inner traversal of the refraction branches (montecarlo.frag:148-152 / 162-165)
+      if (h.hit()) {
+        geom_info<false>(s, h, N, P, ev);
+      } else {
+        N = sl.ld3(SF_NSX); P = sl.ld3(SF_PSX);
+      }
+      O = add(P, muls(N, kBIAS));
+      D = grefract(D, neg(N), p.inv_ior);
+      phase = 0;
+      bounce++;
+      if (bounce >= B) done = true;   // budget exhausted: black
+    }
+    if (!done) {   // the path goes on: its next ray is queued
+      sl.set3(SF_OX, O); sl.set3(SF_DX, D); sl.set3(SF_AX, att); sl.set3(SF_TX, total);
+      sl.setu(SF_RX, rng.x); sl.setu(SF_RY, rng.y); sl.setu(SF_RZ, rng.z);
+      sl.setu(SF_STATE, (uint32_t)bounce | (phase << 8));
+      sl.setu(SF_PASS, (uint32_t)pass);
+      sl.set3(SF_SX, sum);
+      return true;
+    }
+    sum = mk(sum.x + res.x, sum.y + res.y, sum.z + res.z);
+    pass++;
+    if (pass >= g.pass_end) {   // the unit's sum: accumulator (one-segment launch) or its segment slot
+      if (p.n_segments == 1) {
+        float* accp = p.accum + (size_t)g.px * 3;
+        accp[0] = accp[0] + sum.x; accp[1] = accp[1] + sum.y; accp[2] = accp[2] + sum.z;
+      } else {
+        float* part = p.partial + ((size_t)g.seg * p.n_local_px + g.px) * 3;
+        part[0] = sum.x; part[1] = sum.y; part[2] = sum.z;
+      }
+      unit = atomicAdd(q.ctr + SC_UNIT, 1u);
+      if (unit >= q.n_units) {
+        sl.setu(SF_STATE, kSlotDead);
+        return false;
+      }
+      stream_start_unit(p, sl, unit);
+      return true;
+    }
+    // the unit's next pass starts with the cached primary hit
+    const int key0 = (int)sl.ldu(SF_KEY0);
+    h.code = key0;
+    N = sl.ld3(SF_N0X); P = sl.ld3(SF_P0X);
+    first = true;
+    phase = 0;
+    rng = seed_for(u, v, pass, p.date);
+    O = Ocam; D = camera_dir(p, u, v);
+    att = mk(0.8f, 0.8f, 0.8f); total = mk(0.0f, 0.0f, 0.0f);
+    bounce = 0;
+  }
+}
+
+__global__ __launch_bounds__(256, MCPT_MIN_WAVES_SHADE) void stream_shade_kernel(StreamParams q) {
+  const int par = q.parity;
+  const unsigned n = q.ctr[SC_CNT + par];
+  if (blockIdx.x == 0 && threadIdx.x == 0) q.ctr[SC_FETCH + (par ^ 1)] = 0u;   // the next trace kernel's fetch counter
+  const int* in = q.queue[par];
+  int* out = q.queue[par ^ 1];
+  unsigned* cnt_out = q.ctr + SC_CNT + (par ^ 1);
+  const int lane = threadIdx.x & 63;
+  for (unsigned base = blockIdx.x * 256u; base < n; base += gridDim.x * 256u) {   // block-uniform
+    const unsigned i = base + threadIdx.x;
+    int slot = -1;
+    bool push = false;
+    if (i < n) {
+      slot = in[i];
+      push = stream_shade(q, slot);
+    }
+    const uint64_t m = __ballot(push);
+    if (m) {
+      const int leader = __builtin_ffsll((long long)m) - 1;
+      unsigned b = 0;
+      if (lane == leader) b = atomicAdd(cnt_out, (unsigned)__builtin_popcountll(m));
+      b = (unsigned)__shfl((int)b, leader);
+      if (push) out[b + (unsigned)mbcnt64(m)] = slot;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // ray queries: the shader library's traverse_all_bvh / just_hit_bvh / intersect_one_prim /
 // hit_one_prim + intersection_info + intersection_color_info / _mat_info
 // (raytracer_func.frag:718-781, 874-907) for caller-supplied rays, one lane per ray
@@ -1627,5 +1977,21 @@ hipError_t mcpt_launch_combine(const mcpt::RenderParams& p, hipStream_t stream) 
   if (p.n_segments <= 1 || p.n_local_px <= 0) return hipSuccess;
   dim3 block(256), grid((unsigned)((p.n_local_px + 255) / 256));
   hipLaunchKernelGGL(mcpt::combine_kernel, grid, block, 0, stream, p.accum, p.partial, p.n_local_px, p.n_segments);
+  return hipGetLastError();
+}
+
+hipError_t mcpt_launch_stream_init(const mcpt::StreamParams& q, hipStream_t stream) {
+  if (q.n_slots <= 0) return hipSuccess;
+  dim3 block(256), grid((unsigned)((q.n_slots + 255) / 256));
+  hipLaunchKernelGGL(mcpt::stream_init_kernel, grid, block, 0, stream, q);
+  return hipGetLastError();
+}
+
+hipError_t mcpt_launch_stream_iter(const mcpt::StreamParams& q, int persistent_blocks, hipStream_t stream) {
+  dim3 block(256), grid((unsigned)persistent_blocks);
+  hipLaunchKernelGGL(mcpt::stream_trace_kernel, grid, block, 0, stream, q);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(mcpt::stream_shade_kernel, grid, block, 0, stream, q);
   return hipGetLastError();
 }

@@ -26,15 +26,15 @@ import numpy as np
 __all__ = [
     "MCPTError", "lib", "lib_path", "Scene", "Renderer", "camera_canonical",
     "MONTECARLO", "MAT", "MAT_TR", "EVENT_NAMES", "SCENE_KEYS",
-    "TRAVERSAL_AUTO", "TRAVERSAL_LANE", "TRAVERSAL_WAVE",
+    "TRAVERSAL_AUTO", "TRAVERSAL_LANE", "TRAVERSAL_WAVE", "TRAVERSAL_STREAM",
     "Transfo", "average", "write_pfm", "write_png", "material", "light", "Hit", "HIT_DTYPE",
 ]
 
 MONTECARLO, MAT, MAT_TR = 0, 1, 2
-TRAVERSAL_AUTO, TRAVERSAL_LANE, TRAVERSAL_WAVE = 0, 1, 2
+TRAVERSAL_AUTO, TRAVERSAL_LANE, TRAVERSAL_WAVE, TRAVERSAL_STREAM = 0, 1, 2, 3
 # launches of one shape AUTO spends on its timing trials before it settles (up to four candidate
 # schedules, each timed twice: mcpt_capi.hip kTuneRounds); callers that measure run these first
-AUTO_TRIALS = 8
+AUTO_TRIALS = 10
 EVENT_NAMES = ("node", "leaf", "prim", "cand", "geom", "colmat", "sample", "trav", "mesh", "tri", "mgeom")
 # key bindings of montecarlo.cpp:251-290: scene id -> key
 SCENE_KEYS = {1: "Q", 2: "W", 3: "E", 4: "R", 5: "T", 6: "Y", 7: "U", 8: "I"}
@@ -104,6 +104,8 @@ def _declare(L: ctypes.CDLL) -> None:
         "mcpt_set_leaf_batch": (i, [_vp, i]),
         "mcpt_get_leaf_batch": (i, [_vp, ip]),
         "mcpt_set_partial_budget": (i, [_vp, ctypes.c_size_t]),
+        "mcpt_set_stream_pool": (i, [_vp, i, i]),
+        "mcpt_stream_iterations": (i, [_vp, ctypes.POINTER(ctypes.c_longlong)]),
         "mcpt_last_launch_count": (i, [_vp, ip]),
         "mcpt_set_stream": (i, [_vp, _vp]),
         "mcpt_synchronize": (i, [_vp]),
@@ -554,7 +556,7 @@ class Renderer:
         return out
 
     def set_traversal(self, mode: int) -> None:
-        """BVH traversal strategy: TRAVERSAL_AUTO / _LANE / _WAVE (same results)."""
+        """BVH traversal strategy: TRAVERSAL_AUTO / _LANE / _WAVE / _STREAM (same results)."""
         _check(lib().mcpt_set_traversal(self._h, int(mode)), "mcpt_set_traversal")
 
     def set_walk_exit(self, lanes: int) -> None:
@@ -573,6 +575,17 @@ class Renderer:
     def leaf_batch(self) -> int:
         n = ctypes.c_int()
         _check(lib().mcpt_get_leaf_batch(self._h, ctypes.byref(n)), "mcpt_get_leaf_batch")
+        return n.value
+
+    def set_stream_pool(self, slots: int = 0, refill: int = -1) -> None:
+        """Stream schedule knobs (mcpt_set_stream_pool): path slots (0 = default) and the trace
+        kernel's refill threshold (-1 = default).  Same results for every value."""
+        _check(lib().mcpt_set_stream_pool(self._h, int(slots), int(refill)), "mcpt_set_stream_pool")
+
+    def stream_iterations(self) -> int:
+        """Iterations (trace + shade kernel pairs) of the last stream-schedule launch."""
+        n = ctypes.c_longlong()
+        _check(lib().mcpt_stream_iterations(self._h, ctypes.byref(n)), "mcpt_stream_iterations")
         return n.value
 
     def set_partial_budget(self, nbytes: int) -> None:
@@ -594,11 +607,11 @@ class Renderer:
 
     def schedule(self) -> dict:
         """The schedule of the next launch of the last launch shape (mcpt_get_schedule):
-        traversal ("lane"/"wave"), pass segments per work item, AUTO settled or not."""
+        traversal ("lane"/"wave"/"stream"), pass segments per work item, AUTO settled or not."""
         t, k, s = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         _check(lib().mcpt_get_schedule(self._h, ctypes.byref(t), ctypes.byref(k), ctypes.byref(s)),
                "mcpt_get_schedule")
-        return {"traversal": {1: "lane", 2: "wave"}.get(t.value, str(t.value)), "seg_per_item": k.value,
+        return {"traversal": {1: "lane", 2: "wave", 3: "stream"}.get(t.value, str(t.value)), "seg_per_item": k.value,
                 "settled": bool(s.value)}
 
     def set_stream(self, hip_stream_ptr: int) -> None:

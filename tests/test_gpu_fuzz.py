@@ -30,7 +30,7 @@ def test_random_scene_render(mcpt_mod, oracle_mod, renderer, seed):
     first, S, B = int(rng.integers(1, 80)), int(rng.integers(1, 5)), int(rng.integers(0, 11))
     ior = 1.0 if rng.random() < 0.4 else float(rng.uniform(1.05, 2.0))
     variant = 0 if rng.random() < 0.8 else int(rng.integers(1, 3))
-    traversal = int(rng.integers(1, 3))
+    traversal = int(rng.integers(1, 4))
     walk_exit = int(rng.choice([-1, 0, 4, 16, 40]))
     leaf_batch = int(rng.choice([-1, 0, 2, 8, 64]))
     renderer.set_traversal(traversal)

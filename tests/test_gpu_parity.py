@@ -56,7 +56,7 @@ def _compare(gpu, ref, what):
     assert diff.max() <= TOL
 
 
-TRAVERSALS = [1, 2]   # MCPT_TRAVERSAL_LANE, MCPT_TRAVERSAL_WAVE: same bits required from both
+TRAVERSALS = [1, 2, 3]   # MCPT_TRAVERSAL_LANE, _WAVE, _STREAM: same bits required from all
 
 
 @pytest.mark.parametrize("traversal", TRAVERSALS)

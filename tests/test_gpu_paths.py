@@ -1,7 +1,7 @@
 """The HIP kernel against the independent integrator restatement (tests/golden/paths.npz, see
 tests/test_oracle_paths.py): every one of the 688 (pixel, pass) samples (all three tp/ programs) at 1080p, rendered as a
 one-pass launch of the sample's row through the C ABI, must equal the restatement bit for bit,
-under both BVH walks."""
+under every schedule (per-lane walk, wave-coherent walk, stream)."""
 import numpy as np
 import pytest
 
@@ -10,7 +10,7 @@ from test_oracle_paths import GOLDEN
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("traversal", [1, 2])   # MCPT_TRAVERSAL_LANE, MCPT_TRAVERSAL_WAVE
+@pytest.mark.parametrize("traversal", [1, 2, 3])   # MCPT_TRAVERSAL_LANE, _WAVE, _STREAM
 def test_gpu_matches_independent_paths(mcpt_mod, traversal):
     kat = dict(np.load(GOLDEN, allow_pickle=False))
     W, H = int(kat["path_W"]), int(kat["path_H"])

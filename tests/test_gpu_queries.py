@@ -90,7 +90,7 @@ def cone_scene(mcpt_mod, light=1.2):
     return s
 
 
-@pytest.mark.parametrize("traversal", [1, 2])
+@pytest.mark.parametrize("traversal", [1, 2, 3])
 def test_cone_scene_render(mcpt_mod, oracle_mod, renderer, traversal):
     sc = cone_scene(mcpt_mod)
     prims, nodes, leaves = sc.buffers()
