@@ -93,16 +93,16 @@ struct mcpt_ctx {
   int tune_choice = 0;              // resolved candidate once all are measured
   int walk_exit = -1;               // mcpt_set_walk_exit; -1: by BVH depth
   int leaf_batch = -1;              // MCPT_LEAF_BATCH env (tuning); -1: default
-  // stream schedule (MCPT_TRAVERSAL_STREAM): slot pool, ray queues, counters
+  // stream schedule (MCPT_TRAVERSAL_STREAM): slot pool, payload queues, counters
   int n_cu = 0;                     // compute units of the device (persistent grids)
   float* d_slots = nullptr;         // SF_COUNT x slot capacity
-  int* d_queue = nullptr;           // 2 x slot capacity
+  float* d_queue = nullptr;         // 2 x QF_COUNT x slot capacity
   unsigned* d_sctr = nullptr;       // SC_COUNT counters
   int slot_cap = 0;
-  unsigned* h_cnt = nullptr;        // pinned: queue counts read back after each batch (2)
+  unsigned* h_sctr = nullptr;       // pinned: the counters read back after each batch (2 x SC_COUNT)
   hipEvent_t batch_ev[2] = {nullptr, nullptr};
-  int stream_slots = 0;             // MCPT_STREAM_SLOTS env: pool size (0: default)
-  int stream_refill = -1;           // MCPT_STREAM_REFILL env: refill threshold (-1: default)
+  int stream_slots = 0;             // MCPT_STREAM_SLOTS env / mcpt_set_stream_pool (0: default)
+  int stream_refill = -1;           // MCPT_STREAM_REFILL env / mcpt_set_stream_pool (-1: default)
   long long stream_iters = 0;       // iterations of the last stream render (diagnostics)
 };
 
@@ -304,7 +304,7 @@ int mcpt_destroy(mcpt_ctx* c) {
   (void)hipFree(c->d_slots);
   (void)hipFree(c->d_queue);
   (void)hipFree(c->d_sctr);
-  if (c->h_cnt) (void)hipHostFree(c->h_cnt);
+  if (c->h_sctr) (void)hipHostFree(c->h_sctr);
   for (hipEvent_t e : c->batch_ev) if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->evs) (void)hipEventDestroy(e);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -586,27 +586,30 @@ static void corner_rays(const float* invPV, const float* invV, mcpt::RenderParam
   }
 }
 
-// stream schedule defaults: 4 M path slots (160 B of state each: 640 MB) keep every trace
-// kernel of an iteration long against its tail (the last walks of the iteration); a wave refills
-// its lanes once 8 of them have finished their walks
+// stream schedule defaults: 4 Mi path slots (92 B of queue payload x 2 + 64 B of unit data
+// each: 1 GB) keep every trace kernel of an iteration long against its tail (the last walks
+// of the iteration); a wave refills its idle lanes once 8 of them have finished their walks
 constexpr int kStreamSlotsDefault = 1 << 22;
 constexpr int kStreamRefillDefault = 56;
-constexpr int kStreamBatch = 8;   // iterations issued between two checks of the queue count
+constexpr int kStreamBatch = 8;   // iterations issued between two reads of the counters
+// the shade kernel compacts its output (drops dead entries) once fewer than this share of the
+// queue is live
+constexpr double kStreamCompactBelow = 0.6;
 
 static bool stream_applies(const mcpt_ctx* c, int variant, int bounces, bool count) {
   return !count && variant == 0 && bounces > 0 && c->n_meshes == 0;
 }
 
 // One sub-launch (one pass range of <= max_seg segments) with the stream schedule: slots set up,
-// then iterations (trace + shade) in batches until the ray queue is empty.  The host reads the
-// queue count of batch b-1 while batch b runs, so the device never waits for the host.
+// then iterations (trace + shade) in batches until every slot has run out of units.  The host
+// reads the counters of batch b-1 while batch b runs, so the device never waits for the host.
 static int stream_run(mcpt_ctx* c, const mcpt::RenderParams& p) {
   const unsigned long long n_units = (unsigned long long)p.n_local_px * (unsigned long long)p.n_segments;
   if (n_units == 0) return MCPT_OK;
   if (n_units >= (1ULL << 31) || p.n_local_px >= (1LL << 31))
     return set_err(MCPT_ERR_INVALID_ARG, "stream schedule: too many units in one launch");
-  // the kernels address the pool through one buffer resource: below 2 GiB
-  const int max_slots = (int)(((1ULL << 31) - 1) / (mcpt::SF_COUNT * sizeof(float)));
+  // the kernels address a queue / the slot data through one buffer resource: below 2 GiB each
+  const int max_slots = (int)(((1ULL << 31) - 1) / (mcpt::QF_COUNT * sizeof(float)));
   const int want = std::min(c->stream_slots > 0 ? c->stream_slots : kStreamSlotsDefault, max_slots);
   const int n_slots = (int)std::min<unsigned long long>(n_units, (unsigned long long)want);
   if (n_slots > c->slot_cap) {
@@ -614,43 +617,57 @@ static int stream_run(mcpt_ctx* c, const mcpt::RenderParams& p) {
     (void)hipFree(c->d_slots); (void)hipFree(c->d_queue);
     c->d_slots = nullptr; c->d_queue = nullptr; c->slot_cap = 0;
     HIP_OR_RETURN(hipMalloc(&c->d_slots, (size_t)mcpt::SF_COUNT * n_slots * sizeof(float)));
-    HIP_OR_RETURN(hipMalloc(&c->d_queue, (size_t)2 * n_slots * sizeof(int)));
+    HIP_OR_RETURN(hipMalloc(&c->d_queue, (size_t)2 * mcpt::QF_COUNT * n_slots * sizeof(float)));
     c->slot_cap = n_slots;
   }
   if (!c->d_sctr) HIP_OR_RETURN(hipMalloc(&c->d_sctr, mcpt::SC_COUNT * sizeof(unsigned)));
-  if (!c->h_cnt) HIP_OR_RETURN(hipHostMalloc(&c->h_cnt, 2 * sizeof(unsigned), hipHostMallocDefault));
+  if (!c->h_sctr) HIP_OR_RETURN(hipHostMalloc(&c->h_sctr, 2 * mcpt::SC_COUNT * sizeof(unsigned), hipHostMallocDefault));
   for (hipEvent_t& e : c->batch_ev)
     if (!e) HIP_OR_RETURN(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   mcpt::StreamParams q;
   q.r = p;
-  q.st = c->d_slots;
-  // slot field f of slot i at st[f * n_slots + i]: the pool is laid out for this launch's slot count
+  q.slots = c->d_slots;
+  // field f of entry i at queue[par][f * n_slots + i]: laid out for this launch's slot count
   q.queue[0] = c->d_queue;
-  q.queue[1] = c->d_queue + n_slots;
+  q.queue[1] = c->d_queue + (size_t)mcpt::QF_COUNT * n_slots;
   q.ctr = c->d_sctr;
   q.n_slots = n_slots;
   q.n_units = (unsigned)n_units;
   q.parity = 0;
   q.refill = c->stream_refill >= 0 ? c->stream_refill : kStreamRefillDefault;
+  q.compact = 0;
   HIP_OR_RETURN(mcpt_launch_stream_init(q, c->stream));
+  const unsigned n0 = (unsigned)n_slots;   // slots that start with a unit (n_slots <= n_units)
   // every iteration advances each live slot by one traversal; a unit needs at most
   // (passes) x (2 B + 1) + 1 of them, and a slot runs ceil(units / slots) units
   const long long per_unit = (long long)mcpt::kPassChunk * (2LL * p.bounces + 1) + 1;
-  const long long cap = ((long long)((n_units + n_slots - 1) / n_slots) + 1) * per_unit + 2 * kStreamBatch;
-  const int blocks = c->n_cu * 8;   // persistent waves: 8 workgroups of 4 waves per CU
+  const long long cap = ((long long)((n_units + n_slots - 1) / n_slots) + 1) * per_unit + 4 * kStreamBatch;
+  // BVH nodes in the trace kernel's LDS where they fit (MCPT_STREAM_LDS_NODES=1): off by default,
+  // no faster on scenes 3/7/8 (random lanes' node reads conflict in the LDS banks, 11 conflict
+  // cycles per LDS instruction; gpurun_out r03e/r03f)
+  const bool lds_nodes = env_int("MCPT_STREAM_LDS_NODES", 0) != 0 && mcpt_stream_lds_nodes_fit(p.depth);
+  // leaf batching of the trace kernel's walks: 16 lanes (8 for the megakernel; scene 8: 16 is
+  // +4 % over 8 and 32, 4 is -8 %)
+  if (c->leaf_batch < 0) q.r.leaf_batch = 16;
   long long it = 0;
+  bool compact = false;
   for (int b = 0;; ++b) {
     for (int k = 0; k < kStreamBatch; ++k, ++it) {
       q.parity = (int)(it & 1);
-      HIP_OR_RETURN(mcpt_launch_stream_iter(q, blocks, c->stream));
+      q.compact = (k == 0 && compact) ? 1 : 0;
+      HIP_OR_RETURN(mcpt_launch_stream_iter(q, c->n_cu, lds_nodes, c->stream));
     }
-    // queue count the next iteration will read
-    HIP_OR_RETURN(hipMemcpyAsync(c->h_cnt + (b & 1), c->d_sctr + mcpt::SC_CNT + (it & 1), sizeof(unsigned),
-                                 hipMemcpyDeviceToHost, c->stream));
+    unsigned* h = c->h_sctr + (b & 1) * mcpt::SC_COUNT;
+    HIP_OR_RETURN(hipMemcpyAsync(h, c->d_sctr, mcpt::SC_COUNT * sizeof(unsigned), hipMemcpyDeviceToHost, c->stream));
     HIP_OR_RETURN(hipEventRecord(c->batch_ev[b & 1], c->stream));
     if (b >= 1) {
       HIP_OR_RETURN(hipEventSynchronize(c->batch_ev[(b - 1) & 1]));
-      if (c->h_cnt[(b - 1) & 1] == 0u) break;   // batch b found nothing to do
+      const unsigned* hp = c->h_sctr + ((b - 1) & 1) * mcpt::SC_COUNT;
+      const unsigned dead = hp[mcpt::SC_DEAD];
+      if (dead >= n0) break;   // every slot was done by the end of batch b-1
+      // the queue length the iteration after batch b-1 read (in place: unchanged until compacted)
+      const unsigned len = hp[mcpt::SC_CNT + (int)((it - kStreamBatch) & 1)];
+      compact = (double)(n0 - dead) < kStreamCompactBelow * (double)len;
     }
     if (it > cap) return set_err(MCPT_ERR_HIP, "stream schedule did not drain its queue");
   }

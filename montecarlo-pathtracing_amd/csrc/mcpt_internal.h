@@ -90,31 +90,39 @@ struct RenderParams {
 };
 
 // Stream schedule (MCPT_TRAVERSAL_STREAM): wavefront path tracing in two
-// kernels per iteration over a pool of path slots.  Slot state is SoA, field f of slot i at
-// st[f * n_slots + i].
-enum StreamField {
-  SF_OX, SF_OY, SF_OZ, SF_DX, SF_DY, SF_DZ,   // the ray the next traversal walks
-  SF_AX, SF_AY, SF_AZ, SF_TX, SF_TY, SF_TZ,   // att, total
-  SF_RX, SF_RY, SF_RZ,                        // RNG state (u32 bits)
-  SF_STATE,                                   // bounce | phase << 8 (u32 bits)
-  SF_PASS, SF_UNIT,                           // current pass, unit = segment * n_local_px + px
+// kernels per iteration.  Rays travel in a queue of payloads (SoA, field f of entry i at
+// queue[par][f * n_slots + i]): the ray, the path state and, once traced, the hit record, so
+// both kernels read and write them contiguously; the data of a (pixel, pass segment) unit
+// that outlives one ray (its sum, cached primary hit, N/P across an inner walk) stays in the
+// slot that runs the unit (slots[f * n_slots + slot]).
+enum QueueField {
+  QF_OX, QF_OY, QF_OZ, QF_DX, QF_DY, QF_DZ,   // the ray
+  QF_AX, QF_AY, QF_AZ, QF_TX, QF_TY, QF_TZ,   // att, total
+  QF_RX, QF_RY, QF_RZ,                        // RNG state (u32 bits)
+  QF_STATE,                                   // bounce | phase << 8 (u32 bits)
+  QF_PASS, QF_UNIT,                           // current pass; unit = segment * n_local_px + px
+  QF_SLOT,                                    // the slot running the unit (-1: a dead entry)
+  QF_HX, QF_HY, QF_HZ, QF_HCODE,              // the traversal's hit record (pl, code)
+  QF_COUNT
+};
+enum SlotField {
   SF_SX, SF_SY, SF_SZ,                        // the unit's sum (passes in order, from 0)
   SF_N0X, SF_N0Y, SF_N0Z, SF_P0X, SF_P0Y, SF_P0Z, SF_KEY0,   // the unit's cached primary hit
   SF_NSX, SF_NSY, SF_NSZ, SF_PSX, SF_PSY, SF_PSZ,            // N, P kept across an inner walk
-  SF_HX, SF_HY, SF_HZ, SF_HDIST, SF_HCODE,    // the traversal's hit record (pl, dist, code)
   SF_COUNT
 };
-// ctr[]: queue counts [0..1], trace-kernel fetch counters [2..3], next unit [4]
-enum { SC_CNT = 0, SC_FETCH = 2, SC_UNIT = 4, SC_COUNT = 8 };
+// ctr[]: queue lengths [0..1], trace-kernel fetch counters [2..3], next unit [4], dead slots [5]
+enum { SC_CNT = 0, SC_FETCH = 2, SC_UNIT = 4, SC_DEAD = 5, SC_COUNT = 8 };
 struct StreamParams {
   RenderParams r;               // scene, target, the sub-launch's pass range and constants
-  float* st;                    // SF_COUNT x n_slots
-  int* queue[2];                // slots whose ray waits for a traversal (ping-pong by parity)
+  float* slots;                 // SF_COUNT x n_slots
+  float* queue[2];              // QF_COUNT x n_slots each (ping-pong by parity)
   unsigned* ctr;                // SC_* counters
   int n_slots;
   unsigned n_units;             // n_segments x n_local_px
   int parity;                   // iteration & 1: queue[parity] is this iteration's input
   int refill;                   // trace kernel: refill a wave's idle lanes once <= this many still walk
+  int compact;                  // this iteration's shade kernel drops dead entries (atomic append)
 };
 
 // ray-query batch (mcpt_trace): per ray 3 ints (shape, prim, dir) and kTraceFloats floats
@@ -159,4 +167,6 @@ hipError_t mcpt_launch_combine(const mcpt::RenderParams& p, hipStream_t stream);
 // stream schedule: slot set-up (queue[0] = every slot with a unit), then one iteration = the
 // trace kernel over queue[parity] + the shade kernel appending to queue[parity ^ 1]
 hipError_t mcpt_launch_stream_init(const mcpt::StreamParams& q, hipStream_t stream);
-hipError_t mcpt_launch_stream_iter(const mcpt::StreamParams& q, int persistent_blocks, hipStream_t stream);
+hipError_t mcpt_launch_stream_iter(const mcpt::StreamParams& q, int n_cu, bool lds_nodes, hipStream_t stream);
+// the trace kernel can hold a BVH of this depth in LDS (nodes + leaf ids)
+bool mcpt_stream_lds_nodes_fit(int depth);

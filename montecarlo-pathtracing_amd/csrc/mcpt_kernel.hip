@@ -1514,51 +1514,75 @@ __global__ __launch_bounds__(256) void combine_kernel(float* __restrict__ accum,
 
 // ------------------------------------------------------------------------------------
 // stream schedule (MCPT_TRAVERSAL_STREAM): wavefront path tracing for deep
-// BVHs.  A pool of path slots (SoA in HBM, StreamField) each runs one (pixel, pass segment)
-// unit at a time, its passes in order (the unit's sum is the megakernel's segment sum, so the
-// bits are the same); an iteration is
-//   stream_trace_kernel: persistent waves walk the queued slots' rays, a lane taking the next
-//     queued ray as soon as its walk ends (no lane waits for the wave's longest walk);
-//   stream_shade_kernel: one lane per queued slot shades the hit (tp/montecarlo.frag:100-179),
-//     ends passes / units, takes new units, and queues the slot's next ray.
-// Each slot's sequence of operations is the megakernel's (same traversal, same shading, same
-// RNG draws, same sums), only the interleaving across slots changes.
+// BVHs.  A pool of path slots each runs one (pixel, pass segment) unit at a time, its passes
+// in order (the unit's sum is the megakernel's segment sum, so the bits are the same).  The
+// rays travel through a queue of payloads (ray, path state, then hit record); an iteration is
+//   stream_trace_kernel: persistent waves claim chunks of the queue, stage their live rays in
+//     LDS and walk them with the per-lane DFS; a lane whose walk ends takes the next staged ray
+//     at the wave's next refill point (no lane waits for the wave's longest walk);
+//   stream_shade_kernel: one lane per queue entry shades the hit (tp/montecarlo.frag:100-179),
+//     ends passes and units, takes new units, and writes the entry's next payload (in place,
+//     or appended when the host asks for compaction).
+// Each path's sequence of operations is the megakernel's (same traversal, same shading, same
+// RNG draws, same sums): only the interleaving across paths changes.
 // ------------------------------------------------------------------------------------
-constexpr uint32_t kPhaseInner = 1, kPhasePrimary = 2, kSlotDead = 0xFFFFFFFFu;
+constexpr uint32_t kPhaseInner = 1, kPhasePrimary = 2;
+constexpr int kStreamBlock = 256, kStreamWaves = kStreamBlock / 64;   // stream kernels' workgroups
 #ifndef MCPT_MIN_WAVES_STREAM
 #define MCPT_MIN_WAVES_STREAM 8
 #endif
-// the shade kernel streams slot state from HBM: occupancy over registers
+// the shade kernel streams payloads from HBM: occupancy over registers
 #ifndef MCPT_MIN_WAVES_SHADE
 #define MCPT_MIN_WAVES_SHADE 5
 #endif
+// queue entries a trace wave claims (one atomic) and stages in LDS at once
+#ifndef MCPT_STREAM_CHUNK
+#define MCPT_STREAM_CHUNK 128
+#endif
+constexpr int kStreamChunk = MCPT_STREAM_CHUNK;
+// trace waves stage each claimed chunk in order of the rays' direction octants
+#ifndef MCPT_STREAM_SORT
+#define MCPT_STREAM_SORT 1
+#endif
+static_assert(kStreamChunk % 64 == 0, "chunks are staged 64 entries per step");
 
-// Slot i's fields through a buffer resource over the pool: the field's column offset is a
-// wave-uniform scalar (soffset) and the lane's offset one 32-bit VGPR shared by every field, so
-// no 64-bit per-lane address is formed or kept per field (with plain pointers the compiler
-// strength-reduced the field columns into ~40 live 64-bit addresses and spilled them).
-// Pools are < 2 GiB (host check).  0x00020000: the gfx9 raw-buffer descriptor word 3.
-struct SlotRef {
+// Field columns through a buffer resource: the column offset f * n * 4 is a wave-uniform
+// scalar (soffset) and the entry offset i * 4 one 32-bit VGPR shared by every field, so no
+// 64-bit per-lane address is formed or kept per field (with plain pointers the compiler
+// strength-reduced ~40 columns into live 64-bit addresses and spilled them).  Buffers stay
+// below 2 GiB (host check).  0x00020000: the gfx9 raw-buffer descriptor word 3.
+// Queue payloads are streamed once per iteration: their loads and stores carry the
+// non-temporal hint (MCPT_STREAM_NT, aux bit 1: nt on gfx950) so that they do not evict the
+// BVH records the walks read through L2.
+#ifndef MCPT_STREAM_NT
+#define MCPT_STREAM_NT 1
+#endif
+constexpr int kQueueAux = MCPT_STREAM_NT ? 2 : 0;
+template <int AUX>
+struct ColsT {
   __amdgpu_buffer_rsrc_t rs;
-  uint32_t col_bytes;   // n_slots * 4: one field column
-  uint32_t off;         // slot * 4
-  __device__ __forceinline__ uint32_t ldu(int f) const {
-    return __builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, (int)((uint32_t)f * col_bytes), 0);
+  uint32_t col_bytes;   // one column: n * 4 bytes
+  __device__ __forceinline__ uint32_t ldu(int f, uint32_t i) const {
+    return __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(i * 4u), (int)((uint32_t)f * col_bytes), AUX);
   }
-  __device__ __forceinline__ float ld(int f) const { return __uint_as_float(ldu(f)); }
-  __device__ __forceinline__ void setu(int f, uint32_t v) const {
-    __builtin_amdgcn_raw_buffer_store_b32(v, rs, (int)off, (int)((uint32_t)f * col_bytes), 0);
+  __device__ __forceinline__ float ld(int f, uint32_t i) const { return __uint_as_float(ldu(f, i)); }
+  __device__ __forceinline__ void setu(int f, uint32_t i, uint32_t v) const {
+    __builtin_amdgcn_raw_buffer_store_b32(v, rs, (int)(i * 4u), (int)((uint32_t)f * col_bytes), AUX);
   }
-  __device__ __forceinline__ void set(int f, float v) const { setu(f, __float_as_uint(v)); }
-  __device__ __forceinline__ f3 ld3(int f) const { return mk(ld(f), ld(f + 1), ld(f + 2)); }
-  __device__ __forceinline__ void set3(int f, f3 v) const { set(f, v.x); set(f + 1, v.y); set(f + 2, v.z); }
+  __device__ __forceinline__ void set(int f, uint32_t i, float v) const { setu(f, i, __float_as_uint(v)); }
+  __device__ __forceinline__ f3 ld3(int f, uint32_t i) const { return mk(ld(f, i), ld(f + 1, i), ld(f + 2, i)); }
+  __device__ __forceinline__ void set3(int f, uint32_t i, f3 v) const {
+    set(f, i, v.x); set(f + 1, i, v.y); set(f + 2, i, v.z);
+  }
 };
-__device__ __forceinline__ SlotRef slot_ref(const StreamParams& q, uint32_t i) {
-  SlotRef r;
-  r.col_bytes = (uint32_t)q.n_slots * 4u;
-  r.rs = __builtin_amdgcn_make_buffer_rsrc(q.st, 0, (int)((uint32_t)SF_COUNT * r.col_bytes), 0x00020000);
-  r.off = i * 4u;
-  return r;
+typedef ColsT<kQueueAux> Cols;   // queue payloads
+typedef ColsT<0> SlotCols;       // per-unit slot data (read and written at pass ends: cached)
+template <int AUX = kQueueAux>
+__device__ __forceinline__ ColsT<AUX> cols(float* base, int n, int n_fields) {
+  ColsT<AUX> c;
+  c.col_bytes = (uint32_t)n * 4u;
+  c.rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)((uint32_t)n_fields * c.col_bytes), 0x00020000);
+  return c;
 }
 
 // a unit = (pass segment, local pixel): its pixel and its pass range in this launch
@@ -1577,142 +1601,226 @@ __device__ __forceinline__ UnitGeom unit_geom(const RenderParams& p, uint32_t un
   return g;
 }
 
-// a slot starts `unit`: its camera ray is queued for the primary traversal
-__device__ __forceinline__ void stream_start_unit(const RenderParams& p, const SlotRef& sl, uint32_t unit) {
+// a queue entry's path state besides the ray and the hit
+struct Payload {
+  f3 O, D, att, total;
+  Rng rng;
+  uint32_t state, pass, unit;
+};
+__device__ __forceinline__ void put_payload(const Cols& Q, uint32_t i, const Payload& pl, int slot) {
+  Q.set3(QF_OX, i, pl.O); Q.set3(QF_DX, i, pl.D); Q.set3(QF_AX, i, pl.att); Q.set3(QF_TX, i, pl.total);
+  Q.setu(QF_RX, i, pl.rng.x); Q.setu(QF_RY, i, pl.rng.y); Q.setu(QF_RZ, i, pl.rng.z);
+  Q.setu(QF_STATE, i, pl.state); Q.setu(QF_PASS, i, pl.pass); Q.setu(QF_UNIT, i, pl.unit);
+  Q.setu(QF_SLOT, i, (uint32_t)slot);
+}
+// a slot starts `unit`: its camera ray goes to the primary traversal, its sum to 0
+__device__ __forceinline__ void start_unit(const RenderParams& p, const SlotCols& S, int slot, uint32_t unit,
+                                           Payload& pl) {
   const UnitGeom g = unit_geom(p, unit);
-  const f3 D = camera_dir(p, ((float)g.x + 0.5f) / (float)p.W, ((float)g.y + 0.5f) / (float)p.H);
-  sl.set3(SF_OX, mk(p.ox, p.oy, p.oz));
-  sl.set3(SF_DX, D);
-  sl.setu(SF_STATE, kPhasePrimary << 8);
-  sl.setu(SF_PASS, (uint32_t)g.pass_begin);
-  sl.setu(SF_UNIT, unit);
-  sl.set3(SF_SX, mk(0.0f, 0.0f, 0.0f));
+  pl.O = mk(p.ox, p.oy, p.oz);
+  pl.D = camera_dir(p, ((float)g.x + 0.5f) / (float)p.W, ((float)g.y + 0.5f) / (float)p.H);
+  pl.att = mk(0.0f, 0.0f, 0.0f); pl.total = pl.att;
+  pl.rng.x = pl.rng.y = pl.rng.z = 0u;
+  pl.state = kPhasePrimary << 8;
+  pl.pass = (uint32_t)g.pass_begin;
+  pl.unit = unit;
+  S.set3(SF_SX, (uint32_t)slot, mk(0.0f, 0.0f, 0.0f));
 }
 
 __global__ __launch_bounds__(256) void stream_init_kernel(StreamParams q) {
   const int i = blockIdx.x * 256 + threadIdx.x;
+  const unsigned n0 = (unsigned)q.n_slots < q.n_units ? (unsigned)q.n_slots : q.n_units;
   if (i == 0) {
-    const unsigned n0 = (unsigned)q.n_slots < q.n_units ? (unsigned)q.n_slots : q.n_units;
     q.ctr[SC_CNT] = n0;
     q.ctr[SC_CNT + 1] = 0u;
     q.ctr[SC_FETCH] = 0u;
     q.ctr[SC_FETCH + 1] = 0u;
     q.ctr[SC_UNIT] = n0;
+    q.ctr[SC_DEAD] = 0u;
   }
-  if (i >= q.n_slots) return;
-  const SlotRef sl = slot_ref(q, (uint32_t)i);
-  if ((unsigned)i < q.n_units) {
-    stream_start_unit(q.r, sl, (uint32_t)i);
-    q.queue[0][i] = i;
-  } else {
-    sl.setu(SF_STATE, kSlotDead);
-  }
+  if ((unsigned)i >= n0) return;
+  const Cols Q = cols(q.queue[0], q.n_slots, QF_COUNT);
+  const SlotCols S = cols<0>(q.slots, q.n_slots, SF_COUNT);
+  Payload pl;
+  start_unit(q.r, S, i, (uint32_t)i, pl);
+  put_payload(Q, (uint32_t)i, pl, i);
 }
 
-// The traversal half of an iteration: every queued slot's ray walked with the per-lane DFS of
-// walk_run (right child first, cull at push time, batched leaf visits) and its hit record
-// stored.  Persistent waves; a lane whose walk ended takes the next queued ray when the wave
-// leaves walk_run (at <= q.refill walking lanes), through one atomic per wave.
-__global__ __launch_bounds__(256, MCPT_MIN_WAVES_STREAM) void stream_trace_kernel(StreamParams q) {
+// The traversal half of an iteration: every live entry's ray walked with the per-lane DFS of
+// walk_run (right child first, cull at push time, batched leaf visits), its hit record stored
+// in the entry.  Persistent waves: a wave claims kStreamChunk entries with one atomic, stages
+// their rays in LDS (dead entries dropped), and whenever it leaves walk_run (at <= q.refill
+// walking lanes) its idle lanes take the next staged rays — LDS reads, so a refill waits on
+// no memory load.
+// LDSN: the BVH nodes and leaf ids live in the workgroup's LDS (copied once per persistent
+// workgroup; one 1024-thread workgroup per CU, 4 waves/SIMD), so the walk's dependent node
+// loads are LDS reads; primitive records stay in global memory.
+template <bool LDSN> struct TraceCfg {
+  static constexpr int kBlock = 256, kWaves = 4, kChunk = kStreamChunk, kMinWaves = MCPT_MIN_WAVES_STREAM;
+};
+template <> struct TraceCfg<true> {
+  static constexpr int kBlock = 1024, kWaves = 16, kChunk = 64, kMinWaves = 4;
+};
+// LDS of the LDSN trace kernel besides its scene copy: the waves' staged rays
+constexpr int kTraceLdsStaging = TraceCfg<true>::kWaves * TraceCfg<true>::kChunk * 32;
+
+template <bool LDSN>
+__global__ __launch_bounds__(TraceCfg<LDSN>::kBlock, TraceCfg<LDSN>::kMinWaves) void stream_trace_kernel(StreamParams q) {
+  typedef TraceCfg<LDSN> C;
+  constexpr int kChunkT = C::kChunk;
   const RenderParams& p = q.r;
-  const SceneT<false, false> s{p.nodes, p.leaves, p.ptype, p.prims, p.depth, p.minfo, p.mnodes, p.mleaves,
-                               p.mtris, p.mverts, p.mnorms, p.flat_face};
+  SceneT<false, false> s{p.nodes, p.leaves, p.ptype, p.prims, p.depth, p.minfo, p.mnodes, p.mleaves,
+                         p.mtris, p.mverts, p.mnorms, p.flat_face};
+  if constexpr (LDSN) {
+    extern __shared__ float4 s_bvh[];
+    const int n_nodes = (2 << p.depth) - 1, n_leaves = 1 << p.depth;
+    for (int k = threadIdx.x; k < 3 * n_nodes; k += C::kBlock) s_bvh[k] = p.nodes[k];
+    int* s_leaf = (int*)(s_bvh + 3 * n_nodes);
+    for (int k = threadIdx.x; k < n_leaves; k += C::kBlock) s_leaf[k] = p.leaves[k];
+    __syncthreads();
+    s.nodes = s_bvh;
+    s.leaves = s_leaf;
+  }
   const int par = q.parity;
   const unsigned n = q.ctr[SC_CNT + par];
-  if (blockIdx.x == 0 && threadIdx.x == 0) q.ctr[SC_CNT + (par ^ 1)] = 0u;   // the shade kernel's output count
-  const int* in = q.queue[par];
+  if (blockIdx.x == 0 && threadIdx.x == 0) q.ctr[SC_CNT + (par ^ 1)] = 0u;   // the shade kernel's output length
   unsigned* fetch = q.ctr + SC_FETCH + par;
-  const int lane = threadIdx.x & 63;
+  const Cols Q = cols(q.queue[par], q.n_slots, QF_COUNT);
+  __shared__ float4 s_ro[C::kWaves][kChunkT], s_rd[C::kWaves][kChunkT];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float4* ro = s_ro[wave];   // staged rays: (O, queue index bits), (D, 0)
+  float4* rd = s_rd[wave];
+  int live = 0, cc = 0;      // wave-uniform: staged rays of the current chunk, first unserved
+  bool more = true;          // wave-uniform: the queue may hold unclaimed entries
   Ev<false> ev;
   ev.init();
-  int r = -1;
-  bool more = true;
+  int r = -1;                // queue index of this lane's ray
   f3 O = mk(0.0f, 0.0f, 0.0f), D = O;
   Hit h;
   h.pl = O; h.dist = kFLTMAX; h.clear(); h.tri = 0; h.cull2 = 0.0;
   Walk w;
   w.invD = O; w.node = 0; w.level = 0; w.pending = 0;
   for (;;) {
-    const bool need = r < 0 && more;
-    const uint64_t m = __ballot(need);
-    if (m) {
-      const int leader = __builtin_ffsll((long long)m) - 1;
-      unsigned b = 0;
-      if (lane == leader) b = atomicAdd(fetch, (unsigned)__builtin_popcountll(m));
-      b = (unsigned)__shfl((int)b, leader);
-      if (need) {
-        const unsigned idx = b + (unsigned)mbcnt64(m);
-        if (idx < n) {
-          r = in[idx];
-          const SlotRef sl = slot_ref(q, (uint32_t)r);
-          O = sl.ld3(SF_OX);
-          D = sl.ld3(SF_DX);
-          walk_begin<false>(s, D, h, w, ev, p.cull2_max);
-        } else {
+    // idle lanes take staged rays; an empty stage claims and stages the next chunk
+    for (;;) {
+      const uint64_t need = __ballot(r < 0);
+      if (!need) break;
+      if (cc == live) {
+        if (!more) break;
+        unsigned b = 0;
+        if (lane == 0) b = atomicAdd(fetch, (unsigned)kChunkT);
+        b = (unsigned)__shfl((int)b, 0);
+        if (b >= n) {
           more = false;
+          break;
         }
+        const unsigned e = min(b + (unsigned)kChunkT, n);
+        live = 0;
+        cc = 0;
+        // the chunk's live entries (neighbouring pixels' rays), staged in order of the
+        // direction octant (MCPT_STREAM_SORT): lanes that take consecutive staged rays then
+        // walk rays of one octant from nearby origins, which visit the same nodes and take the
+        // same branches
+        constexpr int G = kChunkT / 64;
+        float4 eo[G], ed[G];
+        int key[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const unsigned idx = b + (unsigned)(g * 64) + (unsigned)lane;
+          const int slot = idx < e ? (int)Q.ldu(QF_SLOT, idx) : -1;
+          eo[g] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(idx));
+          ed[g] = eo[g];
+          key[g] = 8;   // dead / beyond the queue: not staged
+          if (slot >= 0) {
+            eo[g].x = Q.ld(QF_OX, idx); eo[g].y = Q.ld(QF_OY, idx); eo[g].z = Q.ld(QF_OZ, idx);
+            ed[g].x = Q.ld(QF_DX, idx); ed[g].y = Q.ld(QF_DY, idx); ed[g].z = Q.ld(QF_DZ, idx);
+            key[g] = MCPT_STREAM_SORT ? ((ed[g].x < 0.0f) | ((ed[g].y < 0.0f) << 1) | ((ed[g].z < 0.0f) << 2)) : 0;
+          }
+        }
+#pragma unroll
+        for (int o = 0; o < (MCPT_STREAM_SORT ? 8 : 1); ++o) {
+#pragma unroll
+          for (int g = 0; g < G; ++g) {
+            const bool mine = key[g] == o;
+            const uint64_t m = __ballot(mine);
+            if (mine) {
+              const int pos = live + mbcnt64(m);
+              ro[pos] = eo[g];
+              rd[pos] = ed[g];
+            }
+            live += __builtin_popcountll(m);
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+        continue;
       }
+      const int k = mbcnt64(need);
+      const int avail = live - cc;
+      if (r < 0 && k < avail) {
+        const float4 a = ro[cc + k], d = rd[cc + k];
+        r = (int)__float_as_uint(a.w);
+        O = mk(a.x, a.y, a.z);
+        D = mk(d.x, d.y, d.z);
+        walk_begin<false>(s, D, h, w, ev, p.cull2_max);
+      }
+      cc += min(__builtin_popcountll(need), avail);
     }
-    if (__ballot(r >= 0) == 0) break;
+    if (__ballot(r >= 0) == 0) break;   // nothing staged and nothing left to claim
     if (r >= 0) {
       if (walk_run<false, true>(s, O, D, h, w, ev, q.refill, p.leaf_batch)) {
-        const SlotRef sl = slot_ref(q, (uint32_t)r);
-        sl.set3(SF_HX, h.pl);
-        sl.setu(SF_HCODE, (uint32_t)h.code);
+        Q.set3(QF_HX, (uint32_t)r, h.pl);
+        Q.setu(QF_HCODE, (uint32_t)r, (uint32_t)h.code);
         r = -1;
       }
     }
   }
 }
 
-// The shading half: slot i's hit through tp/montecarlo.frag:100-179 (the megakernel's shading
-// block, variant montecarlo.frag).  A path that ends adds its result to the unit's sum in pass
-// order and the slot goes on with the unit's next pass, whose camera ray is the cached primary
-// hit (shaded at once, no traversal); a unit that ends writes its sum and the slot takes the
-// next unit.  Returns true when the slot's next ray must be traversed.
-__device__ __forceinline__ bool stream_shade(const StreamParams& q, int i) {
+// The shading half for queue entry i (slot `slot`): the hit through tp/montecarlo.frag:100-179
+// (the megakernel's shading block, variant montecarlo.frag).  A path that ends adds its result
+// to the unit's sum in pass order and the slot goes on with the unit's next pass, whose camera
+// ray is the cached primary hit (shaded at once, no traversal); a unit that ends writes its
+// sum and the slot takes the next unit.  Returns true with the next payload in `out` when the
+// slot's next ray must be traversed, false when the slot has no unit left.
+__device__ __forceinline__ bool stream_shade(const StreamParams& q, const Cols& Qi, uint32_t i, const SlotCols& Sl,
+                                             int slot, Payload& out) {
   const RenderParams& p = q.r;
   const SceneT<false, false> s{p.nodes, p.leaves, p.ptype, p.prims, p.depth, p.minfo, p.mnodes, p.mleaves,
                                p.mtris, p.mverts, p.mnorms, p.flat_face};
   Ev<false> ev;
   ev.init();
-  const SlotRef sl = slot_ref(q, (uint32_t)i);
-  uint32_t unit = sl.ldu(SF_UNIT);
-  UnitGeom g = unit_geom(p, unit);
-  const uint32_t sw = sl.ldu(SF_STATE);
+  const uint32_t sidx = (uint32_t)slot;
+  uint32_t unit = Qi.ldu(QF_UNIT, i);
+  const UnitGeom g = unit_geom(p, unit);
+  const uint32_t sw = Qi.ldu(QF_STATE, i);
   int bounce = (int)(sw & 255u);
   uint32_t phase = sw >> 8;
-  int pass = (int)sl.ldu(SF_PASS);
+  int pass = (int)Qi.ldu(QF_PASS, i);
   const int B = p.bounces;
   const f3 Ocam = mk(p.ox, p.oy, p.oz);
   Hit h;
-  h.pl = sl.ld3(SF_HX); h.code = (int)sl.ldu(SF_HCODE); h.dist = 0.0f; h.tri = 0; h.cull2 = 0.0;
-  f3 O, D, att, total, N = mk(0.0f, 0.0f, 0.0f), P = N;
+  h.pl = Qi.ld3(QF_HX, i); h.code = (int)Qi.ldu(QF_HCODE, i); h.dist = 0.0f; h.tri = 0; h.cull2 = 0.0;
+  f3 O = Qi.ld3(QF_OX, i), D = Qi.ld3(QF_DX, i), att, total, N = mk(0.0f, 0.0f, 0.0f), P = N;
   Rng rng;
   bool first = false;
-  f3 sum = sl.ld3(SF_SX);
+  const float u = ((float)g.x + 0.5f) / (float)p.W, v = ((float)g.y + 0.5f) / (float)p.H;
   if (phase == kPhasePrimary) {
     // the unit's camera-ray hit, computed once and reused by all its passes (exact: the camera
     // ray has no jitter and traversal / intersection_info draw no random numbers)
     const int key0 = hit_key(h);
     f3 N0 = mk(0.0f, 0.0f, 0.0f), P0 = N0;
     if (h.hit()) geom_info<false>(s, h, N0, P0, ev);
-    sl.set3(SF_N0X, N0); sl.set3(SF_P0X, P0); sl.setu(SF_KEY0, (uint32_t)key0);
+    Sl.set3(SF_N0X, sidx, N0); Sl.set3(SF_P0X, sidx, P0); Sl.setu(SF_KEY0, sidx, (uint32_t)key0);
     phase = 0;
     first = true;
     N = N0; P = P0;
     h.code = key0;
-  } else {
-    O = sl.ld3(SF_OX); D = sl.ld3(SF_DX);
-    att = sl.ld3(SF_AX); total = sl.ld3(SF_TX);
-    rng.x = sl.ldu(SF_RX); rng.y = sl.ldu(SF_RY); rng.z = sl.ldu(SF_RZ);
-  }
-  float u = ((float)g.x + 0.5f) / (float)p.W, v = ((float)g.y + 0.5f) / (float)p.H;
-  if (first) {   // pass `pass` of the unit starts
-    rng = seed_for(u, v, pass, p.date);
-    O = Ocam; D = camera_dir(p, u, v);
+    rng = seed_for(u, v, pass, p.date);   // pass `pass` of the unit starts (O, D: the camera ray)
     att = mk(0.8f, 0.8f, 0.8f); total = mk(0.0f, 0.0f, 0.0f);
     bounce = 0;
+  } else {
+    att = Qi.ld3(QF_AX, i); total = Qi.ld3(QF_TX, i);
+    rng.x = Qi.ldu(QF_RX, i); rng.y = Qi.ldu(QF_RY, i); rng.z = Qi.ldu(QF_RZ, i);
   }
   for (;;) {
     bool done = false;
@@ -1776,7 +1884,7 @@ __device__ __forceinline__ bool stream_shade(const StreamParams& q, int i) {
           }
           if (inner) {   // intersection_info leaves N, P untouched on a miss: kept for the inner hit
             phase = kPhaseInner;
-            sl.set3(SF_NSX, N); sl.set3(SF_PSX, P);
+            Sl.set3(SF_NSX, sidx, N); Sl.set3(SF_PSX, sidx, P);
           }
         }
       }
@@ -1785,7 +1893,7 @@ __device__ __forceinline__ bool stream_shade(const StreamParams& q, int i) {
       if (h.hit()) {
         geom_info<false>(s, h, N, P, ev);
       } else {
-        N = sl.ld3(SF_NSX); P = sl.ld3(SF_PSX);
+        N = Sl.ld3(SF_NSX, sidx); P = Sl.ld3(SF_PSX, sidx);
       }
       O = add(P, muls(N, kBIAS));
       D = grefract(D, neg(N), p.inv_ior);
@@ -1794,13 +1902,13 @@ __device__ __forceinline__ bool stream_shade(const StreamParams& q, int i) {
       if (bounce >= B) done = true;   // budget exhausted: black
     }
     if (!done) {   // the path goes on: its next ray is queued
-      sl.set3(SF_OX, O); sl.set3(SF_DX, D); sl.set3(SF_AX, att); sl.set3(SF_TX, total);
-      sl.setu(SF_RX, rng.x); sl.setu(SF_RY, rng.y); sl.setu(SF_RZ, rng.z);
-      sl.setu(SF_STATE, (uint32_t)bounce | (phase << 8));
-      sl.setu(SF_PASS, (uint32_t)pass);
-      sl.set3(SF_SX, sum);
+      out.O = O; out.D = D; out.att = att; out.total = total; out.rng = rng;
+      out.state = (uint32_t)bounce | (phase << 8);
+      out.pass = (uint32_t)pass;
+      out.unit = unit;
       return true;
     }
+    f3 sum = Sl.ld3(SF_SX, sidx);
     sum = mk(sum.x + res.x, sum.y + res.y, sum.z + res.z);
     pass++;
     if (pass >= g.pass_end) {   // the unit's sum: accumulator (one-segment launch) or its segment slot
@@ -1813,16 +1921,16 @@ __device__ __forceinline__ bool stream_shade(const StreamParams& q, int i) {
       }
       unit = atomicAdd(q.ctr + SC_UNIT, 1u);
       if (unit >= q.n_units) {
-        sl.setu(SF_STATE, kSlotDead);
+        atomicAdd(q.ctr + SC_DEAD, 1u);
         return false;
       }
-      stream_start_unit(p, sl, unit);
+      start_unit(p, Sl, slot, unit, out);
       return true;
     }
+    Sl.set3(SF_SX, sidx, sum);
     // the unit's next pass starts with the cached primary hit
-    const int key0 = (int)sl.ldu(SF_KEY0);
-    h.code = key0;
-    N = sl.ld3(SF_N0X); P = sl.ld3(SF_P0X);
+    h.code = (int)Sl.ldu(SF_KEY0, sidx);
+    N = Sl.ld3(SF_N0X, sidx); P = Sl.ld3(SF_P0X, sidx);
     first = true;
     phase = 0;
     rng = seed_for(u, v, pass, p.date);
@@ -1832,29 +1940,37 @@ __device__ __forceinline__ bool stream_shade(const StreamParams& q, int i) {
   }
 }
 
-__global__ __launch_bounds__(256, MCPT_MIN_WAVES_SHADE) void stream_shade_kernel(StreamParams q) {
+__global__ __launch_bounds__(kStreamBlock, MCPT_MIN_WAVES_SHADE) void stream_shade_kernel(StreamParams q) {
   const int par = q.parity;
   const unsigned n = q.ctr[SC_CNT + par];
-  if (blockIdx.x == 0 && threadIdx.x == 0) q.ctr[SC_FETCH + (par ^ 1)] = 0u;   // the next trace kernel's fetch counter
-  const int* in = q.queue[par];
-  int* out = q.queue[par ^ 1];
-  unsigned* cnt_out = q.ctr + SC_CNT + (par ^ 1);
-  const int lane = threadIdx.x & 63;
-  for (unsigned base = blockIdx.x * 256u; base < n; base += gridDim.x * 256u) {   // block-uniform
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    q.ctr[SC_FETCH + (par ^ 1)] = 0u;                // the next trace kernel's fetch counter
+    if (!q.compact) q.ctr[SC_CNT + (par ^ 1)] = n;   // in place: the same length
+  }
+  const Cols Qi = cols(q.queue[par], q.n_slots, QF_COUNT), Qo = cols(q.queue[par ^ 1], q.n_slots, QF_COUNT);
+  const SlotCols Sl = cols<0>(q.slots, q.n_slots, SF_COUNT);
+  __shared__ unsigned s_wc[kStreamWaves + 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (unsigned base = blockIdx.x * (unsigned)kStreamBlock; base < n; base += gridDim.x * (unsigned)kStreamBlock) {   // block-uniform
     const unsigned i = base + threadIdx.x;
-    int slot = -1;
-    bool push = false;
-    if (i < n) {
-      slot = in[i];
-      push = stream_shade(q, slot);
-    }
-    const uint64_t m = __ballot(push);
-    if (m) {
-      const int leader = __builtin_ffsll((long long)m) - 1;
-      unsigned b = 0;
-      if (lane == leader) b = atomicAdd(cnt_out, (unsigned)__builtin_popcountll(m));
-      b = (unsigned)__shfl((int)b, leader);
-      if (push) out[b + (unsigned)mbcnt64(m)] = slot;
+    const int slot = i < n ? (int)Qi.ldu(QF_SLOT, i) : -1;
+    Payload pl;
+    const bool cont = slot >= 0 && stream_shade(q, Qi, i, Sl, slot, pl);
+    if (!q.compact) {   // in place: entry i of the next queue (dead entries marked)
+      if (cont) put_payload(Qo, i, pl, slot);
+      else if (i < n) Qo.setu(QF_SLOT, i, 0xFFFFFFFFu);
+    } else {            // compaction: live entries appended (one atomic per block)
+      const uint64_t m = __ballot(cont);
+      if (lane == 0) s_wc[wave] = (unsigned)__builtin_popcountll(m);
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        unsigned t = 0;
+        for (int k = 0; k < kStreamWaves; ++k) { const unsigned c = s_wc[k]; s_wc[k] = t; t += c; }
+        s_wc[kStreamWaves] = t ? atomicAdd(q.ctr + SC_CNT + (par ^ 1), t) : 0u;
+      }
+      __syncthreads();
+      if (cont) put_payload(Qo, s_wc[kStreamWaves] + s_wc[wave] + (unsigned)mbcnt64(m), pl, slot);
+      __syncthreads();
     }
   }
 }
@@ -1987,11 +2103,30 @@ hipError_t mcpt_launch_stream_init(const mcpt::StreamParams& q, hipStream_t stre
   return hipGetLastError();
 }
 
-hipError_t mcpt_launch_stream_iter(const mcpt::StreamParams& q, int persistent_blocks, hipStream_t stream) {
-  dim3 block(256), grid((unsigned)persistent_blocks);
-  hipLaunchKernelGGL(mcpt::stream_trace_kernel, grid, block, 0, stream, q);
-  hipError_t e = hipGetLastError();
+int mcpt_stream_lds_nodes_bytes(int depth) {
+  return (3 * ((2 << depth) - 1)) * 16 + (1 << depth) * 4;
+}
+bool mcpt_stream_lds_nodes_fit(int depth) {
+  return depth <= 12 && mcpt_stream_lds_nodes_bytes(depth) + mcpt::kTraceLdsStaging <= 160 * 1024;
+}
+
+hipError_t mcpt_launch_stream_iter(const mcpt::StreamParams& q, int n_cu, bool lds_nodes, hipStream_t stream) {
+  hipError_t e;
+  if (lds_nodes) {
+    const size_t shm = (size_t)mcpt_stream_lds_nodes_bytes(q.r.depth);
+    // above the default 64 KiB of dynamic LDS (set on the calling thread's current device)
+    e = hipFuncSetAttribute((const void*)mcpt::stream_trace_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024 - mcpt::kTraceLdsStaging);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(mcpt::stream_trace_kernel<true>, dim3((unsigned)n_cu), dim3(mcpt::TraceCfg<true>::kBlock), shm,
+                       stream, q);
+  } else {
+    hipLaunchKernelGGL(mcpt::stream_trace_kernel<false>, dim3((unsigned)n_cu * 8), dim3(mcpt::kStreamBlock), 0, stream,
+                       q);
+  }
+  e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(mcpt::stream_shade_kernel, grid, block, 0, stream, q);
+  const unsigned persistent_blocks = (unsigned)n_cu * 8;
+  hipLaunchKernelGGL(mcpt::stream_shade_kernel, dim3(persistent_blocks), dim3(mcpt::kStreamBlock), 0, stream, q);
   return hipGetLastError();
 }

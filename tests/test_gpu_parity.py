@@ -450,16 +450,19 @@ def test_gather_rows_then_render_again(mcpt_mod):
         r.close()
 
 
-def test_auto_two_round_trials_settle(mcpt_mod, renderer):
+@pytest.mark.parametrize("scene_id,n_cand", [(6, 4), (8, 5)])
+def test_auto_two_round_trials_settle(mcpt_mod, renderer, scene_id, n_cand):
     """AUTO times each applicable candidate twice (candidate order, then reverse) on launches of
     one shape and then settles (mcpt_get_schedule reports it); mcpt.AUTO_TRIALS launches are
-    enough; the image equals a fixed per-lane render of the same launches."""
-    W, H, S = 1920, 1080, 256   # 8 pass segments: all four candidates apply
+    enough; the image equals a fixed per-lane render of the same launches.  Candidates: per-lane,
+    wave-coherent, per-lane with 2 and 4 segments per item, and (BVH depth >= 8: scene 8) the
+    stream schedule."""
+    W, H, S = 1920, 1080, 256   # 8 pass segments: the segment-group candidates apply
     ipv, iv = mcpt_mod.camera_canonical(W, H)
 
     def run(mode, n):
         renderer.set_traversal(mode)
-        renderer.upload_scene(mcpt_mod.Scene.reference(6))
+        renderer.upload_scene(mcpt_mod.Scene.reference(scene_id))
         renderer.set_target(W, H)
         sched = []
         for k in range(n):
@@ -468,10 +471,15 @@ def test_auto_two_round_trials_settle(mcpt_mod, renderer):
         acc, cnt = renderer.read_accum()
         return acc, cnt, sched
 
+    assert mcpt_mod.AUTO_TRIALS >= 2 * n_cand
     auto, n_a, sched = run(0, mcpt_mod.AUTO_TRIALS + 1)
-    assert not any(s["settled"] for s in sched[:mcpt_mod.AUTO_TRIALS - 1]), sched
-    assert sched[-1]["settled"] and sched[-1]["seg_per_item"] in (1, 2, 4), sched
-    assert sched[-1]["traversal"] in ("lane", "wave")
+    # a trial's time is collected when the next launch starts: settled after 2 * n_cand + 1
+    assert not any(s["settled"] for s in sched[:2 * n_cand]), sched
+    assert all(s["settled"] for s in sched[2 * n_cand:]), sched
+    assert sched[-1]["seg_per_item"] in (1, 2, 4), sched
+    assert sched[-1]["traversal"] in (("lane", "wave", "stream") if n_cand == 5 else ("lane", "wave"))
+    if n_cand == 5:
+        assert "stream" in {s["traversal"] for s in sched[:2 * n_cand]}, sched   # it was tried
     lane, n_l, fixed = run(1, mcpt_mod.AUTO_TRIALS + 1)
     renderer.set_traversal(0)
     assert all(s["settled"] and s["traversal"] == "lane" for s in fixed)

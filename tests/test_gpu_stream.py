@@ -122,3 +122,15 @@ def test_stream_falls_back_where_it_does_not_apply(mcpt_mod, oracle_mod, rendere
         ref = _oracle(oracle_mod, sc, 24, 16, 1, 2, B, variant=variant)
         assert it == 0
         assert np.array_equal(_bits(gpu), _bits(ref.reshape(gpu.shape)))
+
+
+@pytest.mark.parametrize("scene_id,B", [(8, 12), (3, 8)])
+def test_stream_lds_nodes_variant(mcpt_mod, oracle_mod, renderer, monkeypatch, scene_id, B):
+    """The trace kernel with the BVH nodes staged in LDS (MCPT_STREAM_LDS_NODES=1, off by
+    default) gives the same bits."""
+    monkeypatch.setenv("MCPT_STREAM_LDS_NODES", "1")
+    sc = mcpt_mod.Scene.reference(scene_id)
+    gpu, it = _render(mcpt_mod, renderer, sc, 40, 24, 20, 50, B, slots=300)
+    ref = _oracle(oracle_mod, sc, 40, 24, 20, 50, B)
+    assert it > 0
+    assert np.array_equal(_bits(gpu), _bits(ref.reshape(gpu.shape)))

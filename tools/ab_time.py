@@ -50,7 +50,9 @@ def main():
                 r.render(ipv, iv, 1 + (k + 1) * a.spp, a.spp, 0.0, B, 1.0, 0)
                 ms.append(r.last_kernel_ms()[0])
             t = float(np.mean(ms))
+            extra = {"stream_iterations": r.stream_iterations()} if mode == 3 else {}
             print(json.dumps({"lib": a.tag, "scene": sid, "mode": mode, "walk_exit": wx, "bounces": B, "spp": a.spp,
+                              **extra,
                               "kernel_ms": round(t, 3),
                               "msamples_s": round(a.width * a.height * a.spp / t / 1e3, 1)}), flush=True)
     r.close()
