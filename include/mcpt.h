@@ -199,8 +199,8 @@ int mcpt_get_schedule(mcpt_ctx* ctx, int* traversal, int* seg_per_item, int* set
 int mcpt_set_walk_exit(mcpt_ctx* ctx, int lanes);
 int mcpt_get_walk_exit(mcpt_ctx* ctx, int* resolved_lanes);
 
-/* Stream schedule (MCPT_TRAVERSAL_STREAM) knobs: path slots of the pool (0 = default 4 Mi;
- * never more than the launch's (pixel, pass segment) units; 160 B of device state per slot)
+/* Stream schedule (MCPT_TRAVERSAL_STREAM) knobs: path slots (0 = default 16 Mi; never more than
+ * the launch's (pixel, pass segment) units; 248 B of device memory per slot, in two pools)
  * and the trace kernel's refill threshold (a wave takes new rays for its idle lanes once at
  * most `refill` lanes still walk; 0 = only when all are done; -1 = default 56).  Same results
  * for every value.  mcpt_stream_iterations: trace + shade iterations of the last stream launch

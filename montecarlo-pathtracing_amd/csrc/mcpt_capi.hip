@@ -97,10 +97,12 @@ struct mcpt_ctx {
   int n_cu = 0;                     // compute units of the device (persistent grids)
   float* d_slots = nullptr;         // SF_COUNT x slot capacity
   float* d_queue = nullptr;         // 2 x QF_COUNT x slot capacity
-  unsigned* d_sctr = nullptr;       // SC_COUNT counters
-  int slot_cap = 0;
-  unsigned* h_sctr = nullptr;       // pinned: the counters read back after each batch (2 x SC_COUNT)
+  unsigned* d_sctr = nullptr;       // SC_COUNT counters per pool
+  long long slot_cap = 0;           // slots of d_slots / d_queue
+  unsigned* h_sctr = nullptr;       // pinned: each pool's counters read back after each batch (2 x pools x SC_COUNT)
   hipEvent_t batch_ev[2] = {nullptr, nullptr};
+  hipStream_t pool_stream[2] = {nullptr, nullptr};   // the pools' iterations overlap on two streams
+  hipEvent_t pool_ev[3] = {nullptr, nullptr, nullptr};   // fork / join of the pool streams
   int stream_slots = 0;             // MCPT_STREAM_SLOTS env / mcpt_set_stream_pool (0: default)
   int stream_refill = -1;           // MCPT_STREAM_REFILL env / mcpt_set_stream_pool (-1: default)
   long long stream_iters = 0;       // iterations of the last stream render (diagnostics)
@@ -306,6 +308,8 @@ int mcpt_destroy(mcpt_ctx* c) {
   (void)hipFree(c->d_sctr);
   if (c->h_sctr) (void)hipHostFree(c->h_sctr);
   for (hipEvent_t e : c->batch_ev) if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->pool_ev) if (e) (void)hipEventDestroy(e);
+  for (hipStream_t st : c->pool_stream) if (st) (void)hipStreamDestroy(st);
   for (hipEvent_t e : c->evs) (void)hipEventDestroy(e);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
@@ -586,10 +590,12 @@ static void corner_rays(const float* invPV, const float* invV, mcpt::RenderParam
   }
 }
 
-// stream schedule defaults: 4 Mi path slots (92 B of queue payload x 2 + 64 B of unit data
-// each: 1 GB) keep every trace kernel of an iteration long against its tail (the last walks
-// of the iteration); a wave refills its idle lanes once 8 of them have finished their walks
-constexpr int kStreamSlotsDefault = 1 << 22;
+// stream schedule defaults: 16 Mi path slots (2 x 92 B of queue payload + 64 B of unit data
+// each: 4 GB) keep the iterations few and every trace kernel long against its tail (the last
+// walks of the iteration): scene 8, 512 spp, 1080p (33 M units): 4 Mi slots 1,344 iterations
+// 447 Msamples/s, 8 Mi 792 / 472, 12 Mi 624 / 482, 16 Mi 512 / 484, 32 Mi 352 / 478 (the
+// units' own tail grows); a wave refills its idle lanes once 8 of them have finished their walks
+constexpr int kStreamSlotsDefault = 1 << 24;
 constexpr int kStreamRefillDefault = 56;
 constexpr int kStreamBatch = 8;   // iterations issued between two reads of the counters
 // the shade kernel compacts its output (drops dead entries) once fewer than this share of the
@@ -600,18 +606,30 @@ static bool stream_applies(const mcpt_ctx* c, int variant, int bounces, bool cou
   return !count && variant == 0 && bounces > 0 && c->n_meshes == 0;
 }
 
-// One sub-launch (one pass range of <= max_seg segments) with the stream schedule: slots set up,
-// then iterations (trace + shade) in batches until every slot has run out of units.  The host
-// reads the counters of batch b-1 while batch b runs, so the device never waits for the host.
+// path-slot pools of a launch: each runs its own iterations on its own stream, so one pool's
+// shade kernel and trace-kernel tail overlap the other pool's trace kernel
+constexpr int kStreamPools = 2;
+
+// One sub-launch (one pass range of <= max_seg segments) with the stream schedule: the slots of
+// every pool set up, then iterations (trace + shade) in batches until every slot has run out of
+// units.  The host reads the counters of batch b-1 while batch b runs, so the device never waits
+// for the host.
 static int stream_run(mcpt_ctx* c, const mcpt::RenderParams& p) {
   const unsigned long long n_units = (unsigned long long)p.n_local_px * (unsigned long long)p.n_segments;
   if (n_units == 0) return MCPT_OK;
   if (n_units >= (1ULL << 31) || p.n_local_px >= (1LL << 31))
     return set_err(MCPT_ERR_INVALID_ARG, "stream schedule: too many units in one launch");
-  // the kernels address a queue / the slot data through one buffer resource: below 2 GiB each
-  const int max_slots = (int)(((1ULL << 31) - 1) / (mcpt::QF_COUNT * sizeof(float)));
-  const int want = std::min(c->stream_slots > 0 ? c->stream_slots : kStreamSlotsDefault, max_slots);
-  const int n_slots = (int)std::min<unsigned long long>(n_units, (unsigned long long)want);
+  // the kernels address a pool's queue / slot data through one buffer resource: below 2 GiB each
+  const int max_pool = (int)(((1ULL << 31) - 1) / (mcpt::QF_COUNT * sizeof(float)));
+  const int n_pools = (int)std::max(1, std::min(env_int("MCPT_STREAM_POOLS", kStreamPools), kStreamPools));
+  const long long want = c->stream_slots > 0 ? c->stream_slots : kStreamSlotsDefault;
+  const long long n_slots = std::min<long long>((long long)n_units, std::min<long long>(want, (long long)max_pool * n_pools));
+  int pool_n[kStreamPools] = {0, 0};
+  int np = 0;
+  for (int k = 0; k < n_pools; ++k) {
+    pool_n[k] = (int)(n_slots / n_pools + (k < n_slots % n_pools ? 1 : 0));
+    if (pool_n[k] > 0) np = k + 1;
+  }
   if (n_slots > c->slot_cap) {
     HIP_OR_RETURN(hipStreamSynchronize(c->stream));
     (void)hipFree(c->d_slots); (void)hipFree(c->d_queue);
@@ -620,57 +638,96 @@ static int stream_run(mcpt_ctx* c, const mcpt::RenderParams& p) {
     HIP_OR_RETURN(hipMalloc(&c->d_queue, (size_t)2 * mcpt::QF_COUNT * n_slots * sizeof(float)));
     c->slot_cap = n_slots;
   }
-  if (!c->d_sctr) HIP_OR_RETURN(hipMalloc(&c->d_sctr, mcpt::SC_COUNT * sizeof(unsigned)));
-  if (!c->h_sctr) HIP_OR_RETURN(hipHostMalloc(&c->h_sctr, 2 * mcpt::SC_COUNT * sizeof(unsigned), hipHostMallocDefault));
+  if (!c->d_sctr) HIP_OR_RETURN(hipMalloc(&c->d_sctr, kStreamPools * mcpt::SC_COUNT * sizeof(unsigned)));
+  if (!c->h_sctr)
+    HIP_OR_RETURN(hipHostMalloc(&c->h_sctr, 2 * kStreamPools * mcpt::SC_COUNT * sizeof(unsigned), hipHostMallocDefault));
   for (hipEvent_t& e : c->batch_ev)
     if (!e) HIP_OR_RETURN(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  mcpt::StreamParams q;
-  q.r = p;
-  q.slots = c->d_slots;
-  // field f of entry i at queue[par][f * n_slots + i]: laid out for this launch's slot count
-  q.queue[0] = c->d_queue;
-  q.queue[1] = c->d_queue + (size_t)mcpt::QF_COUNT * n_slots;
-  q.ctr = c->d_sctr;
-  q.n_slots = n_slots;
-  q.n_units = (unsigned)n_units;
-  q.parity = 0;
-  q.refill = c->stream_refill >= 0 ? c->stream_refill : kStreamRefillDefault;
-  q.compact = 0;
-  HIP_OR_RETURN(mcpt_launch_stream_init(q, c->stream));
-  const unsigned n0 = (unsigned)n_slots;   // slots that start with a unit (n_slots <= n_units)
-  // every iteration advances each live slot by one traversal; a unit needs at most
-  // (passes) x (2 B + 1) + 1 of them, and a slot runs ceil(units / slots) units
-  const long long per_unit = (long long)mcpt::kPassChunk * (2LL * p.bounces + 1) + 1;
-  const long long cap = ((long long)((n_units + n_slots - 1) / n_slots) + 1) * per_unit + 4 * kStreamBatch;
+  for (hipEvent_t& e : c->pool_ev)
+    if (!e) HIP_OR_RETURN(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  for (hipStream_t& st : c->pool_stream)
+    if (!st) HIP_OR_RETURN(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
   // BVH nodes in the trace kernel's LDS where they fit (MCPT_STREAM_LDS_NODES=1): off by default,
   // no faster on scenes 3/7/8 (random lanes' node reads conflict in the LDS banks, 11 conflict
   // cycles per LDS instruction; gpurun_out r03e/r03f)
   const bool lds_nodes = env_int("MCPT_STREAM_LDS_NODES", 0) != 0 && mcpt_stream_lds_nodes_fit(p.depth);
-  // leaf batching of the trace kernel's walks: 16 lanes (8 for the megakernel; scene 8: 16 is
-  // +4 % over 8 and 32, 4 is -8 %)
-  if (c->leaf_batch < 0) q.r.leaf_batch = 16;
+  mcpt::StreamParams q[kStreamPools];
+  unsigned* unit_ctr = c->d_sctr + mcpt::SC_UNIT;   // pool 0's slot: shared
+  {
+    const unsigned first_free = (unsigned)n_slots;   // units 0 .. n_slots-1 start in the pools' slots
+    HIP_OR_RETURN(hipMemcpyAsync(unit_ctr, &first_free, sizeof(unsigned), hipMemcpyHostToDevice, c->stream));
+  }
+  size_t slot_off = 0, queue_off = 0;
+  int unit_base = 0;
+  for (int k = 0; k < np; ++k) {
+    mcpt::StreamParams& s = q[k];
+    s.r = p;
+    // leaf batching of the trace kernel's walks: 16 lanes (8 for the megakernel; scene 8: 16 is
+    // +4 % over 8 and 32, 4 is -8 %)
+    if (c->leaf_batch < 0) s.r.leaf_batch = 16;
+    // field f of pool entry i at queue[par][f * n + i], slot data likewise: laid out per pool
+    s.slots = c->d_slots + slot_off;
+    s.queue[0] = c->d_queue + queue_off;
+    s.queue[1] = s.queue[0] + (size_t)mcpt::QF_COUNT * pool_n[k];
+    s.ctr = c->d_sctr + k * mcpt::SC_COUNT;
+    s.unit_ctr = unit_ctr;
+    s.n_slots = pool_n[k];
+    s.unit_base = unit_base;
+    s.n_units = (unsigned)n_units;
+    s.parity = 0;
+    s.refill = c->stream_refill >= 0 ? c->stream_refill : kStreamRefillDefault;
+    s.compact = 0;
+    slot_off += (size_t)mcpt::SF_COUNT * pool_n[k];
+    queue_off += (size_t)2 * mcpt::QF_COUNT * pool_n[k];
+    unit_base += pool_n[k];
+    HIP_OR_RETURN(mcpt_launch_stream_init(s, c->stream));
+  }
+  // fork: the pool streams start after the set-up (and everything before it) on the context's stream
+  HIP_OR_RETURN(hipEventRecord(c->pool_ev[2], c->stream));
+  for (int k = 0; k < np; ++k) HIP_OR_RETURN(hipStreamWaitEvent(c->pool_stream[k], c->pool_ev[2], 0));
+  // every iteration advances each live slot by one traversal; a unit needs at most
+  // (passes) x (2 B + 1) + 1 of them, and a slot runs ceil(units / slots) units
+  const long long per_unit = (long long)mcpt::kPassChunk * (2LL * p.bounces + 1) + 1;
+  const long long min_pool = pool_n[np - 1];
+  const long long cap = ((long long)(n_units / min_pool) + 2) * per_unit + 4 * kStreamBatch;
   long long it = 0;
-  bool compact = false;
+  bool compact[kStreamPools] = {false, false}, done[kStreamPools] = {false, false};
   for (int b = 0;; ++b) {
-    for (int k = 0; k < kStreamBatch; ++k, ++it) {
-      q.parity = (int)(it & 1);
-      q.compact = (k == 0 && compact) ? 1 : 0;
-      HIP_OR_RETURN(mcpt_launch_stream_iter(q, c->n_cu, lds_nodes, c->stream));
+    for (int k = 0; k < kStreamBatch; ++k, ++it)
+      for (int j = 0; j < np; ++j) {
+        if (done[j]) continue;
+        q[j].parity = (int)(it & 1);
+        q[j].compact = (k == 0 && compact[j]) ? 1 : 0;
+        HIP_OR_RETURN(mcpt_launch_stream_iter(q[j], c->n_cu, lds_nodes, c->pool_stream[j]));
+      }
+    // every pool's counters after the batch, read on pool 0's stream once all pools are there
+    for (int j = 1; j < np; ++j) {
+      HIP_OR_RETURN(hipEventRecord(c->pool_ev[j], c->pool_stream[j]));
+      HIP_OR_RETURN(hipStreamWaitEvent(c->pool_stream[0], c->pool_ev[j], 0));
     }
-    unsigned* h = c->h_sctr + (b & 1) * mcpt::SC_COUNT;
-    HIP_OR_RETURN(hipMemcpyAsync(h, c->d_sctr, mcpt::SC_COUNT * sizeof(unsigned), hipMemcpyDeviceToHost, c->stream));
-    HIP_OR_RETURN(hipEventRecord(c->batch_ev[b & 1], c->stream));
+    unsigned* h = c->h_sctr + (b & 1) * kStreamPools * mcpt::SC_COUNT;
+    HIP_OR_RETURN(hipMemcpyAsync(h, c->d_sctr, (size_t)np * mcpt::SC_COUNT * sizeof(unsigned), hipMemcpyDeviceToHost,
+                                 c->pool_stream[0]));
+    HIP_OR_RETURN(hipEventRecord(c->batch_ev[b & 1], c->pool_stream[0]));
     if (b >= 1) {
       HIP_OR_RETURN(hipEventSynchronize(c->batch_ev[(b - 1) & 1]));
-      const unsigned* hp = c->h_sctr + ((b - 1) & 1) * mcpt::SC_COUNT;
-      const unsigned dead = hp[mcpt::SC_DEAD];
-      if (dead >= n0) break;   // every slot was done by the end of batch b-1
-      // the queue length the iteration after batch b-1 read (in place: unchanged until compacted)
-      const unsigned len = hp[mcpt::SC_CNT + (int)((it - kStreamBatch) & 1)];
-      compact = (double)(n0 - dead) < kStreamCompactBelow * (double)len;
+      bool all = true;
+      for (int j = 0; j < np; ++j) {
+        const unsigned* hp = c->h_sctr + ((b - 1) & 1) * kStreamPools * mcpt::SC_COUNT + j * mcpt::SC_COUNT;
+        const unsigned dead = hp[mcpt::SC_DEAD];
+        done[j] = dead >= (unsigned)pool_n[j];   // every slot of the pool was done by the end of batch b-1
+        all = all && done[j];
+        // the queue length the iteration after batch b-1 read (in place: unchanged until compacted)
+        const unsigned len = hp[mcpt::SC_CNT + (int)((it - kStreamBatch) & 1)];
+        compact[j] = !done[j] && (double)(pool_n[j] - dead) < kStreamCompactBelow * (double)len;
+      }
+      if (all) break;
     }
     if (it > cap) return set_err(MCPT_ERR_HIP, "stream schedule did not drain its queue");
   }
+  // join: the context's stream (the combine kernel, the caller's next work) waits for the pools
+  HIP_OR_RETURN(hipEventRecord(c->pool_ev[0], c->pool_stream[0]));
+  HIP_OR_RETURN(hipStreamWaitEvent(c->stream, c->pool_ev[0], 0));
   c->stream_iters += it;
   return MCPT_OK;
 }

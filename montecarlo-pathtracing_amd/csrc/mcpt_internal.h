@@ -111,14 +111,17 @@ enum SlotField {
   SF_NSX, SF_NSY, SF_NSZ, SF_PSX, SF_PSY, SF_PSZ,            // N, P kept across an inner walk
   SF_COUNT
 };
-// ctr[]: queue lengths [0..1], trace-kernel fetch counters [2..3], next unit [4], dead slots [5]
+// ctr[]: queue lengths [0..1], trace-kernel fetch counters [2..3], dead slots [5] of one pool;
+// the next unit [4] of the first pool's counters is shared by all pools (StreamParams::unit_ctr)
 enum { SC_CNT = 0, SC_FETCH = 2, SC_UNIT = 4, SC_DEAD = 5, SC_COUNT = 8 };
 struct StreamParams {
   RenderParams r;               // scene, target, the sub-launch's pass range and constants
   float* slots;                 // SF_COUNT x n_slots
   float* queue[2];              // QF_COUNT x n_slots each (ping-pong by parity)
-  unsigned* ctr;                // SC_* counters
-  int n_slots;
+  unsigned* ctr;                // SC_* counters of this pool
+  unsigned* unit_ctr;           // next unit, shared by the pools of a launch
+  int n_slots;                  // this pool's slots
+  int unit_base;                // this pool's slots start with units unit_base, unit_base + 1, ...
   unsigned n_units;             // n_segments x n_local_px
   int parity;                   // iteration & 1: queue[parity] is this iteration's input
   int refill;                   // trace kernel: refill a wave's idle lanes once <= this many still walk

@@ -1627,22 +1627,21 @@ __device__ __forceinline__ void start_unit(const RenderParams& p, const SlotCols
   S.set3(SF_SX, (uint32_t)slot, mk(0.0f, 0.0f, 0.0f));
 }
 
+// the pool's slot i starts unit unit_base + i (the host sizes the pools so that every slot has one)
 __global__ __launch_bounds__(256) void stream_init_kernel(StreamParams q) {
   const int i = blockIdx.x * 256 + threadIdx.x;
-  const unsigned n0 = (unsigned)q.n_slots < q.n_units ? (unsigned)q.n_slots : q.n_units;
   if (i == 0) {
-    q.ctr[SC_CNT] = n0;
+    q.ctr[SC_CNT] = (unsigned)q.n_slots;
     q.ctr[SC_CNT + 1] = 0u;
     q.ctr[SC_FETCH] = 0u;
     q.ctr[SC_FETCH + 1] = 0u;
-    q.ctr[SC_UNIT] = n0;
     q.ctr[SC_DEAD] = 0u;
   }
-  if ((unsigned)i >= n0) return;
+  if (i >= q.n_slots) return;
   const Cols Q = cols(q.queue[0], q.n_slots, QF_COUNT);
   const SlotCols S = cols<0>(q.slots, q.n_slots, SF_COUNT);
   Payload pl;
-  start_unit(q.r, S, i, (uint32_t)i, pl);
+  start_unit(q.r, S, i, (uint32_t)(q.unit_base + i), pl);
   put_payload(Q, (uint32_t)i, pl, i);
 }
 
@@ -1919,7 +1918,7 @@ __device__ __forceinline__ bool stream_shade(const StreamParams& q, const Cols& 
         float* part = p.partial + ((size_t)g.seg * p.n_local_px + g.px) * 3;
         part[0] = sum.x; part[1] = sum.y; part[2] = sum.z;
       }
-      unit = atomicAdd(q.ctr + SC_UNIT, 1u);
+      unit = atomicAdd(q.unit_ctr, 1u);
       if (unit >= q.n_units) {
         atomicAdd(q.ctr + SC_DEAD, 1u);
         return false;
