@@ -367,6 +367,8 @@ class Renderer {
     check(mcpt_gather_rows(c_, h.data(), (int)h.size()), "mcpt_gather_rows");
   }
   void set_traversal(int mode) { check(mcpt_set_traversal(c_, mode), "mcpt_set_traversal"); }
+  // stream schedule knobs (MCPT_TRAVERSAL_STREAM): path slots (0: default), refill threshold (-1: default)
+  void set_stream_pool(int slots, int refill) { check(mcpt_set_stream_pool(c_, slots, refill), "mcpt_set_stream_pool"); }
   int width() const { return W_; }
   int height() const { return H_; }
   mcpt_ctx* handle() const { return c_; }

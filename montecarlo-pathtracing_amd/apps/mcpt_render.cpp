@@ -55,7 +55,7 @@ void usage() {
                "usage: mcpt_render [--scene 1..8] [--width W] [--height H] [--subsampling k]\n"
                "                   [--spp S] [--first-pass P] [--chunk C] [--bounces B] [--ior R]\n"
                "                   [--light L] [--date T] [--variant montecarlo|mat|mat_tr]\n"
-               "                   [--traversal auto|lane|wave] [--device D | --devices D0,D1,...]\n"
+               "                   [--traversal auto|lane|wave|stream] [--device D | --devices D0,D1,...]\n"
                "                   [--out img.png] [--pfm img.pfm]\n");
 }
 
@@ -88,7 +88,10 @@ bool parse(int argc, char** argv, Args& a) {
       if (s != "mat" && s != "mat_tr" && s != "montecarlo") return false;
     } else if (k == "--traversal") {
       const std::string s = v;
-      a.traversal = s == "lane" ? MCPT_TRAVERSAL_LANE : (s == "wave" ? MCPT_TRAVERSAL_WAVE : MCPT_TRAVERSAL_AUTO);
+      a.traversal = s == "lane"     ? MCPT_TRAVERSAL_LANE
+                    : s == "wave"   ? MCPT_TRAVERSAL_WAVE
+                    : s == "stream" ? MCPT_TRAVERSAL_STREAM
+                                    : MCPT_TRAVERSAL_AUTO;
     } else {
       return false;
     }

@@ -126,6 +126,26 @@ def test_headless_app_matches_oracle(oracle_mod, tmp_path):
 
 
 @pytest.mark.gpu
+def test_headless_app_stream_schedule_multi_device(oracle_mod, tmp_path):
+    """mcpt_render --traversal stream on scene 8 with two shard contexts (each runs its own slot
+    pools and streams; the shards' host threads share cuda:0): bit-equal to the oracle."""
+    app = os.path.join(REPO, "montecarlo-pathtracing_amd", "bin", "mcpt_render")
+    W, H, S, B = 40, 32, 5, 12
+    pfm = str(tmp_path / "s8.pfm")
+    r = subprocess.run([app, "--scene", "8", "--width", str(W), "--height", str(H), "--spp", str(S), "--chunk", "2",
+                        "--bounces", str(B), "--traversal", "stream", "--devices", "0,0", "--pfm", pfm],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    img = read_pfm(pfm)
+    prims, nodes, leaves, d, _ = oracle_mod.scene(8)
+    ipv, iv = oracle_mod.camera(W, H)
+    acc = np.zeros((H, W, 3), np.float32)
+    for first, n in ((1, 2), (3, 2), (5, 1)):
+        oracle_mod.render(prims, nodes, leaves, d, ipv, iv, W, H, first, n, 0.0, B, 1.0, 0, accum=acc)
+    assert np.array_equal(img.view(np.uint32), (acc / np.float32(S)).view(np.uint32))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("devices", ["0,0", "0,0,0", "0,0,0,0,0,0,0,0"])
 def test_headless_app_multi_device_bit_equal(oracle_mod, tmp_path, devices):
     """mcpt_render --devices: one host thread per shard context (here all on cuda:0), balanced
