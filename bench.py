@@ -370,17 +370,23 @@ def self_check(args, scene, ipv, iv, frame: torch.Tensor, n_calls: int, S: int, 
     return {"rows": len(rows), "passes": int(n), "bit_equal": diff == 0, "channels_differing": diff}
 
 
-def roofline(workload: str, sha: str, avg_trace_ms: float, ref_bytes: float, bytes_per_sample: float, world: int):
+def roofline(workload: str, sha: str, avg_trace_ms: float, ref_bytes: float, bytes_per_sample: float, world: int,
+             launches: int = 1):
+    """`avg_trace_ms` is one timed call's kernel time, summed over its `launches` sub-launches; a
+    PMC record is used only if it sums the same number of launches."""
     rec = pmc_record(workload, sha) if world == 1 else None
+    if rec is not None and int(rec.get("launches_summed", 1)) != int(launches):
+        rec = None
     t_s = avg_trace_ms / 1e3
     roof = {"bound": "valu", "achieved": None, "peak": VALU_PEAK_T, "unit": "T lane-instr/s", "frac": None,
             "lane_utilisation": None, "useful_frac": None, "traffic": None,
             "hbm": {"achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None},
-            "kernel_ms": round(avg_trace_ms, 3),
+            "kernel_ms": round(avg_trace_ms, 3), "launches_per_call": launches,
             "pmc": {"workload": workload, "lib_sha256": sha, "matched": rec is not None,
                     "source": rec.get("source") if rec else None,
                     "note": None if rec else ("no rocprofv3 PMC record of this workload for this libmcpt.so "
-                                              "build (profiles/pmc_records.json): PMC fields left null"
+                                              "build (summing this call's launches) in profiles/pmc_records.json: "
+                                              "PMC fields left null"
                                               if world == 1 else "PMC records are single-GPU measurements")}}
     if rec is not None and t_s > 0:
         c = rec["counters_per_launch"]
@@ -437,10 +443,11 @@ def run_point(args, sr, rough, S, world, barrier, stat_dev):
         frame = sr.gather()
         e1.record(stream)
         gather_ev.append((e0, e1))
-        kernel_ms.append(sr.r.last_kernel_ms())   # HIP events of this launch (waits for its stop event)
+        kernel_ms.append(sr.r.last_kernel_ms())   # HIP events of this call's launches (waits for the last)
     barrier()
     elapsed = time.perf_counter() - t0
     sched = sr.r.schedule()   # what AUTO picked for this rank's timed launches
+    launches = sr.r.last_launch_count()   # sub-launches of one timed call (segment-sum budget)
     t = torch.tensor([elapsed], dtype=torch.float64, device=stat_dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -465,7 +472,7 @@ def run_point(args, sr, rough, S, world, barrier, stat_dev):
     check = None
     if args.rank == 0 and not args.no_check:
         check = self_check(args, scene, ipv, iv, frame, args.warmup + args.steps, S, args.local_rank)
-    return dict(rough=rough, elapsed=elapsed, sched=sched, gather_ms=gather_ms, avg_trace_ms=avg_trace_ms,
+    return dict(rough=rough, elapsed=elapsed, sched=sched, launches=launches, gather_ms=gather_ms, avg_trace_ms=avg_trace_ms,
                 avg_combine_ms=avg_combine_ms, allstats=allstats, check=check)
 
 
@@ -521,7 +528,7 @@ def main():
         for pt in points:
             a = pt["allstats"]
             pt["roof"] = roofline(workload_key(args, S, pt["rough"]), sha, pt["avg_trace_ms"], float(a[0, 0]),
-                                  float(a[:, 0].sum() / max(a[:, 3].sum(), 1.0)), world)
+                                  float(a[:, 0].sum() / max(a[:, 3].sum(), 1.0)), world, pt["launches"])
         config = {
             "workload": workload_key(args, S, main_pt["rough"] if len(points) == 1 else None)
                         + ("_rough-sweep" if len(points) > 1 else ""),

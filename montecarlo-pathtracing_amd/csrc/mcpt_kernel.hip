@@ -1773,6 +1773,21 @@ __global__ __launch_bounds__(TraceCfg<LDSN>::kBlock, TraceCfg<LDSN>::kMinWaves) 
       }
     }
   }
+#ifdef MCPT_STAMPS
+  // diagnostic build (tools/stamps.py --stream): the walk loop's iterations and lane counts of
+  // this wave's whole life, summed over the wave's lanes (walk_run's counters), into the debug slots
+  {
+    unsigned long long v[7] = {ev.st_lit, ev.st_wit, ev.st_nl, ev.st_nw, ev.st_ll, ev.st_lw, ev.st_leaf};
+    for (int off = 32; off > 0; off >>= 1)
+      for (int k = 0; k < 6; ++k) v[k] += __shfl_xor(v[k], off);
+    for (int off = 32; off > 0; off >>= 1) { const unsigned long long o = __shfl_xor(v[6], off); v[6] = v[6] > o ? v[6] : o; }
+    if (lane == 0 && p.events) {
+      for (int k = 0; k < 6; ++k) atomicAdd(p.events + 9 + k, v[k]);
+      atomicAdd(p.events + 7, v[6]);
+      atomicAdd(p.events + 6, 1ull);
+    }
+  }
+#endif
 }
 
 // The shading half for queue entry i (slot `slot`): the hit through tp/montecarlo.frag:100-179

@@ -14,7 +14,8 @@
 #     --spp N         passes per timed launch (default 256)
 #     --reps R        timed launches per (candidate, K, scene) (default 3)
 #     --k "1 2 4"     pass segments per work item (MCPT_SEG_PER_ITEM), interleaving loop (default "2")
-#     --modes "1"     traversal modes (1 per-lane, 2 wave-coherent; default "1")
+#     --modes "1"     traversal modes (1 per-lane, 2 wave-coherent, 3 stream; default "1")
+#     --walk-exit "16 32"  per-lane walks' suspension thresholds to time (default: the library's)
 #     --parity        run the parity suites (tests/test_gpu_parity.py, test_gpu_paths.py) on every
 #                     candidate first; stop at the first failure
 #     --stamps        also run tools/stamps.py with the stamps variant library (diagnostic build)
@@ -22,7 +23,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 TAG=$1; shift
-SCENES="6 8"; SPP=256; REPS=3; KS="2"; MODES="1"; PARITY=0; STAMPS=0
+SCENES="6 8"; SPP=256; REPS=3; KS="2"; MODES="1"; PARITY=0; STAMPS=0; WX="-1"
 while [ $# -gt 0 ]; do
   case "$1" in
     --scenes) SCENES=$2; shift 2 ;;
@@ -30,6 +31,7 @@ while [ $# -gt 0 ]; do
     --reps) REPS=$2; shift 2 ;;
     --k) KS=$2; shift 2 ;;
     --modes) MODES=$2; shift 2 ;;
+    --walk-exit) WX=$2; shift 2 ;;
     --parity) PARITY=1; shift ;;
     --stamps) STAMPS=1; shift ;;
     *) break ;;
@@ -63,7 +65,7 @@ fi
 for k in $KS; do
   for c in "$@"; do
     with_cand "$c" env MCPT_SEG_PER_ITEM=$k timeout -k 10 300 python tools/ab_time.py --scenes $SCENES \
-      --modes $MODES --spp $SPP --reps $REPS --tag "${c}_K$k" >> $O/ab.jsonl 2>> $O/ab.err || exit $?
+      --modes $MODES --spp $SPP --reps $REPS --walk-exit $WX --tag "${c}_K$k" >> $O/ab.jsonl 2>> $O/ab.err || exit $?
   done
 done
 cat $O/ab.jsonl

@@ -16,6 +16,25 @@ import mcpt  # noqa: E402
 
 W, H, S = 1920, 1080, 32
 r = mcpt.Renderer(0)
+if "--stream" in sys.argv:
+    # the stream schedule's trace kernel (persistent waves): walk-loop iterations and lanes per
+    # block over the kernel's whole life, scene 8 at B 12 (its iterations reset nothing in between)
+    r.set_target(W, H)
+    ipv, iv = mcpt.camera_canonical(W, H)
+    r.upload_scene(mcpt.Scene.reference(8))
+    r.set_traversal(mcpt.TRAVERSAL_STREAM)
+    r.debug_counters(reset=True)
+    r.render(ipv, iv, 1, 64, 0.0, 12, 1.0, 0)
+    c = r.debug_counters(reset=True).astype(float)
+    lit, wit, nl, nw, ll, lw = c[9:15]
+    print(json.dumps({"scene": 8, "mode": "stream", "spp": 64, "wave_lives": int(c[6]),
+                      "walk_loop_simd_util": round(lit / (64 * wit), 3) if wit else None,
+                      "node_block_lane_util": round(nl / (64 * nw), 3) if nw else None,
+                      "leaf_block_lane_util": round(ll / (64 * lw), 3) if lw else None,
+                      "node_iters": nw, "leaf_iters": lw, "iters": wit,
+                      "lane_node_visits": nl, "lane_leaf_visits": ll}), flush=True)
+    r.close()
+    sys.exit(0)
 r.set_target(W, H)
 ipv, iv = mcpt.camera_canonical(W, H)
 for sid, B in [(6, 8), (3, 8), (8, 12)]:
