@@ -80,16 +80,19 @@ struct mcpt_ctx {
   // AUTO schedule: the first sizeable launches after a scene upload run each candidate twice
   // (kernel time per sample from the launch events), later launches use the fastest (results
   // are identical either way).  Candidates: 1 = per-lane walk, 2 = wave-coherent walk, 3 = the
-  // stream schedule (deep BVHs, montecarlo.frag, no meshes), and per-lane walks with 2 (4, on
-  // launches of >= 2 pass segments) or 4 (5, >= 4 segments) pass segments per work item.
+  // stream schedule (deep BVHs, montecarlo.frag, no meshes), per-lane walks with 2 (4, on
+  // launches of >= 2 pass segments) or 4 (5, >= 4 segments) pass segments per work item, and
+  // for BVH depth >= 8 per-lane walks with the deep knobs (leaf batch 16, walk exit 32) and 4
+  // (6) or 8 (7, >= 8 segments) segments per item.
   int tune_pending = 0;             // candidate of the launch whose timing is not collected yet
   double tune_samples = 0.0;        // samples of that launch
   long long tune_shape[2] = {0, 0};      // (local pixels, passes) of that launch
   long long meas_shape[2] = {0, 0};      // shape the measurements below were taken on
   int meas_segs = 0;                // pass segments of that shape (which candidates apply)
-  double tune_ns[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};   // best ns per sample measured, by candidate (same shape)
-  int tune_cnt[6] = {0, 0, 0, 0, 0, 0};                  // trials of each candidate so far
+  double tune_ns[8] = {0.0};       // best ns per sample measured, by candidate (same shape)
+  int tune_cnt[8] = {0};            // trials of each candidate so far
   bool stream_auto = false;         // the stream candidate applies to the current launch
+  bool deep_auto = false;           // the deep-knob candidates apply (BVH depth >= 8, per-lane kernel)
   int tune_choice = 0;              // resolved candidate once all are measured
   int walk_exit = -1;               // mcpt_set_walk_exit; -1: by BVH depth
   int leaf_batch = -1;              // MCPT_LEAF_BATCH env (tuning); -1: default
@@ -158,15 +161,25 @@ static int resolve_leaf_batch(const mcpt_ctx* c) {
 }
 
 constexpr int kCandStream = MCPT_TRAVERSAL_STREAM, kCandLaneSeg2 = 4, kCandLaneSeg4 = 5;
+// deep-BVH candidates (BVH depth >= 8): per-lane walks with the deep knobs at leaf batch 16 and
+// walk exit 32 (instead of 8 / 16), four or eight segments per item.  Scene 8 (C4 workload):
+// 539 / 544 Msamples/s against 515 for the defaults at four segments; scene 3 prefers the
+// defaults (profiles/r03_ab_deep_knobs.jsonl, r02_deep_knobs_sweep.jsonl): timed, not guessed
+constexpr int kCandDeepSeg4 = 6, kCandDeepSeg8 = 7, kCandLast = kCandDeepSeg8;
+constexpr int kDeepLeafBatch = 16, kDeepWalkExit = 32;
 // BVH depth from which AUTO also times the stream schedule (its pool and two launches per
 // iteration only pay where walks are long)
 constexpr int kStreamAutoDepth = 8;
 // the candidates that apply to a launch of `segs` pass segments
 static bool cand_applies(const mcpt_ctx* c, int cand, long long segs) {
   return cand <= 2 || (cand == kCandStream && c->stream_auto) || (cand == kCandLaneSeg2 && segs >= 2) ||
-         (cand == kCandLaneSeg4 && segs >= 4);
+         (cand == kCandLaneSeg4 && segs >= 4) || (cand == kCandDeepSeg4 && c->deep_auto && segs >= 4) ||
+         (cand == kCandDeepSeg8 && c->deep_auto && segs >= 8);
 }
-static int cand_seg_per_item(int cand) { return cand == kCandLaneSeg2 ? 2 : cand == kCandLaneSeg4 ? 4 : 1; }
+static int cand_seg_per_item(int cand) {
+  return cand == kCandLaneSeg2 ? 2 : (cand == kCandLaneSeg4 || cand == kCandDeepSeg4) ? 4 : cand == kCandDeepSeg8 ? 8 : 1;
+}
+static bool cand_deep_knobs(int cand) { return cand == kCandDeepSeg4 || cand == kCandDeepSeg8; }
 
 // AUTO times every applicable candidate kTuneRounds times and keeps each one's best time:
 // round 1 in candidate order, round 2 in reverse, so that the clock ramp and cache warm-up of
@@ -181,11 +194,11 @@ static int resolve_candidate(const mcpt_ctx* c, long long segs) {
   // next trial: in the current round (the fewest trials of any applicable candidate), the
   // first candidate of the round's order not yet timed that often on the measured shape
   int round = kTuneRounds;
-  for (int k = 1; k <= kCandLaneSeg4; ++k)
+  for (int k = 1; k <= kCandLast; ++k)
     if (cand_applies(c, k, segs)) round = std::min(round, c->tune_cnt[k]);
   if (round >= kTuneRounds) return MCPT_TRAVERSAL_LANE;
-  for (int i = 0; i < kCandLaneSeg4; ++i) {
-    const int k = (round % 2 == 0) ? 1 + i : kCandLaneSeg4 - i;
+  for (int i = 0; i < kCandLast; ++i) {
+    const int k = (round % 2 == 0) ? 1 + i : kCandLast - i;
     if (cand_applies(c, k, segs) && c->tune_cnt[k] == round) return k;
   }
   return MCPT_TRAVERSAL_LANE;
@@ -225,7 +238,7 @@ static hipError_t collect_tuning(mcpt_ctx* c) {
   const double* t = c->tune_ns;
   bool all = true;
   int best = MCPT_TRAVERSAL_LANE;
-  for (int k = 1; k <= kCandLaneSeg4; ++k) {
+  for (int k = 1; k <= kCandLast; ++k) {
     if (!cand_applies(c, k, c->meas_segs)) continue;
     if (c->tune_cnt[k] < kTuneRounds) all = false;
     else if (t[k] < t[best]) best = k;
@@ -770,6 +783,7 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   // tails average out) or cost (longer grid tail) depends on the scene and the launch: timed,
   // not guessed (profiles/r01_ab44_seg_per_item.jsonl, r01_ab49_seg_groups_tail.jsonl)
   c->stream_auto = stream_applies(c, variant, bounces, false) && c->depth >= kStreamAutoDepth;
+  c->deep_auto = c->depth >= 8;
   const int cand = count ? (c->traversal == MCPT_TRAVERSAL_AUTO ? MCPT_TRAVERSAL_LANE : c->traversal)
                          : resolve_candidate(c, total_seg);
   const bool stream = cand == kCandStream && stream_applies(c, variant, bounces, count);
@@ -778,6 +792,10 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   p.wave_traversal = (mode == MCPT_TRAVERSAL_WAVE) ? 1 : 0;
   p.walk_exit = resolve_walk_exit(c);
   p.leaf_batch = resolve_leaf_batch(c);
+  if (cand_deep_knobs(cand)) {   // the deep candidates' knobs, unless set explicitly
+    if (c->walk_exit < 0) p.walk_exit = kDeepWalkExit;
+    if (c->leaf_batch < 0) p.leaf_batch = kDeepLeafBatch;
+  }
   // pass segments per work item: candidate 3 of AUTO runs two; MCPT_SEG_PER_ITEM overrides
   const int env_seg = env_int("MCPT_SEG_PER_ITEM", 0);
   p.seg_per_item = env_seg > 0 ? env_seg : cand_seg_per_item(cand);
@@ -1092,13 +1110,16 @@ int mcpt_set_leaf_batch(mcpt_ctx* c, int lanes) {
 
 int mcpt_get_leaf_batch(mcpt_ctx* c, int* resolved) {
   if (!c || !resolved) return MCPT_ERR_INVALID_ARG;
-  *resolved = resolve_leaf_batch(c);
+  // the value the next launch of the last launch shape uses (an AUTO deep candidate sets its own)
+  const int cand = resolve_candidate(c, c->meas_segs);
+  *resolved = (cand_deep_knobs(cand) && c->leaf_batch < 0) ? kDeepLeafBatch : resolve_leaf_batch(c);
   return MCPT_OK;
 }
 
 int mcpt_get_walk_exit(mcpt_ctx* c, int* resolved) {
   if (!c || !resolved) return MCPT_ERR_INVALID_ARG;
-  *resolved = resolve_walk_exit(c);
+  const int cand = resolve_candidate(c, c->meas_segs);
+  *resolved = (cand_deep_knobs(cand) && c->walk_exit < 0) ? kDeepWalkExit : resolve_walk_exit(c);
   return MCPT_OK;
 }
 
