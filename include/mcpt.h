@@ -178,7 +178,7 @@ int mcpt_gather_rows(mcpt_ctx* frame, mcpt_ctx* const* shards, int n_shards);
 /* Select the traversal strategy (mcpt_traversal) for later renders; default AUTO.  AUTO times
  * its schedule candidates (per-lane walk, wave-coherent walk, per-lane walk with two and with
  * four pass segments per work item, where the launch has that many segments; for BVH depth >= 8
- * also the stream schedule and per-lane walks with leaf batch 16 / walk exit 32 at four and
+ * also the stream schedule and per-lane walks with leaf batch 16 / walk exit 40 at four and
  * eight segments per item) on the first launches of >= 2^24 samples after a scene upload: two
  * rounds, forward then reverse order, each candidate's best time per sample kept, compared only
  * between launches of the same shape — at most 14 launches (mcpt.AUTO_TRIALS); later launches

@@ -82,7 +82,7 @@ struct mcpt_ctx {
   // are identical either way).  Candidates: 1 = per-lane walk, 2 = wave-coherent walk, 3 = the
   // stream schedule (deep BVHs, montecarlo.frag, no meshes), per-lane walks with 2 (4, on
   // launches of >= 2 pass segments) or 4 (5, >= 4 segments) pass segments per work item, and
-  // for BVH depth >= 8 per-lane walks with the deep knobs (leaf batch 16, walk exit 32) and 4
+  // for BVH depth >= 8 per-lane walks with the deep knobs (leaf batch 16, walk exit 40) and 4
   // (6) or 8 (7, >= 8 segments) segments per item.
   int tune_pending = 0;             // candidate of the launch whose timing is not collected yet
   double tune_samples = 0.0;        // samples of that launch
@@ -162,11 +162,13 @@ static int resolve_leaf_batch(const mcpt_ctx* c) {
 
 constexpr int kCandStream = MCPT_TRAVERSAL_STREAM, kCandLaneSeg2 = 4, kCandLaneSeg4 = 5;
 // deep-BVH candidates (BVH depth >= 8): per-lane walks with the deep knobs at leaf batch 16 and
-// walk exit 32 (instead of 8 / 16), four or eight segments per item.  Scene 8 (C4 workload):
-// 539 / 544 Msamples/s against 515 for the defaults at four segments; scene 3 prefers the
-// defaults (profiles/r03_ab_deep_knobs.jsonl, r02_deep_knobs_sweep.jsonl): timed, not guessed
+// walk exit 40 (instead of 8 / 16), four or eight segments per item.  Scene 8 (C4 workload):
+// 539 / 544 Msamples/s at walk exit 32 against 515 for the defaults at four segments; walk exit
+// 40 another +2..3 % at eight segments (552 / 540; with the node rows loaded together 574 / 558);
+// scene 3 prefers the defaults (profiles/r03_ab_deep_knobs.jsonl, r03_ab_deep_walk_exit.jsonl,
+// r02_deep_knobs_sweep.jsonl): timed, not guessed
 constexpr int kCandDeepSeg4 = 6, kCandDeepSeg8 = 7, kCandLast = kCandDeepSeg8;
-constexpr int kDeepLeafBatch = 16, kDeepWalkExit = 32;
+constexpr int kDeepLeafBatch = 16, kDeepWalkExit = 40;
 // BVH depth from which AUTO also times the stream schedule (its pool and two launches per
 // iteration only pay where walks are long)
 constexpr int kStreamAutoDepth = 8;

@@ -238,6 +238,44 @@ __device__ __forceinline__ bool box_test(float4 a0, float4 a1, float4 a2, f3 O, 
   return false;
 }
 
+// A node visit's two child records (rows: centre + has-prim flag, half-width, 1/half-width)
+// and their box tests: (hl, hr) = the reference's push decisions for the left and right child.
+// A child whose subtree holds no primitive (flag 0) cannot change the hit and is never tested
+// (COUNT keeps the reference's visits for its event model).
+// In the source a row is first used behind a test (the child-empty flag, the box test's inside
+// early-out, the left child's whole test before the right's), and LLVM sinks each load to its
+// first use, so one node visit of the L1/L2-read kernels was a chain of up to five dependent
+// cache round trips (flag -> centre + 1/w -> w -> right 1/w -> right w, read off the ISA).
+// MCPT_NODE_LOADS_TOGETHER: there, every row is issued at once and an empty asm consumes them
+// at that point, so a visit waits for one round trip (scene 8 +4..5 %, scenes 3/5/7 +1..3 %:
+// profiles/r03_ab_node_loads_together.jsonl).  Same values, same bits.  The LDS-scene kernels
+// (ds_read latency is short: -1 % with the rows together) and the mesh kernels (128-VGPR walk
+// state: they spill) keep the lazy form.
+#ifndef MCPT_NODE_LOADS_TOGETHER
+#define MCPT_NODE_LOADS_TOGETHER 1
+#endif
+#ifndef MCPT_PRIM_TRF_EARLY
+#define MCPT_PRIM_TRF_EARLY 0
+#endif
+template <bool COUNT, class SR>
+__device__ __forceinline__ void node_tests(const SR& s, const float4* __restrict__ nodes, size_t j, f3 O, f3 D,
+                                           f3 invD, double cull2, bool& hl, bool& hr) {
+  if constexpr (MCPT_NODE_LOADS_TOGETHER && !SR::kLds && !SR::kMesh) {
+    const float4* q = nodes + j * 3;
+    float4 l0 = q[0], l1 = q[1], l2 = q[2], r0 = q[3], r1 = q[4], r2 = q[5];
+    asm volatile("" : "+v"(l0.x), "+v"(l0.y), "+v"(l0.z), "+v"(l0.w), "+v"(l1.x), "+v"(l1.y), "+v"(l1.z),
+                 "+v"(l2.x), "+v"(l2.y), "+v"(l2.z));
+    asm volatile("" : "+v"(r0.x), "+v"(r0.y), "+v"(r0.z), "+v"(r0.w), "+v"(r1.x), "+v"(r1.y), "+v"(r1.z),
+                 "+v"(r2.x), "+v"(r2.y), "+v"(r2.z));
+    hl = (COUNT || l0.w != 0.0f) && box_test<false>(l0, l1, l2, O, D, invD, cull2);
+    hr = (COUNT || r0.w != 0.0f) && box_test<false>(r0, r1, r2, O, D, invD, cull2);
+  } else {
+    const float4 l0 = nodes[j * 3], r0 = nodes[j * 3 + 3];
+    hl = (COUNT || l0.w != 0.0f) && box_test<false>(l0, nodes[j * 3 + 1], nodes[j * 3 + 2], O, D, invD, cull2);
+    hr = (COUNT || r0.w != 0.0f) && box_test<false>(r0, nodes[j * 3 + 4], nodes[j * 3 + 5], O, D, invD, cull2);
+  }
+}
+
 // intersect_bvm raytracer_func.frag:273-311: the mesh BVH's box test, in mesh space (O, D),
 // with the entry point taken to world space through the mesh transform (rows t0..t2) and
 // compared with the world distance from Ol.  Same face loop as box_test.
@@ -273,18 +311,26 @@ __device__ __forceinline__ bool box_test_mesh(float4 a0, float4 a1, float4 a2, f
   return false;
 }
 
-template <bool COUNT, bool UNI, class SR>
-__device__ __forceinline__ void accept_cand(const SR& s, int index, int shape, int dir, f3 Pl, f3 Ol,
-                                            Hit& h, Ev<COUNT>& ev) {
+// a candidate hit at local point Pl of primitive `index` (transform rows t0..t2): world
+// distance from Ol, kept if closer
+template <bool COUNT>
+__device__ __forceinline__ void accept_rows(int index, int shape, int dir, f3 Pl, f3 Ol, float4 t0, float4 t1,
+                                            float4 t2, Hit& h, Ev<COUNT>& ev, bool fast_len) {
   ev.inc(EV_CAND);
-  const size_t b = (size_t)index * 8;
-  constexpr bool U = UNI && !SR::kLds;
-  f3 Pg = xpoint(ld4<U>(s.prims, b + 3), ld4<U>(s.prims, b + 4), ld4<U>(s.prims, b + 5), Pl);
-  float dist = wlength3<SR::kFastLen>(sub(Ol, Pg));
+  f3 Pg = xpoint(t0, t1, t2, Pl);
+  float dist = fast_len ? length3(sub(Ol, Pg)) : length3_g(sub(Ol, Pg));
   if (dist < h.dist) {
     h.dist = dist; h.pl = Pl; h.set(index, shape, dir);
     h.cull2 = cull_bound_sq(dist);
   }
+}
+template <bool COUNT, bool UNI, class SR>
+__device__ __forceinline__ void accept_cand(const SR& s, int index, int shape, int dir, f3 Pl, f3 Ol,
+                                            Hit& h, Ev<COUNT>& ev) {
+  const size_t b = (size_t)index * 8;
+  constexpr bool U = UNI && !SR::kLds;
+  accept_rows<COUNT>(index, shape, dir, Pl, Ol, ld4<U>(s.prims, b + 3), ld4<U>(s.prims, b + 4),
+                     ld4<U>(s.prims, b + 5), h, ev, SR::kFastLen);
 }
 
 // Triangle_intersect raytracer_func.frag:354-396 (Möller–Trumbore, mesh space); a hit keeps
@@ -345,7 +391,7 @@ __device__ __forceinline__ void mesh_test(const SR& s, int mesh, int index, f3 O
     } else {
       ev.inc(EV_NODE);
       const size_t j = 2 * (size_t)node + 1;
-      const float4 l0 = nodes[j * 3], r0 = nodes[j * 3 + 3];
+      const float4 l0 = nodes[j * 3], r0 = nodes[j * 3 + 3];   // (mesh kernels: see node_tests)
       bool hl = (COUNT || l0.w != 0.0f) &&
                 box_test_mesh(l0, nodes[j * 3 + 1], nodes[j * 3 + 2], O, D, invD, Ol, t0, t1, t2, h.cull2);
       bool hr = (COUNT || r0.w != 0.0f) &&
@@ -373,11 +419,33 @@ template <bool COUNT, bool UNI, bool ANY = false, class SR>
 __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit& h, Ev<COUNT>& ev) {
   ev.inc(EV_PRIM);
   constexpr bool U = UNI && !SR::kLds;
-  const int pt = ld1<U>(s.ptype, i);
-  if (pt < 0) return;
-  const int t = pt & 15;
+  // per-lane L1/L2 reads (node_tests): the type code and the inverse rows in one round trip,
+  // else the rows' loads wait behind the type test
+  constexpr bool kTogether = MCPT_NODE_LOADS_TOGETHER && !U && !SR::kLds && !SR::kMesh;
+  int pt = ld1<U>(s.ptype, i);
+  if constexpr (!kTogether) {
+    if (pt < 0) return;
+  }
   const size_t b = (size_t)i * 8;
   float4 r0 = ld4<U>(s.prims, b), r1 = ld4<U>(s.prims, b + 1), r2 = ld4<U>(s.prims, b + 2);
+  if constexpr (kTogether) {
+    asm volatile("" : "+v"(pt), "+v"(r0.x), "+v"(r0.y), "+v"(r0.z), "+v"(r0.w), "+v"(r1.x), "+v"(r1.y),
+                 "+v"(r1.z), "+v"(r1.w), "+v"(r2.x), "+v"(r2.y), "+v"(r2.z), "+v"(r2.w));
+  }
+  // MCPT_PRIM_TRF_EARLY: the transform rows a candidate needs ride in the same round trip
+  constexpr bool kTrfEarly = kTogether && MCPT_PRIM_TRF_EARLY;
+  float4 t0 = r0, t1 = r0, t2 = r0;
+  if constexpr (kTrfEarly) {
+    t0 = ld4<U>(s.prims, b + 3); t1 = ld4<U>(s.prims, b + 4); t2 = ld4<U>(s.prims, b + 5);
+    asm volatile("" : "+v"(t0.x), "+v"(t0.y), "+v"(t0.z), "+v"(t1.x), "+v"(t1.y), "+v"(t1.z), "+v"(t2.x),
+                 "+v"(t2.y), "+v"(t2.z));
+  }
+  auto accept = [&](int shape, int dir, f3 Pl) {
+    if constexpr (kTrfEarly) accept_rows<COUNT>(i, shape, dir, Pl, Ow, t0, t1, t2, h, ev, SR::kFastLen);
+    else accept_cand<COUNT, UNI>(s, i, shape, dir, Pl, Ow, h, ev);
+  };
+  if (pt < 0) return;
+  const int t = pt & 15;
   f3 O = xpoint(r0, r1, r2, Ow);
   f3 D = wnormalize3<SR::kFastNorm>(xdir(r0, r1, r2, Dw));
   if (t == CODE_SPHERE) {
@@ -386,16 +454,16 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
     if (delta4 > 0.0f) {
       float sq = wsqrt<SR::kFastSqrt>(delta4);
       float a = -(OD + sq) / D2;
-      if (a > kEPS) accept_cand<COUNT, UNI>(s, i, CODE_SPHERE, 0, add(O, muls(D, a)), Ow, h, ev);
+      if (a > kEPS) accept(CODE_SPHERE, 0, add(O, muls(D, a)));
       a = -(OD - sq) / D2;
-      if (a > kEPS) accept_cand<COUNT, UNI>(s, i, CODE_SPHERE, 0, add(O, muls(D, a)), Ow, h, ev);
+      if (a > kEPS) accept(CODE_SPHERE, 0, add(O, muls(D, a)));
     }
   } else if (t == CODE_QUAD) {
     if (D.z > -kEPS) return;
     float a = -O.z / D.z;
     f3 Pl = add(O, muls(D, a));
     if (__builtin_fabsf(Pl.x) > 1.0f || __builtin_fabsf(Pl.y) > 1.0f) return;
-    accept_cand<COUNT, UNI>(s, i, CODE_QUAD, 0, Pl, Ow, h, ev);
+    accept(CODE_QUAD, 0, Pl);
   } else if (t == CODE_CUBE) {
     float al = kFLTMAX; int cl = 0;
     float o[3] = {O.x, O.y, O.z}, d[3] = {D.x, D.y, D.z};
@@ -409,7 +477,7 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
           if (a < al) { al = a; cl = f; }
       }
     }
-    if (al < kFLTMAX) accept_cand<COUNT, UNI>(s, i, CODE_CUBE, cl, add(O, muls(D, al)), Ow, h, ev);
+    if (al < kFLTMAX) accept(CODE_CUBE, cl, add(O, muls(D, al)));
   } else if (t == CODE_CYLINDER) {
     int cl = -1; float al = kFLTMAX;
     if (__builtin_fabsf(D.z) > kEPS) {
@@ -435,7 +503,7 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
         if (__builtin_fabsf(z) < 1.0f) { cl = 2; al = a; }
       }
     }
-    if (al < kFLTMAX) accept_cand<COUNT, UNI>(s, i, CODE_CYLINDER, cl, add(O, muls(D, al)), Ow, h, ev);
+    if (al < kFLTMAX) accept(CODE_CYLINDER, cl, add(O, muls(D, al)));
   } else if (t == CODE_CONE) {
     int cl = -1; float tl = kFLTMAX;
     if (__builtin_fabsf(D.z) > kEPS) {
@@ -459,7 +527,7 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
       float tt = gmin(t1, t2);
       if (tt < tl) { cl = 2; tl = tt; }
     }
-    if (tl < kFLTMAX) accept_cand<COUNT, UNI>(s, i, CODE_CONE, cl, add(O, muls(D, tl)), Ow, h, ev);
+    if (tl < kFLTMAX) accept(CODE_CONE, cl, add(O, muls(D, tl)));
   } else if (t == CODE_MESH) {
     if constexpr (SR::kMesh) mesh_test<COUNT, ANY>(s, pt >> 4, i, O, D, Ow, h, ev);
   }
@@ -498,11 +566,8 @@ __device__ __forceinline__ void traverse_lane(const SR& s, f3 O, f3 D, Hit& h, E
     if (!is_leaf) {
       ev.inc(EV_NODE);
       const size_t j = 2 * (size_t)node + 1;
-      const float4 l0 = s.nodes[j * 3], r0 = s.nodes[j * 3 + 3];
-      // a child whose subtree holds no primitive (c.w == 0) cannot change the hit: never
-      // visited (the counting build keeps the reference's visits for its event model)
-      bool hl = (COUNT || l0.w != 0.0f) && box_test<false>(l0, s.nodes[j * 3 + 1], s.nodes[j * 3 + 2], O, D, invD, h.cull2);
-      bool hr = (COUNT || r0.w != 0.0f) && box_test<false>(r0, s.nodes[j * 3 + 4], s.nodes[j * 3 + 5], O, D, invD, h.cull2);
+      bool hl, hr;
+      node_tests<COUNT>(s, s.nodes, j, O, D, invD, h.cull2, hl, hr);
       pop = !(hl || hr);
       if (hr) {
         if (hl) pending |= 1u << (level + 1);
@@ -595,9 +660,8 @@ __device__ __forceinline__ bool walk_run(const SR& s, f3 O, f3 D, Hit& h, Walk& 
     if (do_node) {
       ev.inc(EV_NODE);
       const size_t j = 2 * (size_t)w.node + 1;
-      const float4 l0 = s.nodes[j * 3], r0 = s.nodes[j * 3 + 3];
-      bool hl = (COUNT || l0.w != 0.0f) && box_test<false>(l0, s.nodes[j * 3 + 1], s.nodes[j * 3 + 2], O, D, w.invD, h.cull2);
-      bool hr = (COUNT || r0.w != 0.0f) && box_test<false>(r0, s.nodes[j * 3 + 4], s.nodes[j * 3 + 5], O, D, w.invD, h.cull2);
+      bool hl, hr;
+      node_tests<COUNT>(s, s.nodes, j, O, D, w.invD, h.cull2, hl, hr);
       pop = !(hl || hr);
       if (hr) {
         if (hl) w.pending |= 1u << (w.level + 1);
@@ -649,7 +713,7 @@ __device__ __forceinline__ bool walk_run_mesh(const SR& s, f3 O, f3 D, Hit& h, W
         ev.inc(EV_NODE);
         const float4* nodes = s.mnodes + (size_t)mi.x * 3;
         const size_t j = 2 * (size_t)w.mnode + 1;
-        const float4 l0 = nodes[j * 3], r0 = nodes[j * 3 + 3];
+        const float4 l0 = nodes[j * 3], r0 = nodes[j * 3 + 3];   // (mesh kernels: see node_tests)
         const bool hl = (COUNT || l0.w != 0.0f) &&
                         box_test_mesh(l0, nodes[j * 3 + 1], nodes[j * 3 + 2], w.Om, w.Dm, w.invDm, O, t0, t1, t2, h.cull2);
         const bool hr = (COUNT || r0.w != 0.0f) &&
@@ -699,7 +763,7 @@ __device__ __forceinline__ bool walk_run_mesh(const SR& s, f3 O, f3 D, Hit& h, W
     } else {
       ev.inc(EV_NODE);
       const size_t j = 2 * (size_t)w.node + 1;
-      const float4 l0 = s.nodes[j * 3], r0 = s.nodes[j * 3 + 3];
+      const float4 l0 = s.nodes[j * 3], r0 = s.nodes[j * 3 + 3];   // (mesh kernels: see node_tests)
       const bool hl = (COUNT || l0.w != 0.0f) &&
                       box_test<false>(l0, s.nodes[j * 3 + 1], s.nodes[j * 3 + 2], O, D, w.invD, h.cull2);
       const bool hr = (COUNT || r0.w != 0.0f) &&
