@@ -224,6 +224,12 @@ int mcpt_get_leaf_batch(mcpt_ctx* ctx, int* resolved_lanes);
 int mcpt_set_partial_budget(mcpt_ctx* ctx, size_t bytes);
 /* Sub-launches the last render call was split into. */
 int mcpt_last_launch_count(mcpt_ctx* ctx, int* n_launches);
+/* 1 if the last render call ran one pass segment per pass: a call of 2..256 passes whose
+ * launch would have fewer than 4 work items per compute unit (e.g. 256x256 at 4 spp) runs each
+ * pass as its own segment, so a pixel's passes run side by side, and the combine step sums each
+ * 32-pass chunk's passes from 0 in pass order, as one lane would: the bits do not change.
+ * Env MCPT_PASS_SPLIT=0/1 forces it off/on. */
+int mcpt_last_pass_split(mcpt_ctx* ctx, int* split);
 
 /* Ray queries on the uploaded scene — the shader library calls a TP integrator may use
  * (raytracer_func.frag:718-781, 874-907): traverse_all_bvh (any_hit = 0) or just_hit_bvh

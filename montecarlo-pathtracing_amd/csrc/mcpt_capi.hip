@@ -74,6 +74,7 @@ struct mcpt_ctx {
   // combine kernel); a call is split into sub-launches at chunk boundaries (partial_budget)
   std::vector<hipEvent_t> evs;
   int n_sub = 0;                    // sub-launches of the last render call
+  int pass_split = 0;               // the last render call ran one segment per pass (launch())
   bool timed = false;
   size_t partial_budget = kDefaultPartialBudget;
   int traversal = MCPT_TRAVERSAL_AUTO;
@@ -169,6 +170,9 @@ constexpr int kCandStream = MCPT_TRAVERSAL_STREAM, kCandLaneSeg2 = 4, kCandLaneS
 // r02_deep_knobs_sweep.jsonl): timed, not guessed
 constexpr int kCandDeepSeg4 = 6, kCandDeepSeg8 = 7, kCandLast = kCandDeepSeg8;
 constexpr int kDeepLeafBatch = 16, kDeepWalkExit = 40;
+// pass split (launch()): launches with fewer than this many work items per CU, of at most
+// kPassSplitMaxPasses passes
+constexpr int kPassSplitItemsPerCu = 4, kPassSplitMaxPasses = 256;
 // BVH depth from which AUTO also times the stream schedule (its pool and two launches per
 // iteration only pay where walks are long)
 constexpr int kStreamAutoDepth = 8;
@@ -822,13 +826,25 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   if (p.n_tiles > max_items) return set_err(MCPT_ERR_INVALID_ARG, "render target too large for one launch");
   long long max_seg = seg_bytes > 0 ? (long long)(c->partial_budget / (size_t)seg_bytes) : (1LL << 30);
   max_seg = std::max(1LL, std::min(max_seg, p.n_tiles > 0 ? max_items / p.n_tiles : max_items));
+  // Pass split: a launch with too few work items to fill the chip (C1: 256 tiles x 1 segment
+  // on 256 CUs, one wave per SIMD running every pass of its pixels in turn) runs one segment per
+  // pass instead, so the passes of a pixel run side by side in different work items; the split
+  // combine sums each chunk's passes from 0 in pass order (the bits of the unsplit launch).
+  // MCPT_PASS_SPLIT=0/1 forces it off/on (tests, A/B).
+  const int env_split = env_int("MCPT_PASS_SPLIT", -1);
+  const bool split_fits = !stream && n_passes > 1 && n_passes <= max_seg && n_passes <= kPassSplitMaxPasses &&
+                          p.n_tiles * (long long)n_passes <= max_items;
+  const bool split = split_fits && (env_split >= 0 ? env_split > 0
+                                                   : p.n_tiles * total_seg < (long long)kPassSplitItemsPerCu * c->n_cu);
+  p.pass_split = split ? 1 : 0;
+  if (split) p.seg_per_item = 1;
   int n_sub = 0;
   for (long long lo = first_pass, end = (long long)first_pass + n_passes; lo < end; ++n_sub) {
     const long long c0 = fdiv((int)(lo - 1), mcpt::kPassChunk);
-    lo = std::min(end, (c0 + max_seg) * mcpt::kPassChunk + 1);
+    lo = split ? end : std::min(end, (c0 + max_seg) * mcpt::kPassChunk + 1);
   }
   HIP_OR_RETURN(ensure_events(c, std::max(n_sub, 1)));
-  const long long segs = std::min(max_seg, total_seg);   // most segments of one sub-launch
+  const long long segs = split ? n_passes : std::min(max_seg, total_seg);   // most segments of one sub-launch
   if (segs > 1 && (size_t)segs * (size_t)seg_bytes > c->partial_bytes) {
     const size_t need = (size_t)segs * (size_t)seg_bytes;
     HIP_OR_RETURN(hipStreamSynchronize(c->stream));
@@ -849,6 +865,7 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
     c->tune_shape[1] = n_passes;
   }
   c->n_sub = std::max(n_sub, 1);
+  c->pass_split = split ? 1 : 0;
   if (n_sub == 0) {   // no passes: an empty timed interval
     HIP_OR_RETURN(hipEventRecord(ev_start(c, 0), c->stream));
     HIP_OR_RETURN(hipEventRecord(ev_mid(c, 0), c->stream));
@@ -856,10 +873,10 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   }
   for (long long lo = first_pass, end = (long long)first_pass + n_passes, k = 0; lo < end; ++k) {
     const long long c0 = fdiv((int)(lo - 1), mcpt::kPassChunk);
-    const long long hi = std::min(end, (c0 + max_seg) * mcpt::kPassChunk + 1);
+    const long long hi = split ? end : std::min(end, (c0 + max_seg) * mcpt::kPassChunk + 1);
     p.first_pass = (int)lo;
     p.n_passes = (int)(hi - lo);
-    p.n_segments = fdiv((int)(hi - 2), mcpt::kPassChunk) - (int)c0 + 1;
+    p.n_segments = split ? p.n_passes : fdiv((int)(hi - 2), mcpt::kPassChunk) - (int)c0 + 1;
     HIP_OR_RETURN(hipEventRecord(ev_start(c, (int)k), c->stream));
     if (stream) {
       const int st = stream_run(c, p);
@@ -1101,6 +1118,12 @@ int mcpt_set_partial_budget(mcpt_ctx* c, size_t bytes) {
 int mcpt_last_launch_count(mcpt_ctx* c, int* n_launches) {
   if (!c || !n_launches) return MCPT_ERR_INVALID_ARG;
   *n_launches = c->timed ? c->n_sub : 0;
+  return MCPT_OK;
+}
+
+int mcpt_last_pass_split(mcpt_ctx* c, int* split) {
+  if (!c || !split) return MCPT_ERR_INVALID_ARG;
+  *split = c->timed ? c->pass_split : 0;
   return MCPT_OK;
 }
 

@@ -67,6 +67,7 @@ struct RenderParams {
   long long n_local_px;         // n_local_rows × W
   int n_tiles, n_segments;      // 32x8 tiles of the local rows; pass segments of this launch
   int seg_per_item;             // consecutive segments one work item runs (>= 1)
+  int pass_split;               // 1: one segment per pass (n_segments = n_passes; small launches)
   int depth, n_prims;
   int lds_scene_bytes;          // > 0: stage the scene into LDS (<= kLdsSceneBytes, no meshes)
   // triangle meshes (mcpt_upload_meshes); n_meshes == 0: none

@@ -1103,8 +1103,12 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
   const bool live = x < p.W && lr < p.n_local_rows;   // (no early return: LDS staging barrier)
   const int cbase = floordiv(p.first_pass - 1, kPassChunk);   // chunk of the launch's first pass
   const int c0 = cbase + seg_lo;
-  const int pass_begin = max(p.first_pass, c0 * kPassChunk + 1);
+  int pass_begin = max(p.first_pass, c0 * kPassChunk + 1);
   int pass_end = min(p.first_pass + p.n_passes, (c0 + 1) * kPassChunk + 1);   // this unit's end
+  if (p.pass_split) {   // one segment per pass (small launches; combine_split_kernel sums them)
+    pass_begin = p.first_pass + seg_lo;
+    pass_end = pass_begin + 1;
+  }
   int y = live ? p.rows[lr] : 0;   // this shard's local row -> image row (mcpt_set_target*)
   int pslot = tid;                 // LDS slot of this unit's pixel (per-pixel rows of s_pix, s_hit0)
 
@@ -1564,6 +1568,28 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
 }
 
 // accum += seg_0 + seg_1 + ... in chunk order (one thread per pixel channel triple)
+// pass-split launches (RenderParams::pass_split): slot k holds pass first_pass + k's value
+// (0 + v, as a lane's segment sum starts); each accumulation chunk's passes are summed from 0 in
+// pass order, as one lane would have, and the chunk sum is added to the accumulator in chunk
+// order: the bits of an unsplit launch
+__global__ __launch_bounds__(256) void combine_split_kernel(float* __restrict__ accum, const float* __restrict__ partial,
+                                                            long long n_px, int first_pass, int n_passes) {
+  long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n_px) return;
+  float a0 = accum[i * 3], a1 = accum[i * 3 + 1], a2 = accum[i * 3 + 2];
+  float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f;
+  for (int k = 0; k < n_passes; ++k) {
+    const float* q = partial + ((size_t)k * n_px + i) * 3;
+    s0 = s0 + q[0]; s1 = s1 + q[1]; s2 = s2 + q[2];
+    const int pass = first_pass + k;
+    if (k + 1 == n_passes || floordiv(pass - 1, kPassChunk) != floordiv(pass, kPassChunk)) {   // chunk ends
+      a0 = a0 + s0; a1 = a1 + s1; a2 = a2 + s2;
+      s0 = 0.0f; s1 = 0.0f; s2 = 0.0f;
+    }
+  }
+  accum[i * 3] = a0; accum[i * 3 + 1] = a1; accum[i * 3 + 2] = a2;
+}
+
 __global__ __launch_bounds__(256) void combine_kernel(float* __restrict__ accum, const float* __restrict__ partial,
                                                       long long n_px, int n_seg) {
   long long i = (long long)blockIdx.x * 256 + threadIdx.x;
@@ -2170,7 +2196,11 @@ hipError_t mcpt_launch_render(const mcpt::RenderParams& p, bool count, hipStream
 hipError_t mcpt_launch_combine(const mcpt::RenderParams& p, hipStream_t stream) {
   if (p.n_segments <= 1 || p.n_local_px <= 0) return hipSuccess;
   dim3 block(256), grid((unsigned)((p.n_local_px + 255) / 256));
-  hipLaunchKernelGGL(mcpt::combine_kernel, grid, block, 0, stream, p.accum, p.partial, p.n_local_px, p.n_segments);
+  if (p.pass_split)
+    hipLaunchKernelGGL(mcpt::combine_split_kernel, grid, block, 0, stream, p.accum, p.partial, p.n_local_px,
+                       p.first_pass, p.n_passes);
+  else
+    hipLaunchKernelGGL(mcpt::combine_kernel, grid, block, 0, stream, p.accum, p.partial, p.n_local_px, p.n_segments);
   return hipGetLastError();
 }
 

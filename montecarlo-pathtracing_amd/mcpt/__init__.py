@@ -107,6 +107,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "mcpt_set_stream_pool": (i, [_vp, i, i]),
         "mcpt_stream_iterations": (i, [_vp, ctypes.POINTER(ctypes.c_longlong)]),
         "mcpt_last_launch_count": (i, [_vp, ip]),
+        "mcpt_last_pass_split": (i, [_vp, ip]),
         "mcpt_set_stream": (i, [_vp, _vp]),
         "mcpt_synchronize": (i, [_vp]),
         "mcpt_last_render_ms": (i, [_vp, fp]),
@@ -598,6 +599,13 @@ class Renderer:
         n = ctypes.c_int()
         _check(lib().mcpt_last_launch_count(self._h, ctypes.byref(n)), "mcpt_last_launch_count")
         return n.value
+
+    def last_pass_split(self) -> bool:
+        """mcpt_last_pass_split: the last render call ran one segment per pass (small launches;
+        same bits)."""
+        n = ctypes.c_int()
+        _check(lib().mcpt_last_pass_split(self._h, ctypes.byref(n)), "mcpt_last_pass_split")
+        return bool(n.value)
 
     def traversal(self) -> int:
         """The strategy AUTO resolves to for the uploaded scene."""

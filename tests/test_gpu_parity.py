@@ -150,6 +150,37 @@ def test_partial_budget_split_bit_equal(mcpt_mod, oracle_mod, renderer, budget_s
     assert np.array_equal(ev, ev_ref), (ev, ev_ref)
 
 
+@pytest.mark.parametrize("traversal", [1, 2])
+@pytest.mark.parametrize("scene_id,B", [(1, 3), (6, 8), (8, 12)])
+@pytest.mark.parametrize("first,S", [(1, 4), (30, 5), (1, 40), (7, 100), (33, 2)])
+def test_pass_split_bit_equal(mcpt_mod, oracle_mod, renderer, monkeypatch, traversal, scene_id, B, first, S):
+    """Pass split (one segment per pass, the split combine summing each chunk's passes in order)
+    against the unsplit launch and the oracle, with pass ranges that start inside a chunk and
+    straddle chunk boundaries."""
+    W, H = 40, 24
+    monkeypatch.setenv("MCPT_PASS_SPLIT", "0")
+    whole = _gpu(mcpt_mod, renderer, scene_id, W, H, first, S, B, traversal=traversal)
+    assert not renderer.last_pass_split()
+    monkeypatch.setenv("MCPT_PASS_SPLIT", "1")
+    split = _gpu(mcpt_mod, renderer, scene_id, W, H, first, S, B, traversal=traversal)
+    assert renderer.last_pass_split()
+    assert renderer.last_launch_count() == 1
+    assert np.array_equal(whole.view(np.uint32), split.view(np.uint32))
+    ref, _ = _oracle(oracle_mod, scene_id, W, H, first, S, B)
+    _compare(split, ref, f"pass split scene {scene_id} passes {first}..{first + S - 1}")
+
+
+def test_pass_split_default_small_launch(mcpt_mod, renderer, monkeypatch):
+    """Without the override, a launch with few work items per CU splits, a large one does not."""
+    monkeypatch.delenv("MCPT_PASS_SPLIT", raising=False)
+    _gpu(mcpt_mod, renderer, 1, 256, 256, 1, 4, 3, traversal=1)   # C1's shape: 256 tiles
+    assert renderer.last_pass_split()
+    _gpu(mcpt_mod, renderer, 6, 1920, 1080, 1, 2, 8, traversal=1)  # 8,160 tiles
+    assert not renderer.last_pass_split()
+    _gpu(mcpt_mod, renderer, 1, 256, 256, 1, 1, 3, traversal=1)   # one pass: nothing to split
+    assert not renderer.last_pass_split()
+
+
 @pytest.mark.parametrize("first,S", [(20, 50), (1, 64), (33, 1), (7, 100)])
 def test_pass_segments_vs_oracle(mcpt_mod, oracle_mod, renderer, first, S):
     """Launches spanning several accumulation chunks (segment sums + combine kernel)."""
