@@ -220,7 +220,7 @@ int mcpt_get_leaf_batch(mcpt_ctx* ctx, int* resolved_lanes);
 /* Bound (bytes) of the device buffer holding the per-chunk partial sums of one launch.  A
  * render call whose pass range spans more 32-pass chunks than fit is run as several launches
  * cut at chunk boundaries (e.g. 84,000 passes at 4K in one call); the accumulator is
- * bit-identical for any budget.  Default 1 GiB (env MCPT_PARTIAL_BYTES at create). */
+ * bit-identical for any budget.  Default 4 GiB (env MCPT_PARTIAL_BYTES at create). */
 int mcpt_set_partial_budget(mcpt_ctx* ctx, size_t bytes);
 /* Sub-launches the last render call was split into. */
 int mcpt_last_launch_count(mcpt_ctx* ctx, int* n_launches);

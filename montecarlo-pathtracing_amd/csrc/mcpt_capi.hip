@@ -35,9 +35,11 @@ static int set_err(int status, const char* what, hipError_t e = hipSuccess) {
     if (e_ != hipSuccess) return set_err(MCPT_ERR_HIP, #call, e_);  \
   } while (0)
 
-// default bound of the segment-sum buffer of one sub-launch (1 GiB: 42 segments = 1,344
-// passes per launch at 1080p, 10 at 4K; mcpt_set_partial_budget / MCPT_PARTIAL_BYTES)
-constexpr size_t kDefaultPartialBudget = size_t(1) << 30;
+// default bound of the segment-sum buffer of one sub-launch (4 GiB of the 288 GB of HBM: 172
+// segments = 5,504 passes per launch at 1080p, 43 = 1,376 at 4K, so a C5 step of 1,024 passes
+// is one launch: +0.7 % against four launches under a 1 GiB bound, whose grid tails add up,
+// profiles/r03_ab_partial_budget_c5.jsonl; mcpt_set_partial_budget / MCPT_PARTIAL_BYTES)
+constexpr size_t kDefaultPartialBudget = size_t(4) << 30;
 
 struct mcpt_ctx {
   int device = 0;

@@ -30,7 +30,8 @@ def load(d, launches=1):
     """Counters of the timed step's path-tracing launches in each pass, summed: the LAST
     `launches` dispatches (earlier ones are warm-up, including AUTO's timing trials).  A render
     call spanning more pass segments than the segment-sum budget holds runs as several
-    sub-launches (C5: 4), and bench.py times the whole call, so its record sums them."""
+    sub-launches (C5 under the old 1 GiB partial budget: 4; one since the 4 GiB default), and
+    bench.py times the whole call, so its record sums them."""
     out = {}
     for f in glob.glob(os.path.join(d, "*", "run_counter_collection.csv")):
         per_dispatch = collections.defaultdict(dict)
