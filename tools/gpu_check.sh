@@ -23,11 +23,13 @@ if [ "${2:-}" != "nopmc" ]; then
   python tools/pmc_summary.py $O/pmc_c4 scene8_1920x1080_512spp_B12 $O/pmc_records.json > /dev/null &&
   cp $O/pmc_records.json profiles/pmc_records.json || exit $?
 fi
-if [ "${3:-}" = "pmcall" ]; then   # PMC records for the C3 line's dominant point and C5 too
+if [ "${3:-}" = "pmcall" ]; then   # PMC records for the C3 line's dominant point, C5 and C1 too
   bash tools/pmc.sh $O/pmc_c3 --config c3 --rough 0 && echo "pmc c3 ok" &&
   python tools/pmc_summary.py $O/pmc_c3 scene6_1920x1080_1024spp_B8_ior1.5_rough0 $O/pmc_records.json > /dev/null &&
   bash tools/pmc.sh $O/pmc_c5 --config c5 && echo "pmc c5 ok" &&
   python tools/pmc_summary.py $O/pmc_c5 scene6_3840x2160_1024spp_B8 $O/pmc_records.json --launches=1 > /dev/null &&
+  bash tools/pmc.sh $O/pmc_c1 --config c1 && echo "pmc c1 ok" &&
+  python tools/pmc_summary.py $O/pmc_c1 scene1_256x256_4spp_B3 $O/pmc_records.json > /dev/null &&
   cp $O/pmc_records.json profiles/pmc_records.json || exit $?
 fi
 timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err && echo "bench ok" && cat $O/bench.json &&

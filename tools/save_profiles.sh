@@ -17,7 +17,7 @@ cp $O/bench.json ${P}_bench.json
 cp $O/prof/run_kernel_stats.csv ${P}_kernel_stats.csv
 python tools/trace_summary.py $O/prof/run_kernel_trace.csv \
   "$R $V: rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu-baseline" > ${P}_kernel_trace_summary.txt
-for d in pmc pmc_c4 pmc_c3 pmc_c5; do
+for d in pmc pmc_c4 pmc_c3 pmc_c5 pmc_c1; do
   [ -d $O/$d ] || continue
   mkdir -p ${P}_$d
   for k in fetch sqa sqb sqc write; do
