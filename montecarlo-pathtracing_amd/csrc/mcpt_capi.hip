@@ -672,6 +672,8 @@ static int stream_run(mcpt_ctx* c, const mcpt::RenderParams& p) {
   // no faster on scenes 3/7/8 (random lanes' node reads conflict in the LDS banks, 11 conflict
   // cycles per LDS instruction; gpurun_out r03e/r03f)
   const bool lds_nodes = env_int("MCPT_STREAM_LDS_NODES", 0) != 0 && mcpt_stream_lds_nodes_fit(p.depth);
+  // two walks per lane in the trace kernel (walk_run2), measured, off by default
+  const bool dual = env_int("MCPT_STREAM_DUAL", 0) != 0;
   mcpt::StreamParams q[kStreamPools];
   unsigned* unit_ctr = c->d_sctr + mcpt::SC_UNIT;   // pool 0's slot: shared
   {
@@ -719,7 +721,7 @@ static int stream_run(mcpt_ctx* c, const mcpt::RenderParams& p) {
         if (done[j]) continue;
         q[j].parity = (int)(it & 1);
         q[j].compact = (k == 0 && compact[j]) ? 1 : 0;
-        HIP_OR_RETURN(mcpt_launch_stream_iter(q[j], c->n_cu, lds_nodes, c->pool_stream[j]));
+        HIP_OR_RETURN(mcpt_launch_stream_iter(q[j], c->n_cu, lds_nodes, dual, c->pool_stream[j]));
       }
     // every pool's counters after the batch, read on pool 0's stream once all pools are there
     for (int j = 1; j < np; ++j) {

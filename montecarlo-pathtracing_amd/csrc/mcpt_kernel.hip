@@ -684,6 +684,81 @@ __device__ __forceinline__ bool walk_run(const SR& s, f3 O, f3 D, Hit& h, Walk& 
   }
 }
 
+// Two independent per-lane walks, A and B, advanced together (the stream trace kernel's
+// MCPT_STREAM_DUAL build: the verdict's "two walks per lane" latency lever, measured in
+// DESIGN.md §4.1d).  A node iteration issues both walks' six rows before either walk's box
+// tests, so a lane keeps two dependent load chains in flight; a leaf iteration (batched over
+// both walks' waiting leaves, as walk_run) runs A's then B's primitive test.  run_a / run_b:
+// the walk is in progress (cleared when it completes).  Returns once at most `exit` walks of
+// the wave are still running and fewer than at entry, or when this lane has none.  Each walk's
+// own visit sequence is walk_run's (same bits).
+template <class SR>
+__device__ __forceinline__ void walk_run2(const SR& s, f3 oa, f3 da, Hit& ha, Walk& wa, bool& run_a, f3 ob, f3 db,
+                                          Hit& hb, Walk& wb, bool& run_b, int exit, int leaf_batch) {
+  Ev<false> ev;
+  const int leaf0 = (1 << s.depth) - 1;
+  auto walks = [&]() { return __builtin_popcountll(__ballot(run_a)) + __builtin_popcountll(__ballot(run_b)); };
+  const int n0 = walks();
+  auto node_step = [&](Walk& w, Hit& h, f3 O, f3 D, size_t j, float4 l0, float4 l1, float4 l2, float4 r0,
+                       float4 r1, float4 r2) {
+    const bool hl = l0.w != 0.0f && box_test<false>(l0, l1, l2, O, D, w.invD, h.cull2);
+    const bool hr = r0.w != 0.0f && box_test<false>(r0, r1, r2, O, D, w.invD, h.cull2);
+    if (hr) {
+      if (hl) w.pending |= 1u << (w.level + 1);
+      w.node = (int)j + 1; w.level++;
+    } else if (hl) {
+      w.node = (int)j; w.level++;
+    }
+    return !(hl || hr);
+  };
+  auto pop = [&](Walk& w, bool& run) {
+    if (w.pending == 0) { run = false; return; }
+    const int L = 31 - __builtin_clz(w.pending);
+    w.pending &= ~(1u << L);
+    w.node = ((w.node + 1) >> (w.level - L)) - 2;
+    w.level = L;
+  };
+  while (run_a || run_b) {
+    const bool lf_a = run_a && wa.node >= leaf0, lf_b = run_b && wb.node >= leaf0;
+    const int on_leaf = __builtin_popcountll(__ballot(lf_a)) + __builtin_popcountll(__ballot(lf_b));
+    const bool leaves = on_leaf >= leaf_batch || on_leaf == walks();   // wave-uniform
+    bool pop_a = false, pop_b = false;
+    if (leaves) {
+      if (lf_a) {
+        const int p = s.leaves[wa.node - leaf0];
+        if (p >= 0) prim_test<false, false, false>(s, p, oa, da, ha, ev);
+        pop_a = true;
+      }
+      if (lf_b) {
+        const int p = s.leaves[wb.node - leaf0];
+        if (p >= 0) prim_test<false, false, false>(s, p, ob, db, hb, ev);
+        pop_b = true;
+      }
+    } else {
+      const bool nd_a = run_a && !lf_a, nd_b = run_b && !lf_b;
+      const size_t ja = 2 * (size_t)(nd_a ? wa.node : 0) + 1, jb = 2 * (size_t)(nd_b ? wb.node : 0) + 1;
+      const float4* qa = s.nodes + ja * 3;
+      const float4* qb = s.nodes + jb * 3;
+      float4 a0 = qa[0], a1 = qa[1], a2 = qa[2], a3 = qa[3], a4 = qa[4], a5 = qa[5];
+      float4 b0 = qb[0], b1 = qb[1], b2 = qb[2], b3 = qb[3], b4 = qb[4], b5 = qb[5];
+      asm volatile("" : "+v"(a0.x), "+v"(a0.y), "+v"(a0.z), "+v"(a0.w), "+v"(a1.x), "+v"(a1.y), "+v"(a1.z),
+                   "+v"(a2.x), "+v"(a2.y), "+v"(a2.z));
+      asm volatile("" : "+v"(a3.x), "+v"(a3.y), "+v"(a3.z), "+v"(a3.w), "+v"(a4.x), "+v"(a4.y), "+v"(a4.z),
+                   "+v"(a5.x), "+v"(a5.y), "+v"(a5.z));
+      asm volatile("" : "+v"(b0.x), "+v"(b0.y), "+v"(b0.z), "+v"(b0.w), "+v"(b1.x), "+v"(b1.y), "+v"(b1.z),
+                   "+v"(b2.x), "+v"(b2.y), "+v"(b2.z));
+      asm volatile("" : "+v"(b3.x), "+v"(b3.y), "+v"(b3.z), "+v"(b3.w), "+v"(b4.x), "+v"(b4.y), "+v"(b4.z),
+                   "+v"(b5.x), "+v"(b5.y), "+v"(b5.z));
+      if (nd_a) pop_a = node_step(wa, ha, oa, da, ja, a0, a1, a2, a3, a4, a5);
+      if (nd_b) pop_b = node_step(wb, hb, ob, db, jb, b0, b1, b2, b3, b4, b5);
+    }
+    if (pop_a) pop(wa, run_a);
+    if (pop_b) pop(wb, run_b);
+    const int n = walks();
+    if (n <= exit && n < n0) return;
+  }
+}
+
 // walk_run for scenes with mesh instances.  The reference runs an instance's whole mesh DFS
 // (Mesh_intersect raytracer_func.frag:642-678) inside the scene DFS's leaf visit; nested that
 // way on the GPU, only the lanes sitting on a mesh leaf walk their (long, divergent) mesh
@@ -1753,8 +1828,14 @@ template <> struct TraceCfg<true> {
 // LDS of the LDSN trace kernel besides its scene copy: the waves' staged rays
 constexpr int kTraceLdsStaging = TraceCfg<true>::kWaves * TraceCfg<true>::kChunk * 32;
 
-template <bool LDSN>
-__global__ __launch_bounds__(TraceCfg<LDSN>::kBlock, TraceCfg<LDSN>::kMinWaves) void stream_trace_kernel(StreamParams q) {
+// DUAL (MCPT_STREAM_DUAL=1, L1/L2 nodes only): each lane walks two staged rays at once
+// (walk_run2), at MCPT_MIN_WAVES_STREAM_DUAL waves per SIMD.
+#ifndef MCPT_MIN_WAVES_STREAM_DUAL
+#define MCPT_MIN_WAVES_STREAM_DUAL 5
+#endif
+template <bool LDSN, bool DUAL = false>
+__global__ __launch_bounds__(TraceCfg<LDSN>::kBlock, DUAL ? MCPT_MIN_WAVES_STREAM_DUAL : TraceCfg<LDSN>::kMinWaves)
+void stream_trace_kernel(StreamParams q) {
   typedef TraceCfg<LDSN> C;
   constexpr int kChunkT = C::kChunk;
   const RenderParams& p = q.r;
@@ -1783,14 +1864,9 @@ __global__ __launch_bounds__(TraceCfg<LDSN>::kBlock, TraceCfg<LDSN>::kMinWaves) 
   bool more = true;          // wave-uniform: the queue may hold unclaimed entries
   Ev<false> ev;
   ev.init();
-  int r = -1;                // queue index of this lane's ray
-  f3 O = mk(0.0f, 0.0f, 0.0f), D = O;
-  Hit h;
-  h.pl = O; h.dist = kFLTMAX; h.clear(); h.tri = 0; h.cull2 = 0.0;
-  Walk w;
-  w.invD = O; w.node = 0; w.level = 0; w.pending = 0;
-  for (;;) {
-    // idle lanes take staged rays; an empty stage claims and stages the next chunk
+  // idle lanes take staged rays into slot (r, O, D, h, w); an empty stage claims and stages
+  // the next chunk
+  auto take = [&](int& r, f3& O, f3& D, Hit& h, Walk& w) {
     for (;;) {
       const uint64_t need = __ballot(r < 0);
       if (!need) break;
@@ -1854,13 +1930,41 @@ __global__ __launch_bounds__(TraceCfg<LDSN>::kBlock, TraceCfg<LDSN>::kMinWaves) 
       }
       cc += min(__builtin_popcountll(need), avail);
     }
-    if (__ballot(r >= 0) == 0) break;   // nothing staged and nothing left to claim
-    if (r >= 0) {
-      if (walk_run<false, true>(s, O, D, h, w, ev, q.refill, p.leaf_batch)) {
-        Q.set3(QF_HX, (uint32_t)r, h.pl);
-        Q.setu(QF_HCODE, (uint32_t)r, (uint32_t)h.code);
-        r = -1;
+  };
+  auto put_hit = [&](int r, const Hit& h) {
+    Q.set3(QF_HX, (uint32_t)r, h.pl);
+    Q.setu(QF_HCODE, (uint32_t)r, (uint32_t)h.code);
+  };
+  int r = -1;                // queue index of this lane's ray
+  f3 O = mk(0.0f, 0.0f, 0.0f), D = O;
+  Hit h;
+  h.pl = O; h.dist = kFLTMAX; h.clear(); h.tri = 0; h.cull2 = 0.0;
+  Walk w;
+  w.invD = O; w.node = 0; w.level = 0; w.pending = 0;
+  if constexpr (!DUAL) {
+    for (;;) {
+      take(r, O, D, h, w);
+      if (__ballot(r >= 0) == 0) break;   // nothing staged and nothing left to claim
+      if (r >= 0) {
+        if (walk_run<false, true>(s, O, D, h, w, ev, q.refill, p.leaf_batch)) {
+          put_hit(r, h);
+          r = -1;
+        }
       }
+    }
+  } else {
+    int r2 = -1;             // the lane's second ray
+    f3 O2 = O, D2 = O;
+    Hit h2 = h;
+    Walk w2 = w;
+    for (;;) {
+      take(r, O, D, h, w);
+      take(r2, O2, D2, h2, w2);
+      bool run_a = r >= 0, run_b = r2 >= 0;
+      if (__ballot(run_a || run_b) == 0) break;
+      if (run_a || run_b) walk_run2(s, O, D, h, w, run_a, O2, D2, h2, w2, run_b, 2 * q.refill, p.leaf_batch);
+      if (r >= 0 && !run_a) { put_hit(r, h); r = -1; }
+      if (r2 >= 0 && !run_b) { put_hit(r2, h2); r2 = -1; }
     }
   }
 #ifdef MCPT_STAMPS
@@ -2218,9 +2322,13 @@ bool mcpt_stream_lds_nodes_fit(int depth) {
   return depth <= 12 && mcpt_stream_lds_nodes_bytes(depth) + mcpt::kTraceLdsStaging <= 160 * 1024;
 }
 
-hipError_t mcpt_launch_stream_iter(const mcpt::StreamParams& q, int n_cu, bool lds_nodes, hipStream_t stream) {
+hipError_t mcpt_launch_stream_iter(const mcpt::StreamParams& q, int n_cu, bool lds_nodes, bool dual,
+                                   hipStream_t stream) {
   hipError_t e;
-  if (lds_nodes) {
+  if (dual && !lds_nodes) {   // persistent: MCPT_MIN_WAVES_STREAM_DUAL workgroups of 4 waves per CU
+    hipLaunchKernelGGL((mcpt::stream_trace_kernel<false, true>), dim3((unsigned)n_cu * MCPT_MIN_WAVES_STREAM_DUAL),
+                       dim3(mcpt::kStreamBlock), 0, stream, q);
+  } else if (lds_nodes) {
     const size_t shm = (size_t)mcpt_stream_lds_nodes_bytes(q.r.depth);
     // above the default 64 KiB of dynamic LDS (set on the calling thread's current device)
     e = hipFuncSetAttribute((const void*)mcpt::stream_trace_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
