@@ -434,6 +434,11 @@ def run_point(args, sr, rough, S, world, barrier, stat_dev):
         frame = sr.gather()
     barrier()
     kernel_ms, gather_ev = [], []
+    # the library keeps the HIP events of its last TIMING_RING render calls: the steps are
+    # queued back to back and their kernel times read once per half ring (one wait per 32
+    # steps) and after the loop, instead of a wait after every step (which exposed the launch
+    # latency of short steps: C1's 0.08 ms launches)
+    half = mcpt.Renderer.TIMING_RING // 2
     t0 = time.perf_counter()
     for k in range(args.warmup, args.warmup + args.steps):
         sr.render(ipv, iv, k * S + 1, S, 0.0, B, args.ior, mcpt.MONTECARLO)
@@ -443,8 +448,10 @@ def run_point(args, sr, rough, S, world, barrier, stat_dev):
         frame = sr.gather()
         e1.record(stream)
         gather_ev.append((e0, e1))
-        kernel_ms.append(sr.r.last_kernel_ms())   # HIP events of this call's launches (waits for the last)
+        if (k - args.warmup + 1) % half == 0:
+            kernel_ms.extend(sr.r.kernel_ms_back(b) for b in reversed(range(half)))
     barrier()
+    kernel_ms.extend(sr.r.kernel_ms_back(b) for b in reversed(range(args.steps % half)))
     elapsed = time.perf_counter() - t0
     sched = sr.r.schedule()   # what AUTO picked for this rank's timed launches
     launches = sr.r.last_launch_count()   # sub-launches of one timed call (segment-sum budget)

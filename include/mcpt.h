@@ -267,6 +267,10 @@ int mcpt_last_render_ms(mcpt_ctx* ctx, float* ms);
 /* The same interval split into the path-tracing kernel and the chunk-combine kernel
  * (launches spanning more than one 32-pass accumulation chunk). */
 int mcpt_last_kernel_ms(mcpt_ctx* ctx, float* trace_ms, float* combine_ms);
+/* The same for the render call `back` calls before the last (0: the last).  A context keeps the
+ * events of its last 64 calls, so a caller can queue a run of calls and read their times
+ * afterwards without waiting after each (waits for that call only). */
+int mcpt_kernel_ms_back(mcpt_ctx* ctx, int back, float* trace_ms, float* combine_ms);
 
 /* ---------------------------------------------------------------------------------
  * 2. host scene producer (BVH_GPU_Scene-compatible)

@@ -40,6 +40,8 @@ static int set_err(int status, const char* what, hipError_t e = hipSuccess) {
 // is one launch: +0.7 % against four launches under a 1 GiB bound, whose grid tails add up,
 // profiles/r03_ab_partial_budget_c5.jsonl; mcpt_set_partial_budget / MCPT_PARTIAL_BYTES)
 constexpr size_t kDefaultPartialBudget = size_t(4) << 30;
+// render calls whose events a context keeps (mcpt_kernel_ms_back)
+constexpr int kTimingRing = 64;
 
 struct mcpt_ctx {
   int device = 0;
@@ -72,9 +74,14 @@ struct mcpt_ctx {
   unsigned long long* d_events = nullptr;
   float* d_partial = nullptr;       // pass-segment sums (launches spanning > 1 chunk)
   size_t partial_bytes = 0;
-  // per sub-launch of the last render call: (start, after the path-tracing kernel, after the
-  // combine kernel); a call is split into sub-launches at chunk boundaries (partial_budget)
-  std::vector<hipEvent_t> evs;
+  // per sub-launch of a render call: (start, after the path-tracing kernel, after the combine
+  // kernel); a call is split into sub-launches at chunk boundaries (partial_budget).  The last
+  // kTimingRing calls keep their events (mcpt_kernel_ms_back), so a caller can time a run of
+  // calls without waiting after each; ring_pos = the last call's slot.
+  std::vector<hipEvent_t> evs[kTimingRing];
+  int ring_n_sub[kTimingRing] = {};
+  int ring_pos = 0;
+  long long n_timed = 0;            // render calls timed so far
   int n_sub = 0;                    // sub-launches of the last render call
   int pass_split = 0;               // the last render call ran one segment per pass (launch())
   bool timed = false;
@@ -114,31 +121,37 @@ struct mcpt_ctx {
   long long stream_iters = 0;       // iterations of the last stream render (diagnostics)
 };
 
-// events of sub-launch k: start / mid / stop
-static hipEvent_t ev_start(const mcpt_ctx* c, int k) { return c->evs[3 * k]; }
-static hipEvent_t ev_mid(const mcpt_ctx* c, int k) { return c->evs[3 * k + 1]; }
-static hipEvent_t ev_stop(const mcpt_ctx* c, int k) { return c->evs[3 * k + 2]; }
-static hipError_t ensure_events(mcpt_ctx* c, int n_sub) {
-  while ((int)c->evs.size() < 3 * n_sub) {
+// events of sub-launch k of the last call: start / mid / stop
+static hipEvent_t ev_start(const mcpt_ctx* c, int k) { return c->evs[c->ring_pos][3 * k]; }
+static hipEvent_t ev_mid(const mcpt_ctx* c, int k) { return c->evs[c->ring_pos][3 * k + 1]; }
+static hipEvent_t ev_stop(const mcpt_ctx* c, int k) { return c->evs[c->ring_pos][3 * k + 2]; }
+static hipError_t ensure_events(mcpt_ctx* c, int slot, int n_sub) {
+  while ((int)c->evs[slot].size() < 3 * n_sub) {
     hipEvent_t e = nullptr;
     hipError_t r = hipEventCreate(&e);
     if (r != hipSuccess) return r;
-    c->evs.push_back(e);
+    c->evs[slot].push_back(e);
   }
   return hipSuccess;
 }
-// (path-tracing kernel ms, combine kernel ms) summed over the sub-launches of the last call
-static hipError_t sub_launch_ms(const mcpt_ctx* c, float* trace_ms, float* combine_ms) {
+// (path-tracing kernel ms, combine kernel ms) summed over the sub-launches of the call in ring
+// slot `slot` (waits for it)
+static hipError_t slot_launch_ms(const mcpt_ctx* c, int slot, float* trace_ms, float* combine_ms) {
   *trace_ms = 0.0f; *combine_ms = 0.0f;
-  for (int k = 0; k < c->n_sub; ++k) {
+  const std::vector<hipEvent_t>& v = c->evs[slot];
+  for (int k = 0; k < c->ring_n_sub[slot]; ++k) {
     float a = 0.0f, b = 0.0f;
-    hipError_t e = hipEventSynchronize(ev_stop(c, k));
-    if (e == hipSuccess) e = hipEventElapsedTime(&a, ev_start(c, k), ev_mid(c, k));
-    if (e == hipSuccess) e = hipEventElapsedTime(&b, ev_mid(c, k), ev_stop(c, k));
+    hipError_t e = hipEventSynchronize(v[3 * k + 2]);
+    if (e == hipSuccess) e = hipEventElapsedTime(&a, v[3 * k], v[3 * k + 1]);
+    if (e == hipSuccess) e = hipEventElapsedTime(&b, v[3 * k + 1], v[3 * k + 2]);
     if (e != hipSuccess) return e;
     *trace_ms += a; *combine_ms += b;
   }
   return hipSuccess;
+}
+// the same for the last call
+static hipError_t sub_launch_ms(const mcpt_ctx* c, float* trace_ms, float* combine_ms) {
+  return slot_launch_ms(c, c->ring_pos, trace_ms, combine_ms);
 }
 
 static int env_int(const char* name, int dflt) {
@@ -290,7 +303,7 @@ int mcpt_create(int device_ordinal, mcpt_ctx** out) {
       c->n_cu <= 0)
     c->n_cu = 256;
   hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
-  if (e == hipSuccess) e = ensure_events(c, 1);
+  if (e == hipSuccess) e = ensure_events(c, 0, 1);
   if (const char* pb = std::getenv("MCPT_PARTIAL_BYTES")) c->partial_budget = (size_t)std::strtoull(pb, nullptr, 10);
   if (e == hipSuccess) e = hipMalloc(&c->d_events, sizeof(unsigned long long) * MCPT_DEBUG_SLOTS);
   if (e == hipSuccess) e = hipMemset(c->d_events, 0, sizeof(unsigned long long) * MCPT_DEBUG_SLOTS);
@@ -331,7 +344,8 @@ int mcpt_destroy(mcpt_ctx* c) {
   for (hipEvent_t e : c->batch_ev) if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->pool_ev) if (e) (void)hipEventDestroy(e);
   for (hipStream_t st : c->pool_stream) if (st) (void)hipStreamDestroy(st);
-  for (hipEvent_t e : c->evs) (void)hipEventDestroy(e);
+  for (const std::vector<hipEvent_t>& v : c->evs)
+    for (hipEvent_t e : v) (void)hipEventDestroy(e);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
   return MCPT_OK;
@@ -847,7 +861,8 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
     const long long c0 = fdiv((int)(lo - 1), mcpt::kPassChunk);
     lo = split ? end : std::min(end, (c0 + max_seg) * mcpt::kPassChunk + 1);
   }
-  HIP_OR_RETURN(ensure_events(c, std::max(n_sub, 1)));
+  const int slot = (c->ring_pos + 1) % kTimingRing;   // this call's events (ring of calls)
+  HIP_OR_RETURN(ensure_events(c, slot, std::max(n_sub, 1)));
   const long long segs = split ? n_passes : std::min(max_seg, total_seg);   // most segments of one sub-launch
   if (segs > 1 && (size_t)segs * (size_t)seg_bytes > c->partial_bytes) {
     const size_t need = (size_t)segs * (size_t)seg_bytes;
@@ -869,6 +884,9 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
     c->tune_shape[1] = n_passes;
   }
   c->n_sub = std::max(n_sub, 1);
+  c->ring_pos = slot;
+  c->ring_n_sub[slot] = c->n_sub;
+  c->n_timed++;
   c->pass_split = split ? 1 : 0;
   if (n_sub == 0) {   // no passes: an empty timed interval
     HIP_OR_RETURN(hipEventRecord(ev_start(c, 0), c->stream));
@@ -1189,6 +1207,15 @@ int mcpt_last_render_ms(mcpt_ctx* c, float* ms) {
   HIP_OR_RETURN(hipSetDevice(c->device));
   HIP_OR_RETURN(hipEventSynchronize(ev_stop(c, c->n_sub - 1)));
   HIP_OR_RETURN(hipEventElapsedTime(ms, ev_start(c, 0), ev_stop(c, c->n_sub - 1)));
+  return MCPT_OK;
+}
+
+int mcpt_kernel_ms_back(mcpt_ctx* c, int back, float* trace_ms, float* combine_ms) {
+  if (!c || !trace_ms || !combine_ms) return MCPT_ERR_INVALID_ARG;
+  if (back < 0 || back >= kTimingRing || back >= c->n_timed)
+    return set_err(MCPT_ERR_INVALID_ARG, "mcpt_kernel_ms_back: no such call in the timing ring");
+  HIP_OR_RETURN(hipSetDevice(c->device));
+  HIP_OR_RETURN(slot_launch_ms(c, (c->ring_pos - back + kTimingRing) % kTimingRing, trace_ms, combine_ms));
   return MCPT_OK;
 }
 

@@ -112,6 +112,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "mcpt_synchronize": (i, [_vp]),
         "mcpt_last_render_ms": (i, [_vp, fp]),
         "mcpt_last_kernel_ms": (i, [_vp, fp, fp]),
+        "mcpt_kernel_ms_back": (i, [_vp, ctypes.c_int, fp, fp]),
         "mcpt_scene_create": (i, [ctypes.POINTER(_vp)]),
         "mcpt_scene_destroy": (i, [_vp]),
         "mcpt_scene_clear": (i, [_vp]),
@@ -637,4 +638,14 @@ class Renderer:
         """(path-tracing kernel ms, chunk-combine kernel ms) of the last render."""
         a, b = ctypes.c_float(), ctypes.c_float()
         _check(lib().mcpt_last_kernel_ms(self._h, ctypes.byref(a), ctypes.byref(b)), "mcpt_last_kernel_ms")
+        return a.value, b.value
+
+    # render calls whose kernel times a context keeps (mcpt_kernel_ms_back)
+    TIMING_RING = 64
+
+    def kernel_ms_back(self, back: int) -> Tuple[float, float]:
+        """mcpt_kernel_ms_back: (path-tracing ms, combine ms) of the render call `back` calls
+        before the last (0: the last; < TIMING_RING); waits for that call only."""
+        a, b = ctypes.c_float(), ctypes.c_float()
+        _check(lib().mcpt_kernel_ms_back(self._h, int(back), ctypes.byref(a), ctypes.byref(b)), "mcpt_kernel_ms_back")
         return a.value, b.value

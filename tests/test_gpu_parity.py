@@ -516,3 +516,26 @@ def test_auto_two_round_trials_settle(mcpt_mod, renderer, scene_id, n_cand):
     assert all(s["settled"] and s["traversal"] == "lane" for s in fixed)
     assert n_a == n_l
     assert np.array_equal(auto.view(np.uint32), lane.view(np.uint32))
+
+
+def test_kernel_ms_back_ring(mcpt_mod, renderer):
+    """mcpt_kernel_ms_back: the events of the last TIMING_RING calls are kept; a call further
+    back (or before any call) is an error."""
+    W, H = 64, 40
+    renderer.set_traversal(1)
+    renderer.upload_scene(mcpt_mod.Scene.reference(6))
+    renderer.set_target(W, H)
+    ipv, iv = mcpt_mod.camera_canonical(W, H)
+    for k in range(3):
+        renderer.render(ipv, iv, 1 + 8 * k, 8 * (k + 1), 0.0, 8, 1.0, 0)   # 8, 16, 24 passes
+    t = [renderer.kernel_ms_back(b)[0] for b in (2, 1, 0)]
+    assert all(x > 0.0 for x in t)
+    assert renderer.kernel_ms_back(0) == renderer.last_kernel_ms()
+    with pytest.raises(RuntimeError):
+        renderer.kernel_ms_back(mcpt_mod.Renderer.TIMING_RING)
+    r2 = mcpt_mod.Renderer(0)
+    try:
+        with pytest.raises(RuntimeError):
+            r2.kernel_ms_back(0)
+    finally:
+        r2.close()
