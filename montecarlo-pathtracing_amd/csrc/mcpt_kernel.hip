@@ -251,9 +251,15 @@ __device__ __forceinline__ bool box_test(float4 a0, float4 a1, float4 a2, f3 O, 
 // profiles/r03_ab_node_loads_together.jsonl).  Same values, same bits.  The LDS-scene kernels
 // (ds_read latency is short: -1 % with the rows together) and the mesh kernels (128-VGPR walk
 // state: they spill) keep the lazy form.
+// The asm takes the rows as inputs only (1): it defines no new values, so the register
+// allocator keeps the rows in their load tuples.  With in-out operands (2, the first form) it
+// copied 11 of them out per node visit (v_mov; the deep walk's node block 17 -> 6 VALU outside
+// the box tests): scene 8 +1.4..1.7 %, scenes 3/5/7 -1.3..+1.9 %
+// (profiles/r03_ab_node_loads_inputs.jsonl).
 #ifndef MCPT_NODE_LOADS_TOGETHER
 #define MCPT_NODE_LOADS_TOGETHER 1
 #endif
+#define MCPT_ROWS_IN(...) asm volatile("" ::__VA_ARGS__)
 #ifndef MCPT_PRIM_TRF_EARLY
 #define MCPT_PRIM_TRF_EARLY 0
 #endif
@@ -263,10 +269,17 @@ __device__ __forceinline__ void node_tests(const SR& s, const float4* __restrict
   if constexpr (MCPT_NODE_LOADS_TOGETHER && !SR::kLds && !SR::kMesh) {
     const float4* q = nodes + j * 3;
     float4 l0 = q[0], l1 = q[1], l2 = q[2], r0 = q[3], r1 = q[4], r2 = q[5];
+#if MCPT_NODE_LOADS_TOGETHER == 1
+    MCPT_ROWS_IN("v"(l0.x), "v"(l0.y), "v"(l0.z), "v"(l0.w), "v"(l1.x), "v"(l1.y), "v"(l1.z), "v"(l2.x),
+                 "v"(l2.y), "v"(l2.z));
+    MCPT_ROWS_IN("v"(r0.x), "v"(r0.y), "v"(r0.z), "v"(r0.w), "v"(r1.x), "v"(r1.y), "v"(r1.z), "v"(r2.x),
+                 "v"(r2.y), "v"(r2.z));
+#else
     asm volatile("" : "+v"(l0.x), "+v"(l0.y), "+v"(l0.z), "+v"(l0.w), "+v"(l1.x), "+v"(l1.y), "+v"(l1.z),
                  "+v"(l2.x), "+v"(l2.y), "+v"(l2.z));
     asm volatile("" : "+v"(r0.x), "+v"(r0.y), "+v"(r0.z), "+v"(r0.w), "+v"(r1.x), "+v"(r1.y), "+v"(r1.z),
                  "+v"(r2.x), "+v"(r2.y), "+v"(r2.z));
+#endif
     hl = (COUNT || l0.w != 0.0f) && box_test<false>(l0, l1, l2, O, D, invD, cull2);
     hr = (COUNT || r0.w != 0.0f) && box_test<false>(r0, r1, r2, O, D, invD, cull2);
   } else {
@@ -429,8 +442,13 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
   const size_t b = (size_t)i * 8;
   float4 r0 = ld4<U>(s.prims, b), r1 = ld4<U>(s.prims, b + 1), r2 = ld4<U>(s.prims, b + 2);
   if constexpr (kTogether) {
+#if MCPT_NODE_LOADS_TOGETHER == 1
+    MCPT_ROWS_IN("v"(pt), "v"(r0.x), "v"(r0.y), "v"(r0.z), "v"(r0.w), "v"(r1.x), "v"(r1.y), "v"(r1.z),
+                 "v"(r1.w), "v"(r2.x), "v"(r2.y), "v"(r2.z), "v"(r2.w));
+#else
     asm volatile("" : "+v"(pt), "+v"(r0.x), "+v"(r0.y), "+v"(r0.z), "+v"(r0.w), "+v"(r1.x), "+v"(r1.y),
                  "+v"(r1.z), "+v"(r1.w), "+v"(r2.x), "+v"(r2.y), "+v"(r2.z), "+v"(r2.w));
+#endif
   }
   // MCPT_PRIM_TRF_EARLY: the transform rows a candidate needs ride in the same round trip
   constexpr bool kTrfEarly = kTogether && MCPT_PRIM_TRF_EARLY;
