@@ -260,6 +260,25 @@ __device__ __forceinline__ bool box_test(float4 a0, float4 a1, float4 a2, f3 O, 
 #define MCPT_NODE_LOADS_TOGETHER 1
 #endif
 #define MCPT_ROWS_IN(...) asm volatile("" ::__VA_ARGS__)
+// Row k of a per-lane record array at a 32-bit byte offset from the array's wave-uniform base
+// (n_prims < 2^24 keeps every node and primitive row below 2^31 bytes): the load takes the
+// base from SGPRs with a 32-bit lane offset (global_load ... saddr) instead of a 64-bit VALU
+// address per visit (MCPT_ROW_OFFSET32=0: the 64-bit form).
+#ifndef MCPT_ROW_OFFSET32
+#define MCPT_ROW_OFFSET32 1
+#endif
+__device__ __forceinline__ const float4* row_ptr(const float4* __restrict__ base, size_t k) {
+  if (MCPT_ROW_OFFSET32) return (const float4*)((const char*)base + (uint32_t)k * 16u);
+  return base + k;
+}
+// the two child records of a node pair j (rows 3j .. 3j+5): byte offset 48 j, with j * 3 as
+// one full-rate shift-add (LLVM turns * 48 into v_mul_lo_u32, a quarter-rate instruction)
+__device__ __forceinline__ const float4* node_rows(const float4* __restrict__ nodes, size_t j) {
+  if (!MCPT_ROW_OFFSET32) return nodes + j * 3;
+  uint32_t t;
+  asm("v_lshl_add_u32 %0, %1, 1, %1" : "=v"(t) : "v"((uint32_t)j));
+  return (const float4*)((const char*)nodes + (t << 4));
+}
 #ifndef MCPT_PRIM_TRF_EARLY
 #define MCPT_PRIM_TRF_EARLY 0
 #endif
@@ -267,7 +286,7 @@ template <bool COUNT, class SR>
 __device__ __forceinline__ void node_tests(const SR& s, const float4* __restrict__ nodes, size_t j, f3 O, f3 D,
                                            f3 invD, double cull2, bool& hl, bool& hr) {
   if constexpr (MCPT_NODE_LOADS_TOGETHER && !SR::kLds && !SR::kMesh) {
-    const float4* q = nodes + j * 3;
+    const float4* q = node_rows(nodes, j);
     float4 l0 = q[0], l1 = q[1], l2 = q[2], r0 = q[3], r1 = q[4], r2 = q[5];
 #if MCPT_NODE_LOADS_TOGETHER == 1
     MCPT_ROWS_IN("v"(l0.x), "v"(l0.y), "v"(l0.z), "v"(l0.w), "v"(l1.x), "v"(l1.y), "v"(l1.z), "v"(l2.x),
@@ -435,12 +454,18 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
   // per-lane L1/L2 reads (node_tests): the type code and the inverse rows in one round trip,
   // else the rows' loads wait behind the type test
   constexpr bool kTogether = MCPT_NODE_LOADS_TOGETHER && !U && !SR::kLds && !SR::kMesh;
-  int pt = ld1<U>(s.ptype, i);
+  int pt = kTogether && MCPT_ROW_OFFSET32 ? s.ptype[(uint32_t)i] : ld1<U>(s.ptype, i);
   if constexpr (!kTogether) {
     if (pt < 0) return;
   }
   const size_t b = (size_t)i * 8;
-  float4 r0 = ld4<U>(s.prims, b), r1 = ld4<U>(s.prims, b + 1), r2 = ld4<U>(s.prims, b + 2);
+  float4 r0, r1, r2;
+  if constexpr (kTogether) {
+    const float4* q = row_ptr(s.prims, b);
+    r0 = q[0]; r1 = q[1]; r2 = q[2];
+  } else {
+    r0 = ld4<U>(s.prims, b); r1 = ld4<U>(s.prims, b + 1); r2 = ld4<U>(s.prims, b + 2);
+  }
   if constexpr (kTogether) {
 #if MCPT_NODE_LOADS_TOGETHER == 1
     MCPT_ROWS_IN("v"(pt), "v"(r0.x), "v"(r0.y), "v"(r0.z), "v"(r0.w), "v"(r1.x), "v"(r1.y), "v"(r1.z),
@@ -660,7 +685,7 @@ __device__ __forceinline__ bool walk_run(const SR& s, f3 O, f3 D, Hit& h, Walk& 
 #endif
     if (do_leaf) {
       ev.inc(EV_LEAF);
-      int p = s.leaves[w.node - leaf0];
+      int p = s.leaves[MCPT_ROW_OFFSET32 ? (size_t)(uint32_t)(w.node - leaf0) : (size_t)(w.node - leaf0)];
       if (p >= 0) prim_test<COUNT, false, false>(s, p, O, D, h, ev);
     }
 #ifdef MCPT_STAMPS
