@@ -154,6 +154,10 @@ int mcpt_debug_counters(mcpt_ctx* ctx, unsigned long long* out, int reset);
  * Synchronizes the context's stream. */
 int mcpt_read_accum(mcpt_ctx* ctx, float* rgb_out, int* pass_count);
 int mcpt_clear_accum(mcpt_ctx* ctx);
+/* The inverse of mcpt_read_accum: load n_local_rows × W × 3 f32 sums and the number of passes
+ * they hold into the context's accumulator; later renders add to them (resuming a progressive
+ * render from a checkpoint, mcpt_checkpoint_read).  Synchronizes the context's stream. */
+int mcpt_write_accum(mcpt_ctx* ctx, const float* rgb, int pass_count);
 
 /* Device pointer of the local accumulator (for an RCCL gather by the caller). */
 int mcpt_accum_device_ptr(mcpt_ctx* ctx, void** dev_ptr, size_t* bytes);
@@ -333,6 +337,26 @@ int mcpt_average(const float* accum, long long n_values, int pass_count, float* 
 int mcpt_write_pfm(const char* path, const float* rgb, int W, int H);
 /* what the 8-bit default framebuffer shows: clamp to [0,1], round(255·c), no gamma; PNG RGB8 */
 int mcpt_write_png(const char* path, const float* rgb, int W, int H);
+
+/* Checkpoint / resume of a progressive render: the reference's pass loop
+ * (montecarlo.cpp:454-466) accumulates into one framebuffer for as long as the window stays
+ * open; here a long render (C5: 84,000 passes) can stop and continue in another process with
+ * the same bits, because a pass's samples depend only on (pixel, pass, date) and the
+ * accumulator is additive.  A file holds the accumulator sums (rows × W × RGB f32, as
+ * mcpt_read_accum returns them), the passes they hold, the first pass of the next render call,
+ * and a caller tag (scene and render parameters) that the reader compares.
+ * Layout, little endian: "MCPTCKP1", int32 W, rows, pass_count, next_pass, tag bytes, the tag,
+ * then the floats.  The write goes to `path`.tmp and is renamed over `path`, so an
+ * interrupted write leaves the previous checkpoint intact. */
+#define MCPT_CHECKPOINT_TAG_MAX 1024
+int mcpt_checkpoint_write(const char* path, const float* rgb, int W, int rows, int pass_count, int next_pass,
+                          const char* tag);
+/* Reads the header into W, rows, pass_count, next_pass (any may be NULL) and the tag into tag_out
+ * (MCPT_CHECKPOINT_TAG_MAX bytes, NUL-terminated; may be NULL); the sums into rgb_out
+ * (rows × W × 3 floats) unless it is NULL.  MCPT_ERR_INVALID_ARG for a missing, foreign or
+ * truncated file. */
+int mcpt_checkpoint_read(const char* path, float* rgb_out, int* W, int* rows, int* pass_count, int* next_pass,
+                         char* tag_out);
 
 #ifdef __cplusplus
 }

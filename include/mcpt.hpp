@@ -350,6 +350,31 @@ class Renderer {
     check(mcpt_read_accum(c_, rgb.data(), &n), "mcpt_read_accum");
     return n;
   }
+  // the inverse of read_accum (resume): local rows × W × 3 sums holding `passes` passes
+  void write_accum(const std::vector<float>& rgb, int passes) {
+    if (rgb.size() != (size_t)rows_ * W_ * 3) throw Error("write_accum: wrong size", MCPT_ERR_INVALID_ARG);
+    check(mcpt_write_accum(c_, rgb.data(), passes), "mcpt_write_accum");
+  }
+  // checkpoint / resume of a progressive render (mcpt_checkpoint_write / _read): the file holds
+  // the sums, their pass count, the next call's first pass and a tag of the render parameters
+  void save_checkpoint(const std::string& path, int next_pass, const std::string& tag) const {
+    std::vector<float> acc;
+    const int n = read_accum(acc);
+    check(mcpt_checkpoint_write(path.c_str(), acc.data(), W_, rows_, n, next_pass, tag.c_str()),
+          "mcpt_checkpoint_write");
+  }
+  // returns the next first pass; throws if the file's shape or tag differs from this render's
+  int load_checkpoint(const std::string& path, const std::string& tag) {
+    int w = 0, rows = 0, n = 0, next = 0;
+    std::vector<char> t(MCPT_CHECKPOINT_TAG_MAX);
+    check(mcpt_checkpoint_read(path.c_str(), nullptr, &w, &rows, nullptr, nullptr, nullptr), "mcpt_checkpoint_read");
+    if (w != W_ || rows != rows_) throw Error("checkpoint: framebuffer shape differs", MCPT_ERR_INVALID_ARG);
+    std::vector<float> acc((size_t)rows * w * 3);
+    check(mcpt_checkpoint_read(path.c_str(), acc.data(), nullptr, nullptr, &n, &next, t.data()), "mcpt_checkpoint_read");
+    if (tag != t.data()) throw Error("checkpoint: render parameters differ (" + std::string(t.data()) + ")", MCPT_ERR_INVALID_ARG);
+    write_accum(acc, n);
+    return next;
+  }
   // fs_frag: the averaged image (single-shard target)
   std::vector<float> read_image() const {
     std::vector<float> acc;

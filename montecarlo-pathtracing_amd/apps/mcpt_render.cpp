@@ -3,7 +3,8 @@
 //
 // Builds one of the 8 reference scenes (keys Q..I = 1..8), accumulates passes with the
 // reference's uniform ABI (numero_pass, date, NB_BOUNCES, refract_ind, shader variant),
-// progressively in chunks like the "lock" mode, then writes the averaged image (fs_frag,
+// progressively in chunks like the "lock" mode (optionally writing a checkpoint after each
+// chunk, and resuming from one), then writes the averaged image (fs_frag,
 // montecarlo.cpp:59-70) as PFM (float) and/or PNG (8-bit framebuffer view).  Prints one JSON
 // line with the timing.  Host C++ over the C ABI (include/mcpt.hpp); no CPU fallback.
 //
@@ -34,6 +35,7 @@ struct Args {
   int device = 0, subsampling = 0, variant = MCPT_MONTECARLO, traversal = MCPT_TRAVERSAL_AUTO;
   float ior = 1.0f, light = 1.2f, date = 0.0f;
   std::string png, pfm;
+  std::string checkpoint, resume;   // --checkpoint FILE (after every chunk), --resume FILE
   std::vector<int> devices;   // --devices: one shard per entry
 };
 
@@ -56,7 +58,8 @@ void usage() {
                "                   [--spp S] [--first-pass P] [--chunk C] [--bounces B] [--ior R]\n"
                "                   [--light L] [--date T] [--variant montecarlo|mat|mat_tr]\n"
                "                   [--traversal auto|lane|wave|stream] [--device D | --devices D0,D1,...]\n"
-               "                   [--out img.png] [--pfm img.pfm]\n");
+               "                   [--out img.png] [--pfm img.pfm]\n"
+               "                   [--checkpoint state.ckpt] [--resume state.ckpt]   (one device)\n");
 }
 
 bool parse(int argc, char** argv, Args& a) {
@@ -82,6 +85,8 @@ bool parse(int argc, char** argv, Args& a) {
     }
     else if (k == "--out") a.png = v;
     else if (k == "--pfm") a.pfm = v;
+    else if (k == "--checkpoint") a.checkpoint = v;
+    else if (k == "--resume") a.resume = v;
     else if (k == "--variant") {
       const std::string s = v;
       a.variant = s == "mat" ? MCPT_MAT : (s == "mat_tr" ? MCPT_MAT_TR : MCPT_MONTECARLO);
@@ -96,6 +101,7 @@ bool parse(int argc, char** argv, Args& a) {
       return false;
     }
   }
+  if (!a.devices.empty() && (!a.checkpoint.empty() || !a.resume.empty())) return false;   // one device only
   return a.width > 0 && a.height > 0 && a.spp >= 0 && a.chunk > 0 && a.subsampling >= 0 && a.subsampling < 16;
 }
 
@@ -123,11 +129,20 @@ int main(int argc, char** argv) {
       r.set_traversal(a.traversal);
       r.upload(scene);
       r.set_target(W, H);
+      // checkpoint / resume: --spp counts the whole render's passes (first_pass .. first_pass +
+      // spp - 1); a resumed run continues at the checkpoint's next pass with its sums loaded,
+      // and the tag makes a resume with other render parameters fail
+      char tag[256];
+      std::snprintf(tag, sizeof(tag), "scene=%d W=%d H=%d bounces=%d ior=%a light=%a date=%a variant=%d first=%d",
+                    a.scene, W, H, a.bounces, a.ior, a.light, a.date, a.variant, a.first_pass);
+      int next = a.first_pass;
+      if (!a.resume.empty()) next = r.load_checkpoint(a.resume, tag);
       const auto t0 = std::chrono::steady_clock::now();
-      for (int done = 0; done < a.spp; done += a.chunk) {
+      for (int done = next - a.first_pass; done < a.spp; done += a.chunk) {
         const int n = std::min(a.chunk, a.spp - done);
         r.render(cam, a.first_pass + done, n, a.date, a.bounces, a.ior, a.variant);
         kernel_ms += r.last_render_ms();
+        if (!a.checkpoint.empty()) r.save_checkpoint(a.checkpoint, a.first_pass + done + n, tag);
       }
       img = r.read_image();
       wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

@@ -959,6 +959,17 @@ int mcpt_read_accum(mcpt_ctx* c, float* rgb_out, int* pass_count) {
   return MCPT_OK;
 }
 
+int mcpt_write_accum(mcpt_ctx* c, const float* rgb, int pass_count) {
+  if (!c || !rgb || pass_count < 0) return MCPT_ERR_INVALID_ARG;
+  if (!c->has_target) return MCPT_ERR_NO_TARGET;
+  HIP_OR_RETURN(hipSetDevice(c->device));
+  if (c->accum_bytes)
+    HIP_OR_RETURN(hipMemcpyAsync(c->d_accum, rgb, c->accum_bytes, hipMemcpyHostToDevice, c->stream));
+  HIP_OR_RETURN(hipStreamSynchronize(c->stream));
+  c->pass_count = pass_count;
+  return MCPT_OK;
+}
+
 int mcpt_accum_device_ptr(mcpt_ctx* c, void** dev_ptr, size_t* bytes) {
   if (!c || !dev_ptr) return MCPT_ERR_INVALID_ARG;
   if (!c->has_target) return MCPT_ERR_NO_TARGET;

@@ -8,6 +8,8 @@
 //  * mcpt_write_png: what the default framebuffer shows: each channel clamped to [0,1] and
 //    converted to 8-bit unorm by round(255·c) (GL float→unorm rule, no gamma), written as an
 //    8-bit RGB PNG (top row first) with stored (uncompressed) deflate blocks.
+//  * mcpt_checkpoint_write / _read: a progressive render's accumulator, pass count and next
+//    first pass in one file, so the pass loop (montecarlo.cpp:454-466) can stop and resume.
 //  * mcpt_transfo_*, mcpt_mat4_mul: easycppogl Transfo (gl_eigen.cpp:29-105, degrees) and
 //    Eigen's float product, evaluated with the same arithmetic as the scene producer, so a
 //    C++ caller composing transforms gets the reference's matrices bit for bit.
@@ -16,6 +18,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "../../include/mcpt.h"
@@ -125,6 +128,56 @@ int mcpt_write_png(const char* path, const float* rgb, int W, int H) {
   if (!f) return MCPT_ERR_INVALID_ARG;
   const bool ok = std::fwrite(out.data(), 1, out.size(), f) == out.size();
   return (std::fclose(f) == 0 && ok) ? MCPT_OK : MCPT_ERR_INVALID_ARG;
+}
+
+// checkpoint file (mcpt.h): magic, 5 int32 (W, rows, pass_count, next_pass, tag bytes), tag, floats
+static const char kCkptMagic[8] = {'M', 'C', 'P', 'T', 'C', 'K', 'P', '1'};
+
+int mcpt_checkpoint_write(const char* path, const float* rgb, int W, int rows, int pass_count, int next_pass,
+                          const char* tag) {
+  if (!path || !rgb || W <= 0 || rows <= 0 || pass_count < 0) return MCPT_ERR_INVALID_ARG;
+  const size_t tag_len = tag ? std::strlen(tag) : 0;
+  if (tag_len >= MCPT_CHECKPOINT_TAG_MAX) return MCPT_ERR_INVALID_ARG;
+  const std::string tmp = std::string(path) + ".tmp";
+  FILE* f = std::fopen(tmp.c_str(), "wb");
+  if (!f) return MCPT_ERR_INVALID_ARG;
+  const int32_t hdr[5] = {W, rows, pass_count, next_pass, (int32_t)tag_len};
+  const size_t n = (size_t)W * rows * 3;
+  bool ok = std::fwrite(kCkptMagic, 1, 8, f) == 8 && std::fwrite(hdr, sizeof(int32_t), 5, f) == 5 &&
+            std::fwrite(tag ? tag : "", 1, tag_len, f) == tag_len && std::fwrite(rgb, sizeof(float), n, f) == n;
+  ok = (std::fclose(f) == 0) && ok;
+  if (!ok || std::rename(tmp.c_str(), path) != 0) {
+    std::remove(tmp.c_str());
+    return MCPT_ERR_INVALID_ARG;
+  }
+  return MCPT_OK;
+}
+
+int mcpt_checkpoint_read(const char* path, float* rgb_out, int* W, int* rows, int* pass_count, int* next_pass,
+                         char* tag_out) {
+  if (!path) return MCPT_ERR_INVALID_ARG;
+  FILE* f = std::fopen(path, "rb");
+  if (!f) return MCPT_ERR_INVALID_ARG;
+  char magic[8];
+  int32_t hdr[5];
+  char tag[MCPT_CHECKPOINT_TAG_MAX];
+  bool ok = std::fread(magic, 1, 8, f) == 8 && std::memcmp(magic, kCkptMagic, 8) == 0 &&
+            std::fread(hdr, sizeof(int32_t), 5, f) == 5 && hdr[0] > 0 && hdr[1] > 0 && hdr[2] >= 0 &&
+            hdr[4] >= 0 && hdr[4] < MCPT_CHECKPOINT_TAG_MAX &&
+            std::fread(tag, 1, (size_t)hdr[4], f) == (size_t)hdr[4];
+  if (ok && rgb_out) {
+    const size_t n = (size_t)hdr[0] * hdr[1] * 3;
+    ok = std::fread(rgb_out, sizeof(float), n, f) == n;
+  }
+  std::fclose(f);
+  if (!ok) return MCPT_ERR_INVALID_ARG;
+  tag[hdr[4]] = '\0';
+  if (W) *W = hdr[0];
+  if (rows) *rows = hdr[1];
+  if (pass_count) *pass_count = hdr[2];
+  if (next_pass) *next_pass = hdr[3];
+  if (tag_out) std::memcpy(tag_out, tag, (size_t)hdr[4] + 1);
+  return MCPT_OK;
 }
 
 int mcpt_transfo_translate(float x, float y, float z, float* out16) {

@@ -142,6 +142,9 @@ def _declare(L: ctypes.CDLL) -> None:
         "mcpt_average": (i, [fp, ctypes.c_longlong, i, fp]),
         "mcpt_write_pfm": (i, [ctypes.c_char_p, fp, i, i]),
         "mcpt_write_png": (i, [ctypes.c_char_p, fp, i, i]),
+        "mcpt_write_accum": (i, [_vp, fp, i]),
+        "mcpt_checkpoint_write": (i, [ctypes.c_char_p, fp, i, i, i, i, ctypes.c_char_p]),
+        "mcpt_checkpoint_read": (i, [ctypes.c_char_p, fp, ip, ip, ip, ip, ctypes.c_char_p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -392,6 +395,32 @@ def write_png(path: str, rgb: np.ndarray) -> None:
     _check(lib().mcpt_write_png(str(path).encode(), _fp(a), a.shape[1], a.shape[0]), "mcpt_write_png")
 
 
+# ---- checkpoint / resume of a progressive render (mcpt.h: mcpt_checkpoint_write / _read)
+CHECKPOINT_TAG_MAX = 1024
+
+
+def checkpoint_write(path: str, accum: np.ndarray, pass_count: int, next_pass: int, tag: str = "") -> None:
+    """accum: rows × W × 3 f32 sums holding `pass_count` passes; `next_pass` = the first pass
+    of the render call that continues; `tag` = the render parameters the reader compares."""
+    a = np.ascontiguousarray(accum, np.float32)
+    if a.ndim != 3 or a.shape[2] != 3:
+        raise MCPTError("checkpoint_write: accum must be rows x W x 3")
+    _check(lib().mcpt_checkpoint_write(str(path).encode(), _fp(a), a.shape[1], a.shape[0], int(pass_count),
+                                       int(next_pass), tag.encode()), "mcpt_checkpoint_write")
+
+
+def checkpoint_read(path: str) -> Tuple[np.ndarray, int, int, str]:
+    """(accum rows × W × 3, pass_count, next_pass, tag) of a checkpoint file."""
+    w, rows, pc, nxt = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    tag = ctypes.create_string_buffer(CHECKPOINT_TAG_MAX)
+    _check(lib().mcpt_checkpoint_read(str(path).encode(), None, ctypes.byref(w), ctypes.byref(rows), None, None,
+                                      None), "mcpt_checkpoint_read")
+    out = np.empty((rows.value, w.value, 3), np.float32)
+    _check(lib().mcpt_checkpoint_read(str(path).encode(), _fp(out), None, None, ctypes.byref(pc), ctypes.byref(nxt),
+                                      tag), "mcpt_checkpoint_read")
+    return out, pc.value, nxt.value, tag.value.decode()
+
+
 class Renderer:
     """Device context: scene on the GPU, row-band framebuffer, pass accumulation."""
 
@@ -517,6 +546,29 @@ class Renderer:
 
     def clear_accum(self) -> None:
         _check(lib().mcpt_clear_accum(self._h), "mcpt_clear_accum")
+
+    def write_accum(self, accum: np.ndarray, pass_count: int) -> None:
+        """mcpt_write_accum: load local rows × W × 3 sums holding `pass_count` passes."""
+        a = np.ascontiguousarray(accum, np.float32)
+        if a.shape != (self.n_local_rows, self.W, 3):
+            raise MCPTError(f"write_accum: expected {(self.n_local_rows, self.W, 3)}, got {a.shape}")
+        _check(lib().mcpt_write_accum(self._h, _fp(a), int(pass_count)), "mcpt_write_accum")
+
+    def save_checkpoint(self, path: str, next_pass: int, tag: str = "") -> None:
+        """Write this context's accumulator, its pass count and `next_pass` to `path`."""
+        acc, n = self.read_accum()
+        checkpoint_write(path, acc, n, next_pass, tag)
+
+    def load_checkpoint(self, path: str, tag: Optional[str] = None) -> int:
+        """Resume from `path`: checks the target shape (and `tag`, if given), loads the sums and
+        pass count, returns the first pass of the next render call."""
+        acc, n, nxt, t = checkpoint_read(path)
+        if acc.shape != (self.n_local_rows, self.W, 3):
+            raise MCPTError(f"load_checkpoint: checkpoint is {acc.shape}, target {(self.n_local_rows, self.W, 3)}")
+        if tag is not None and t != tag:
+            raise MCPTError(f"load_checkpoint: tag {t!r} != {tag!r}")
+        self.write_accum(acc, n)
+        return nxt
 
     def accum_device_ptr(self) -> Tuple[int, int]:
         p = _vp()
