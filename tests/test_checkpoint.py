@@ -85,6 +85,10 @@ def test_resume_bit_equal_to_uninterrupted(mcpt_mod, tmp_path):
     got, n_got = b2.read_accum()
     assert n_got == n_want == 64
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    # call boundaries on the 32-pass accumulation chunks: also one call over passes 1..64
+    c = renderer()
+    c.render(ipv, iv, 1, 64, 0.0, B, 1.0, mcpt_mod.MONTECARLO)
+    assert np.array_equal(c.read_accum()[0].view(np.uint32), want.view(np.uint32))
     with pytest.raises(mcpt_mod.MCPTError):
         renderer().load_checkpoint(p, "scene=7")
     small = mcpt_mod.Renderer(0)
