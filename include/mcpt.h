@@ -353,10 +353,10 @@ int mcpt_checkpoint_write(const char* path, const float* rgb, int W, int rows, i
                           const char* tag);
 /* Reads the header into W, rows, pass_count, next_pass (any may be NULL) and the tag into tag_out
  * (MCPT_CHECKPOINT_TAG_MAX bytes, NUL-terminated; may be NULL); the sums into rgb_out
- * (rows × W × 3 floats) unless it is NULL.  MCPT_ERR_INVALID_ARG for a missing, foreign or
- * truncated file. */
-int mcpt_checkpoint_read(const char* path, float* rgb_out, int* W, int* rows, int* pass_count, int* next_pass,
-                         char* tag_out);
+ * (rows × W × 3 floats, at most `capacity` floats) unless it is NULL.  MCPT_ERR_INVALID_ARG for
+ * a missing, foreign or truncated file, or sums larger than `capacity`. */
+int mcpt_checkpoint_read(const char* path, float* rgb_out, long long capacity, int* W, int* rows, int* pass_count,
+                         int* next_pass, char* tag_out);
 
 #ifdef __cplusplus
 }

@@ -367,10 +367,12 @@ class Renderer {
   int load_checkpoint(const std::string& path, const std::string& tag) {
     int w = 0, rows = 0, n = 0, next = 0;
     std::vector<char> t(MCPT_CHECKPOINT_TAG_MAX);
-    check(mcpt_checkpoint_read(path.c_str(), nullptr, &w, &rows, nullptr, nullptr, nullptr), "mcpt_checkpoint_read");
+    check(mcpt_checkpoint_read(path.c_str(), nullptr, 0, &w, &rows, nullptr, nullptr, nullptr), "mcpt_checkpoint_read");
     if (w != W_ || rows != rows_) throw Error("checkpoint: framebuffer shape differs", MCPT_ERR_INVALID_ARG);
     std::vector<float> acc((size_t)rows * w * 3);
-    check(mcpt_checkpoint_read(path.c_str(), acc.data(), nullptr, nullptr, &n, &next, t.data()), "mcpt_checkpoint_read");
+    check(mcpt_checkpoint_read(path.c_str(), acc.data(), (long long)acc.size(), &w, &rows, &n, &next, t.data()),
+          "mcpt_checkpoint_read");
+    if (w != W_ || rows != rows_) throw Error("checkpoint: framebuffer shape differs", MCPT_ERR_INVALID_ARG);
     if (tag != t.data()) throw Error("checkpoint: render parameters differ (" + std::string(t.data()) + ")", MCPT_ERR_INVALID_ARG);
     write_accum(acc, n);
     return next;

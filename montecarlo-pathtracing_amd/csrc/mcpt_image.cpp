@@ -153,8 +153,8 @@ int mcpt_checkpoint_write(const char* path, const float* rgb, int W, int rows, i
   return MCPT_OK;
 }
 
-int mcpt_checkpoint_read(const char* path, float* rgb_out, int* W, int* rows, int* pass_count, int* next_pass,
-                         char* tag_out) {
+int mcpt_checkpoint_read(const char* path, float* rgb_out, long long capacity, int* W, int* rows, int* pass_count,
+                         int* next_pass, char* tag_out) {
   if (!path) return MCPT_ERR_INVALID_ARG;
   FILE* f = std::fopen(path, "rb");
   if (!f) return MCPT_ERR_INVALID_ARG;
@@ -167,7 +167,7 @@ int mcpt_checkpoint_read(const char* path, float* rgb_out, int* W, int* rows, in
             std::fread(tag, 1, (size_t)hdr[4], f) == (size_t)hdr[4];
   if (ok && rgb_out) {
     const size_t n = (size_t)hdr[0] * hdr[1] * 3;
-    ok = std::fread(rgb_out, sizeof(float), n, f) == n;
+    ok = capacity >= 0 && n <= (size_t)capacity && std::fread(rgb_out, sizeof(float), n, f) == n;
   }
   std::fclose(f);
   if (!ok) return MCPT_ERR_INVALID_ARG;

@@ -144,7 +144,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "mcpt_write_png": (i, [ctypes.c_char_p, fp, i, i]),
         "mcpt_write_accum": (i, [_vp, fp, i]),
         "mcpt_checkpoint_write": (i, [ctypes.c_char_p, fp, i, i, i, i, ctypes.c_char_p]),
-        "mcpt_checkpoint_read": (i, [ctypes.c_char_p, fp, ip, ip, ip, ip, ctypes.c_char_p]),
+        "mcpt_checkpoint_read": (i, [ctypes.c_char_p, fp, ctypes.c_longlong, ip, ip, ip, ip, ctypes.c_char_p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -413,11 +413,14 @@ def checkpoint_read(path: str) -> Tuple[np.ndarray, int, int, str]:
     """(accum rows × W × 3, pass_count, next_pass, tag) of a checkpoint file."""
     w, rows, pc, nxt = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
     tag = ctypes.create_string_buffer(CHECKPOINT_TAG_MAX)
-    _check(lib().mcpt_checkpoint_read(str(path).encode(), None, ctypes.byref(w), ctypes.byref(rows), None, None,
+    _check(lib().mcpt_checkpoint_read(str(path).encode(), None, 0, ctypes.byref(w), ctypes.byref(rows), None, None,
                                       None), "mcpt_checkpoint_read")
     out = np.empty((rows.value, w.value, 3), np.float32)
-    _check(lib().mcpt_checkpoint_read(str(path).encode(), _fp(out), None, None, ctypes.byref(pc), ctypes.byref(nxt),
-                                      tag), "mcpt_checkpoint_read")
+    # the capacity bounds the read if the file was replaced in between; the shape is re-read
+    _check(lib().mcpt_checkpoint_read(str(path).encode(), _fp(out), out.size, ctypes.byref(w), ctypes.byref(rows),
+                                      ctypes.byref(pc), ctypes.byref(nxt), tag), "mcpt_checkpoint_read")
+    if (rows.value, w.value, 3) != out.shape:
+        raise MCPTError("checkpoint_read: the file changed while it was read")
     return out, pc.value, nxt.value, tag.value.decode()
 
 

@@ -42,6 +42,12 @@ def test_checkpoint_rejects_bad_files(mcpt_mod, tmp_path):
     for bad in (cut, foreign, str(tmp_path / "missing.ckpt")):
         with pytest.raises(mcpt_mod.MCPTError):
             mcpt_mod.checkpoint_read(bad)
+    # the reader never writes more than the caller's capacity (a file replaced between the
+    # header read and the sums read)
+    small = np.zeros(4 * 5 * 3 - 1, np.float32)
+    assert mcpt_mod.lib().mcpt_checkpoint_read(p.encode(), mcpt_mod._fp(small), small.size,
+                                               None, None, None, None, None) == -1
+    assert mcpt_mod.lib().mcpt_checkpoint_read(p.encode(), mcpt_mod._fp(small), -1, None, None, None, None, None) == -1
     with pytest.raises(mcpt_mod.MCPTError):               # tag longer than the format allows
         mcpt_mod.checkpoint_write(p, acc, 1, 2, "x" * mcpt_mod.CHECKPOINT_TAG_MAX)
     with pytest.raises(mcpt_mod.MCPTError):
