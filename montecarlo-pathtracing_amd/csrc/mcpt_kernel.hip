@@ -260,6 +260,10 @@ __device__ __forceinline__ bool box_test(float4 a0, float4 a1, float4 a2, f3 O, 
 #define MCPT_NODE_LOADS_TOGETHER 1
 #endif
 #define MCPT_ROWS_IN(...) asm volatile("" ::__VA_ARGS__)
+// the LDS-scene kernels with the rows together too (A/B knob; off: the lazy form)
+#ifndef MCPT_LDS_ROWS_TOGETHER
+#define MCPT_LDS_ROWS_TOGETHER 0
+#endif
 // Row k of a per-lane record array at a 32-bit byte offset from the array's wave-uniform base
 // (n_prims < 2^24 keeps every node and primitive row below 2^31 bytes): the load takes the
 // base from SGPRs with a 32-bit lane offset (global_load ... saddr) instead of a 64-bit VALU
@@ -285,7 +289,7 @@ __device__ __forceinline__ const float4* node_rows(const float4* __restrict__ no
 template <bool COUNT, class SR>
 __device__ __forceinline__ void node_tests(const SR& s, const float4* __restrict__ nodes, size_t j, f3 O, f3 D,
                                            f3 invD, double cull2, bool& hl, bool& hr) {
-  if constexpr (MCPT_NODE_LOADS_TOGETHER && !SR::kLds && !SR::kMesh) {
+  if constexpr (MCPT_NODE_LOADS_TOGETHER && (!SR::kLds || MCPT_LDS_ROWS_TOGETHER) && !SR::kMesh) {
     const float4* q = node_rows(nodes, j);
     float4 l0 = q[0], l1 = q[1], l2 = q[2], r0 = q[3], r1 = q[4], r2 = q[5];
 #if MCPT_NODE_LOADS_TOGETHER == 1
@@ -453,7 +457,7 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
   constexpr bool U = UNI && !SR::kLds;
   // per-lane L1/L2 reads (node_tests): the type code and the inverse rows in one round trip,
   // else the rows' loads wait behind the type test
-  constexpr bool kTogether = MCPT_NODE_LOADS_TOGETHER && !U && !SR::kLds && !SR::kMesh;
+  constexpr bool kTogether = MCPT_NODE_LOADS_TOGETHER && !U && (!SR::kLds || MCPT_LDS_ROWS_TOGETHER) && !SR::kMesh;
   int pt = kTogether && MCPT_ROW_OFFSET32 ? s.ptype[(uint32_t)i] : ld1<U>(s.ptype, i);
   if constexpr (!kTogether) {
     if (pt < 0) return;
