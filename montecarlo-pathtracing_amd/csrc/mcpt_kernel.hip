@@ -483,9 +483,9 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
   constexpr bool kTrfEarly = kTogether && MCPT_PRIM_TRF_EARLY;
   float4 t0 = r0, t1 = r0, t2 = r0;
   if constexpr (kTrfEarly) {
-    t0 = ld4<U>(s.prims, b + 3); t1 = ld4<U>(s.prims, b + 4); t2 = ld4<U>(s.prims, b + 5);
-    asm volatile("" : "+v"(t0.x), "+v"(t0.y), "+v"(t0.z), "+v"(t1.x), "+v"(t1.y), "+v"(t1.z), "+v"(t2.x),
-                 "+v"(t2.y), "+v"(t2.z));
+    const float4* q = row_ptr(s.prims, b + 3);
+    t0 = q[0]; t1 = q[1]; t2 = q[2];
+    MCPT_ROWS_IN("v"(t0.x), "v"(t0.y), "v"(t0.z), "v"(t1.x), "v"(t1.y), "v"(t1.z), "v"(t2.x), "v"(t2.y), "v"(t2.z));
   }
   auto accept = [&](int shape, int dir, f3 Pl) {
     if constexpr (kTrfEarly) accept_rows<COUNT>(i, shape, dir, Pl, Ow, t0, t1, t2, h, ev, SR::kFastLen);
