@@ -89,11 +89,11 @@ struct mcpt_ctx {
   int traversal = MCPT_TRAVERSAL_AUTO;
   // AUTO schedule: the first sizeable launches after a scene upload run each candidate twice
   // (kernel time per sample from the launch events), later launches use the fastest (results
-  // are identical either way).  Candidates: 1 = per-lane walk, 2 = wave-coherent walk, 3 = the
-  // stream schedule (deep BVHs, montecarlo.frag, no meshes), per-lane walks with 2 (4, on
-  // launches of >= 2 pass segments) or 4 (5, >= 4 segments) pass segments per work item, and
-  // for BVH depth >= 8 per-lane walks with the deep knobs (leaf batch 16, walk exit 40) and 4
-  // (6) or 8 (7, >= 8 segments) segments per item.
+  // are identical either way).  Candidates: 1 = per-lane walk, 2 = wave-coherent walk (BVH depth
+  // < 8), per-lane walks with 2 (4, on launches of >= 2 pass segments) or 4 (5, >= 4 segments)
+  // pass segments per work item, and for BVH depth >= 8 per-lane walks with the deep knobs (leaf
+  // batch 16, walk exit 40) and 4 (6) or 8 (7, >= 8 segments) segments per item.  (3, the stream
+  // schedule, is only run when selected explicitly.)
   int tune_pending = 0;             // candidate of the launch whose timing is not collected yet
   double tune_samples = 0.0;        // samples of that launch
   long long tune_shape[2] = {0, 0};      // (local pixels, passes) of that launch
@@ -101,7 +101,6 @@ struct mcpt_ctx {
   int meas_segs = 0;                // pass segments of that shape (which candidates apply)
   double tune_ns[8] = {0.0};       // best ns per sample measured, by candidate (same shape)
   int tune_cnt[8] = {0};            // trials of each candidate so far
-  bool stream_auto = false;         // the stream candidate applies to the current launch
   bool deep_auto = false;           // the deep-knob candidates apply (BVH depth >= 8, per-lane kernel)
   int tune_choice = 0;              // resolved candidate once all are measured
   int walk_exit = -1;               // mcpt_set_walk_exit; -1: by BVH depth
@@ -123,8 +122,9 @@ struct mcpt_ctx {
 
 // events of sub-launch k of the last call: start / mid / stop
 static hipEvent_t ev_start(const mcpt_ctx* c, int k) { return c->evs[c->ring_pos][3 * k]; }
-static hipEvent_t ev_mid(const mcpt_ctx* c, int k) { return c->evs[c->ring_pos][3 * k + 1]; }
 static hipEvent_t ev_stop(const mcpt_ctx* c, int k) { return c->evs[c->ring_pos][3 * k + 2]; }
+// event i of sub-launch k in ring slot `slot` (0 start, 1 mid, 2 stop)
+static hipEvent_t ev_at(const mcpt_ctx* c, int slot, int k, int i) { return c->evs[slot][3 * k + i]; }
 static hipError_t ensure_events(mcpt_ctx* c, int slot, int n_sub) {
   while ((int)c->evs[slot].size() < 3 * n_sub) {
     hipEvent_t e = nullptr;
@@ -188,12 +188,15 @@ constexpr int kDeepLeafBatch = 16, kDeepWalkExit = 40;
 // pass split (launch()): launches with fewer than this many work items per CU, of at most
 // kPassSplitMaxPasses passes
 constexpr int kPassSplitItemsPerCu = 4, kPassSplitMaxPasses = 256;
-// BVH depth from which AUTO also times the stream schedule (its pool and two launches per
-// iteration only pay where walks are long)
-constexpr int kStreamAutoDepth = 8;
+// AUTO does not time the wave-coherent walk on BVHs at least this deep: the union of a wave's
+// incoherent secondary rays visits nearly the whole tree, and on scene 8 (C4) one trial launch
+// took 8.36 s against 1.81 s for the per-lane walk (profiles/r03_r03s_c4_kernel_stats.csv).  The
+// stream schedule (candidate 3) is never timed by AUTO: it was 5 % behind the megakernel on
+// scene 8 and 4-7x slower on shallow scenes; mcpt_set_traversal selects it.
+constexpr int kWaveAutoMaxDepth = 7;
 // the candidates that apply to a launch of `segs` pass segments
 static bool cand_applies(const mcpt_ctx* c, int cand, long long segs) {
-  return cand <= 2 || (cand == kCandStream && c->stream_auto) || (cand == kCandLaneSeg2 && segs >= 2) ||
+  return cand == 1 || (cand == 2 && c->depth <= kWaveAutoMaxDepth) || (cand == kCandLaneSeg2 && segs >= 2) ||
          (cand == kCandLaneSeg4 && segs >= 4) || (cand == kCandDeepSeg4 && c->deep_auto && segs >= 4) ||
          (cand == kCandDeepSeg8 && c->deep_auto && segs >= 8);
 }
@@ -686,8 +689,6 @@ static int stream_run(mcpt_ctx* c, const mcpt::RenderParams& p) {
   // no faster on scenes 3/7/8 (random lanes' node reads conflict in the LDS banks, 11 conflict
   // cycles per LDS instruction; gpurun_out r03e/r03f)
   const bool lds_nodes = env_int("MCPT_STREAM_LDS_NODES", 0) != 0 && mcpt_stream_lds_nodes_fit(p.depth);
-  // two walks per lane in the trace kernel (walk_run2), measured, off by default
-  const bool dual = env_int("MCPT_STREAM_DUAL", 0) != 0;
   mcpt::StreamParams q[kStreamPools];
   unsigned* unit_ctr = c->d_sctr + mcpt::SC_UNIT;   // pool 0's slot: shared
   {
@@ -729,13 +730,14 @@ static int stream_run(mcpt_ctx* c, const mcpt::RenderParams& p) {
   const long long cap = ((long long)(n_units / min_pool) + 2) * per_unit + 4 * kStreamBatch;
   long long it = 0;
   bool compact[kStreamPools] = {false, false}, done[kStreamPools] = {false, false};
+  const int st = [&]() -> int {
   for (int b = 0;; ++b) {
     for (int k = 0; k < kStreamBatch; ++k, ++it)
       for (int j = 0; j < np; ++j) {
         if (done[j]) continue;
         q[j].parity = (int)(it & 1);
         q[j].compact = (k == 0 && compact[j]) ? 1 : 0;
-        HIP_OR_RETURN(mcpt_launch_stream_iter(q[j], c->n_cu, lds_nodes, dual, c->pool_stream[j]));
+        HIP_OR_RETURN(mcpt_launch_stream_iter(q[j], c->n_cu, lds_nodes, c->pool_stream[j]));
       }
     // every pool's counters after the batch, read on pool 0's stream once all pools are there
     for (int j = 1; j < np; ++j) {
@@ -762,10 +764,31 @@ static int stream_run(mcpt_ctx* c, const mcpt::RenderParams& p) {
     }
     if (it > cap) return set_err(MCPT_ERR_HIP, "stream schedule did not drain its queue");
   }
-  // join: the context's stream (the combine kernel, the caller's next work) waits for the pools
-  HIP_OR_RETURN(hipEventRecord(c->pool_ev[0], c->pool_stream[0]));
-  HIP_OR_RETURN(hipStreamWaitEvent(c->stream, c->pool_ev[0], 0));
+  return MCPT_OK;
+  }();
+  // join: the context's stream (the combine kernel, the caller's next work) waits for every
+  // pool stream.  Also after an error: kernels already queued on a pool stream still read and
+  // write d_slots / d_queue / d_partial, which the context frees or reallocates only after
+  // synchronizing its own stream, so that stream must not run ahead of them.
+  bool joined = true;
+  for (int j = 0; j < np; ++j)
+    joined = joined && hipEventRecord(c->pool_ev[j], c->pool_stream[j]) == hipSuccess &&
+             hipStreamWaitEvent(c->stream, c->pool_ev[j], 0) == hipSuccess;
+  if (!joined)   // cannot order them: wait for them here
+    for (int j = 0; j < np; ++j) (void)hipStreamSynchronize(c->pool_stream[j]);
+  if (st != MCPT_OK) return st;
+  if (!joined) return set_err(MCPT_ERR_HIP, "stream schedule: joining the pool streams failed");
   c->stream_iters += it;
+  return MCPT_OK;
+}
+
+// the stream schedule's pools (4 GB at the default 16 Mi slots), once no longer selected
+static int free_stream_pools(mcpt_ctx* c) {
+  if (!c->d_slots && !c->d_queue) return MCPT_OK;
+  HIP_OR_RETURN(hipSetDevice(c->device));
+  HIP_OR_RETURN(hipStreamSynchronize(c->stream));
+  (void)hipFree(c->d_slots); (void)hipFree(c->d_queue);
+  c->d_slots = nullptr; c->d_queue = nullptr; c->slot_cap = 0;
   return MCPT_OK;
 }
 
@@ -806,7 +829,6 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   // segment groups need segments to group; whether longer items pay (the lanes' pass-count
   // tails average out) or cost (longer grid tail) depends on the scene and the launch: timed,
   // not guessed (profiles/r01_ab44_seg_per_item.jsonl, r01_ab49_seg_groups_tail.jsonl)
-  c->stream_auto = stream_applies(c, variant, bounces, false) && c->depth >= kStreamAutoDepth;
   c->deep_auto = c->depth >= 8;
   const int cand = count ? (c->traversal == MCPT_TRAVERSAL_AUTO ? MCPT_TRAVERSAL_LANE : c->traversal)
                          : resolve_candidate(c, total_seg);
@@ -876,6 +898,30 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   p.partial = c->d_partial;
   if (count) HIP_OR_RETURN(hipMemsetAsync(c->d_events, 0, sizeof(unsigned long long) * mcpt::EV_COUNT, c->stream));
   const double samples = (double)p.n_local_px * n_passes;
+  // The call's events go to ring slot `slot`; the ring position (what mcpt_last_render_ms and
+  // the AUTO timing read) moves there only once every event of the call has been recorded, so a
+  // call that fails part-way leaves the previous call's complete timings in place.
+  if (n_sub == 0) {   // no passes: an empty timed interval
+    for (int i = 0; i < 3; ++i) HIP_OR_RETURN(hipEventRecord(ev_at(c, slot, 0, i), c->stream));
+  }
+  for (long long lo = first_pass, end = (long long)first_pass + n_passes, k = 0; lo < end; ++k) {
+    const long long c0 = fdiv((int)(lo - 1), mcpt::kPassChunk);
+    const long long hi = split ? end : std::min(end, (c0 + max_seg) * mcpt::kPassChunk + 1);
+    p.first_pass = (int)lo;
+    p.n_passes = (int)(hi - lo);
+    p.n_segments = split ? p.n_passes : fdiv((int)(hi - 2), mcpt::kPassChunk) - (int)c0 + 1;
+    HIP_OR_RETURN(hipEventRecord(ev_at(c, slot, (int)k, 0), c->stream));
+    if (stream) {
+      const int st = stream_run(c, p);
+      if (st != MCPT_OK) return st;
+    } else {
+      HIP_OR_RETURN(mcpt_launch_render(p, count, c->stream));
+    }
+    HIP_OR_RETURN(hipEventRecord(ev_at(c, slot, (int)k, 1), c->stream));
+    HIP_OR_RETURN(mcpt_launch_combine(p, c->stream));
+    HIP_OR_RETURN(hipEventRecord(ev_at(c, slot, (int)k, 2), c->stream));
+    lo = hi;
+  }
   if (!count && c->traversal == MCPT_TRAVERSAL_AUTO && !c->tune_choice && samples >= kTuneMinSamples) {
     if (p.n_local_px != c->meas_shape[0] || n_passes != c->meas_shape[1]) c->meas_segs = (int)total_seg;
     c->tune_pending = cand;
@@ -888,29 +934,6 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   c->ring_n_sub[slot] = c->n_sub;
   c->n_timed++;
   c->pass_split = split ? 1 : 0;
-  if (n_sub == 0) {   // no passes: an empty timed interval
-    HIP_OR_RETURN(hipEventRecord(ev_start(c, 0), c->stream));
-    HIP_OR_RETURN(hipEventRecord(ev_mid(c, 0), c->stream));
-    HIP_OR_RETURN(hipEventRecord(ev_stop(c, 0), c->stream));
-  }
-  for (long long lo = first_pass, end = (long long)first_pass + n_passes, k = 0; lo < end; ++k) {
-    const long long c0 = fdiv((int)(lo - 1), mcpt::kPassChunk);
-    const long long hi = split ? end : std::min(end, (c0 + max_seg) * mcpt::kPassChunk + 1);
-    p.first_pass = (int)lo;
-    p.n_passes = (int)(hi - lo);
-    p.n_segments = split ? p.n_passes : fdiv((int)(hi - 2), mcpt::kPassChunk) - (int)c0 + 1;
-    HIP_OR_RETURN(hipEventRecord(ev_start(c, (int)k), c->stream));
-    if (stream) {
-      const int st = stream_run(c, p);
-      if (st != MCPT_OK) return st;
-    } else {
-      HIP_OR_RETURN(mcpt_launch_render(p, count, c->stream));
-    }
-    HIP_OR_RETURN(hipEventRecord(ev_mid(c, (int)k), c->stream));
-    HIP_OR_RETURN(mcpt_launch_combine(p, c->stream));
-    HIP_OR_RETURN(hipEventRecord(ev_stop(c, (int)k), c->stream));
-    lo = hi;
-  }
   c->timed = true;
   c->pass_count += n_passes;
   if (count) {
@@ -1120,6 +1143,7 @@ int mcpt_set_traversal(mcpt_ctx* c, int mode) {
     return set_err(MCPT_ERR_INVALID_ARG, "mcpt_set_traversal: bad mode");
   c->traversal = mode;
   reset_tuning(c);
+  if (mode != MCPT_TRAVERSAL_STREAM) return free_stream_pools(c);
   return MCPT_OK;
 }
 

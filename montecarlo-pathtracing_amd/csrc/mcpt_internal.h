@@ -171,6 +171,6 @@ hipError_t mcpt_launch_combine(const mcpt::RenderParams& p, hipStream_t stream);
 // stream schedule: slot set-up (queue[0] = every slot with a unit), then one iteration = the
 // trace kernel over queue[parity] + the shade kernel appending to queue[parity ^ 1]
 hipError_t mcpt_launch_stream_init(const mcpt::StreamParams& q, hipStream_t stream);
-hipError_t mcpt_launch_stream_iter(const mcpt::StreamParams& q, int n_cu, bool lds_nodes, bool dual, hipStream_t stream);
+hipError_t mcpt_launch_stream_iter(const mcpt::StreamParams& q, int n_cu, bool lds_nodes, hipStream_t stream);
 // the trace kernel can hold a BVH of this depth in LDS (nodes + leaf ids)
 bool mcpt_stream_lds_nodes_fit(int depth);

@@ -45,37 +45,17 @@
 #ifndef MCPT_FOLD_END
 #define MCPT_FOLD_END 1
 #endif
-// random_ray job compaction (rr_jobs): the shading round's two random_ray calls (the bounce's
-// `ray` and the reflect branch's new direction) run as one compacted batch across the wave.
-// Bit-exact, measured slower (scene 6 -18 %, scene 8 -9 %: DESIGN.md §4.1), off by default.
-#ifndef MCPT_RR_COMPACT
-#define MCPT_RR_COMPACT 0
-#endif
-// per-wave unit pool: a lane whose (pixel, segment) unit ends claims any unclaimed unit of
-// its wave's 64 x K pool (LDS counter) instead of its own pixel's next segment.  Bit-exact,
-// measured no faster than the static order, off by default.
-#ifndef MCPT_UNIT_POOL
-#define MCPT_UNIT_POOL 0
-#endif
 
 
 namespace mcpt {
 
-// math inside the BVH walk loop (primitive tests): the short exact sequences of mcpt_math.h
-// (FAST) or the generic IEEE expansions — same results either way.  The LDS-scene kernels
-// (shallow BVHs) take the short sequences (+2.4 % scene 6, +2 % scenes 1/2/4:
-// profiles/r02_ab10_walk_fast_math.jsonl); the L2-read deep-BVH kernels keep the generic ones,
-// whose fallback branches cost them registers (scene 8 -2.7 %; r01: -6..-9 % on scenes 3/7/8,
-// profiles/r01_ab19_fast_math.jsonl).  MCPT_WALK_FAST_MATH=1 forces the short ones everywhere.
-#ifndef MCPT_WALK_FAST_MATH
-#define MCPT_WALK_FAST_MATH 0
-#endif
-// which short sequences the L2-read kernels use (bits: 1 normalize, 2 length, 4 sqrt, 8 rcp);
-// the LDS-scene kernels use all of them.  Default: normalize only (scenes 3/5/7/8 +1.2..+5 %;
-// sqrt alone +-0; normalize + sqrt -9..-15 %: profiles/r02_ab12_l2_fast_math.jsonl)
-#ifndef MCPT_L2_FAST
-#define MCPT_L2_FAST (MCPT_WALK_FAST_MATH ? 15 : 1)
-#endif
+// math inside the BVH walk loop (primitive tests): the short exact sequences of mcpt_math.h or
+// the generic IEEE expansions — same results either way.  The LDS-scene kernels (shallow BVHs)
+// take all four short sequences (+2.4 % scene 6, +2 % scenes 1/2/4:
+// profiles/r02_ab10_walk_fast_math.jsonl); the L2-read deep-BVH kernels only the normalize
+// (+1.2..+5 % on scenes 3/5/7/8; sqrt alone +-0, normalize + sqrt -9..-15 % through register
+// allocation: profiles/r02_ab12_l2_fast_math.jsonl).  Bits: 1 normalize, 2 length, 4 sqrt, 8 rcp.
+constexpr int kL2Fast = 1;
 template <bool FAST>
 __device__ __forceinline__ f3 wnormalize3(f3 a) {
   if constexpr (FAST) return normalize3(a); else return normalize3_g(a);
@@ -144,7 +124,7 @@ struct SceneT {
   static constexpr bool kMesh = MESH;
   static constexpr bool kLds = LDS;
   // walk-loop math (wnormalize3, wlength3, wsqrt, wrcp): short exact sequences or generic
-  static constexpr int kFast = LDS ? 15 : MCPT_L2_FAST;
+  static constexpr int kFast = LDS ? 15 : kL2Fast;
   static constexpr bool kFastNorm = kFast & 1, kFastLen = kFast & 2, kFastSqrt = kFast & 4, kFastRcp = kFast & 8;
   const float4* __restrict__ nodes;   // 3 per node: (c, has-prim) (w, 0) (1/w, 0)
   const int* __restrict__ leaves;
@@ -246,63 +226,39 @@ __device__ __forceinline__ bool box_test(float4 a0, float4 a1, float4 a2, f3 O, 
 // early-out, the left child's whole test before the right's), and LLVM sinks each load to its
 // first use, so one node visit of the L1/L2-read kernels was a chain of up to five dependent
 // cache round trips (flag -> centre + 1/w -> w -> right 1/w -> right w, read off the ISA).
-// MCPT_NODE_LOADS_TOGETHER: there, every row is issued at once and an empty asm consumes them
-// at that point, so a visit waits for one round trip (scene 8 +4..5 %, scenes 3/5/7 +1..3 %:
-// profiles/r03_ab_node_loads_together.jsonl).  Same values, same bits.  The LDS-scene kernels
-// (ds_read latency is short: -1 % with the rows together) and the mesh kernels (128-VGPR walk
-// state: they spill) keep the lazy form.
-// The asm takes the rows as inputs only (1): it defines no new values, so the register
-// allocator keeps the rows in their load tuples.  With in-out operands (2, the first form) it
-// copied 11 of them out per node visit (v_mov; the deep walk's node block 17 -> 6 VALU outside
-// the box tests): scene 8 +1.4..1.7 %, scenes 3/5/7 -1.3..+1.9 %
-// (profiles/r03_ab_node_loads_inputs.jsonl).
-#ifndef MCPT_NODE_LOADS_TOGETHER
-#define MCPT_NODE_LOADS_TOGETHER 1
-#endif
+// So in those kernels every row is issued at once and an empty asm consumes them at that
+// point: a visit waits for one round trip (scene 8 +4..5 %, scenes 3/5/7 +1..3 %:
+// profiles/r03_ab_node_loads_together.jsonl).  Same values, same bits.  The asm takes the rows
+// as inputs only: it defines no new values, so the register allocator keeps the rows in their
+// load tuples (in-out operands made it copy 11 rows per visit: -1.4..-1.7 % on scene 8,
+// profiles/r03_ab_node_loads_inputs.jsonl).  The LDS-scene kernels (ds_read latency is short:
+// -0.2..-1 % with the rows together, profiles/r03_ab_lds_rows_together.jsonl) and the mesh
+// kernels (128-VGPR walk state: they spill) keep the lazy form.
 #define MCPT_ROWS_IN(...) asm volatile("" ::__VA_ARGS__)
-// the LDS-scene kernels with the rows together too (A/B knob; off: the lazy form)
-#ifndef MCPT_LDS_ROWS_TOGETHER
-#define MCPT_LDS_ROWS_TOGETHER 0
-#endif
 // Row k of a per-lane record array at a 32-bit byte offset from the array's wave-uniform base
 // (n_prims < 2^24 keeps every node and primitive row below 2^31 bytes): the load takes the
 // base from SGPRs with a 32-bit lane offset (global_load ... saddr) instead of a 64-bit VALU
-// address per visit (MCPT_ROW_OFFSET32=0: the 64-bit form).
-#ifndef MCPT_ROW_OFFSET32
-#define MCPT_ROW_OFFSET32 1
-#endif
+// address per visit (+0.9..1.3 %: profiles/r03_ab_row_offset32.jsonl).
 __device__ __forceinline__ const float4* row_ptr(const float4* __restrict__ base, size_t k) {
-  if (MCPT_ROW_OFFSET32) return (const float4*)((const char*)base + (uint32_t)k * 16u);
-  return base + k;
+  return (const float4*)((const char*)base + (uint32_t)k * 16u);
 }
 // the two child records of a node pair j (rows 3j .. 3j+5): byte offset 48 j, with j * 3 as
 // one full-rate shift-add (LLVM turns * 48 into v_mul_lo_u32, a quarter-rate instruction)
 __device__ __forceinline__ const float4* node_rows(const float4* __restrict__ nodes, size_t j) {
-  if (!MCPT_ROW_OFFSET32) return nodes + j * 3;
   uint32_t t;
   asm("v_lshl_add_u32 %0, %1, 1, %1" : "=v"(t) : "v"((uint32_t)j));
   return (const float4*)((const char*)nodes + (t << 4));
 }
-#ifndef MCPT_PRIM_TRF_EARLY
-#define MCPT_PRIM_TRF_EARLY 0
-#endif
 template <bool COUNT, class SR>
 __device__ __forceinline__ void node_tests(const SR& s, const float4* __restrict__ nodes, size_t j, f3 O, f3 D,
                                            f3 invD, double cull2, bool& hl, bool& hr) {
-  if constexpr (MCPT_NODE_LOADS_TOGETHER && (!SR::kLds || MCPT_LDS_ROWS_TOGETHER) && !SR::kMesh) {
+  if constexpr (!SR::kLds && !SR::kMesh) {
     const float4* q = node_rows(nodes, j);
     float4 l0 = q[0], l1 = q[1], l2 = q[2], r0 = q[3], r1 = q[4], r2 = q[5];
-#if MCPT_NODE_LOADS_TOGETHER == 1
     MCPT_ROWS_IN("v"(l0.x), "v"(l0.y), "v"(l0.z), "v"(l0.w), "v"(l1.x), "v"(l1.y), "v"(l1.z), "v"(l2.x),
                  "v"(l2.y), "v"(l2.z));
     MCPT_ROWS_IN("v"(r0.x), "v"(r0.y), "v"(r0.z), "v"(r0.w), "v"(r1.x), "v"(r1.y), "v"(r1.z), "v"(r2.x),
                  "v"(r2.y), "v"(r2.z));
-#else
-    asm volatile("" : "+v"(l0.x), "+v"(l0.y), "+v"(l0.z), "+v"(l0.w), "+v"(l1.x), "+v"(l1.y), "+v"(l1.z),
-                 "+v"(l2.x), "+v"(l2.y), "+v"(l2.z));
-    asm volatile("" : "+v"(r0.x), "+v"(r0.y), "+v"(r0.z), "+v"(r0.w), "+v"(r1.x), "+v"(r1.y), "+v"(r1.z),
-                 "+v"(r2.x), "+v"(r2.y), "+v"(r2.z));
-#endif
     hl = (COUNT || l0.w != 0.0f) && box_test<false>(l0, l1, l2, O, D, invD, cull2);
     hr = (COUNT || r0.w != 0.0f) && box_test<false>(r0, r1, r2, O, D, invD, cull2);
   } else {
@@ -457,8 +413,8 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
   constexpr bool U = UNI && !SR::kLds;
   // per-lane L1/L2 reads (node_tests): the type code and the inverse rows in one round trip,
   // else the rows' loads wait behind the type test
-  constexpr bool kTogether = MCPT_NODE_LOADS_TOGETHER && !U && (!SR::kLds || MCPT_LDS_ROWS_TOGETHER) && !SR::kMesh;
-  int pt = kTogether && MCPT_ROW_OFFSET32 ? s.ptype[(uint32_t)i] : ld1<U>(s.ptype, i);
+  constexpr bool kTogether = !U && !SR::kLds && !SR::kMesh;
+  int pt = kTogether ? s.ptype[(uint32_t)i] : ld1<U>(s.ptype, i);
   if constexpr (!kTogether) {
     if (pt < 0) return;
   }
@@ -467,30 +423,12 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
   if constexpr (kTogether) {
     const float4* q = row_ptr(s.prims, b);
     r0 = q[0]; r1 = q[1]; r2 = q[2];
+    MCPT_ROWS_IN("v"(pt), "v"(r0.x), "v"(r0.y), "v"(r0.z), "v"(r0.w), "v"(r1.x), "v"(r1.y), "v"(r1.z),
+                 "v"(r1.w), "v"(r2.x), "v"(r2.y), "v"(r2.z), "v"(r2.w));
   } else {
     r0 = ld4<U>(s.prims, b); r1 = ld4<U>(s.prims, b + 1); r2 = ld4<U>(s.prims, b + 2);
   }
-  if constexpr (kTogether) {
-#if MCPT_NODE_LOADS_TOGETHER == 1
-    MCPT_ROWS_IN("v"(pt), "v"(r0.x), "v"(r0.y), "v"(r0.z), "v"(r0.w), "v"(r1.x), "v"(r1.y), "v"(r1.z),
-                 "v"(r1.w), "v"(r2.x), "v"(r2.y), "v"(r2.z), "v"(r2.w));
-#else
-    asm volatile("" : "+v"(pt), "+v"(r0.x), "+v"(r0.y), "+v"(r0.z), "+v"(r0.w), "+v"(r1.x), "+v"(r1.y),
-                 "+v"(r1.z), "+v"(r1.w), "+v"(r2.x), "+v"(r2.y), "+v"(r2.z), "+v"(r2.w));
-#endif
-  }
-  // MCPT_PRIM_TRF_EARLY: the transform rows a candidate needs ride in the same round trip
-  constexpr bool kTrfEarly = kTogether && MCPT_PRIM_TRF_EARLY;
-  float4 t0 = r0, t1 = r0, t2 = r0;
-  if constexpr (kTrfEarly) {
-    const float4* q = row_ptr(s.prims, b + 3);
-    t0 = q[0]; t1 = q[1]; t2 = q[2];
-    MCPT_ROWS_IN("v"(t0.x), "v"(t0.y), "v"(t0.z), "v"(t1.x), "v"(t1.y), "v"(t1.z), "v"(t2.x), "v"(t2.y), "v"(t2.z));
-  }
-  auto accept = [&](int shape, int dir, f3 Pl) {
-    if constexpr (kTrfEarly) accept_rows<COUNT>(i, shape, dir, Pl, Ow, t0, t1, t2, h, ev, SR::kFastLen);
-    else accept_cand<COUNT, UNI>(s, i, shape, dir, Pl, Ow, h, ev);
-  };
+  auto accept = [&](int shape, int dir, f3 Pl) { accept_cand<COUNT, UNI>(s, i, shape, dir, Pl, Ow, h, ev); };
   if (pt < 0) return;
   const int t = pt & 15;
   f3 O = xpoint(r0, r1, r2, Ow);
@@ -689,7 +627,7 @@ __device__ __forceinline__ bool walk_run(const SR& s, f3 O, f3 D, Hit& h, Walk& 
 #endif
     if (do_leaf) {
       ev.inc(EV_LEAF);
-      int p = s.leaves[MCPT_ROW_OFFSET32 ? (size_t)(uint32_t)(w.node - leaf0) : (size_t)(w.node - leaf0)];
+      int p = s.leaves[(uint32_t)(w.node - leaf0)];
       if (p >= 0) prim_test<COUNT, false, false>(s, p, O, D, h, ev);
     }
 #ifdef MCPT_STAMPS
@@ -731,80 +669,6 @@ __device__ __forceinline__ bool walk_run(const SR& s, f3 O, f3 D, Hit& h, Walk& 
   }
 }
 
-// Two independent per-lane walks, A and B, advanced together (the stream trace kernel's
-// MCPT_STREAM_DUAL build: the verdict's "two walks per lane" latency lever, measured in
-// DESIGN.md §4.1d).  A node iteration issues both walks' six rows before either walk's box
-// tests, so a lane keeps two dependent load chains in flight; a leaf iteration (batched over
-// both walks' waiting leaves, as walk_run) runs A's then B's primitive test.  run_a / run_b:
-// the walk is in progress (cleared when it completes).  Returns once at most `exit` walks of
-// the wave are still running and fewer than at entry, or when this lane has none.  Each walk's
-// own visit sequence is walk_run's (same bits).
-template <class SR>
-__device__ __forceinline__ void walk_run2(const SR& s, f3 oa, f3 da, Hit& ha, Walk& wa, bool& run_a, f3 ob, f3 db,
-                                          Hit& hb, Walk& wb, bool& run_b, int exit, int leaf_batch) {
-  Ev<false> ev;
-  const int leaf0 = (1 << s.depth) - 1;
-  auto walks = [&]() { return __builtin_popcountll(__ballot(run_a)) + __builtin_popcountll(__ballot(run_b)); };
-  const int n0 = walks();
-  auto node_step = [&](Walk& w, Hit& h, f3 O, f3 D, size_t j, float4 l0, float4 l1, float4 l2, float4 r0,
-                       float4 r1, float4 r2) {
-    const bool hl = l0.w != 0.0f && box_test<false>(l0, l1, l2, O, D, w.invD, h.cull2);
-    const bool hr = r0.w != 0.0f && box_test<false>(r0, r1, r2, O, D, w.invD, h.cull2);
-    if (hr) {
-      if (hl) w.pending |= 1u << (w.level + 1);
-      w.node = (int)j + 1; w.level++;
-    } else if (hl) {
-      w.node = (int)j; w.level++;
-    }
-    return !(hl || hr);
-  };
-  auto pop = [&](Walk& w, bool& run) {
-    if (w.pending == 0) { run = false; return; }
-    const int L = 31 - __builtin_clz(w.pending);
-    w.pending &= ~(1u << L);
-    w.node = ((w.node + 1) >> (w.level - L)) - 2;
-    w.level = L;
-  };
-  while (run_a || run_b) {
-    const bool lf_a = run_a && wa.node >= leaf0, lf_b = run_b && wb.node >= leaf0;
-    const int on_leaf = __builtin_popcountll(__ballot(lf_a)) + __builtin_popcountll(__ballot(lf_b));
-    const bool leaves = on_leaf >= leaf_batch || on_leaf == walks();   // wave-uniform
-    bool pop_a = false, pop_b = false;
-    if (leaves) {
-      if (lf_a) {
-        const int p = s.leaves[wa.node - leaf0];
-        if (p >= 0) prim_test<false, false, false>(s, p, oa, da, ha, ev);
-        pop_a = true;
-      }
-      if (lf_b) {
-        const int p = s.leaves[wb.node - leaf0];
-        if (p >= 0) prim_test<false, false, false>(s, p, ob, db, hb, ev);
-        pop_b = true;
-      }
-    } else {
-      const bool nd_a = run_a && !lf_a, nd_b = run_b && !lf_b;
-      const size_t ja = 2 * (size_t)(nd_a ? wa.node : 0) + 1, jb = 2 * (size_t)(nd_b ? wb.node : 0) + 1;
-      const float4* qa = s.nodes + ja * 3;
-      const float4* qb = s.nodes + jb * 3;
-      float4 a0 = qa[0], a1 = qa[1], a2 = qa[2], a3 = qa[3], a4 = qa[4], a5 = qa[5];
-      float4 b0 = qb[0], b1 = qb[1], b2 = qb[2], b3 = qb[3], b4 = qb[4], b5 = qb[5];
-      asm volatile("" : "+v"(a0.x), "+v"(a0.y), "+v"(a0.z), "+v"(a0.w), "+v"(a1.x), "+v"(a1.y), "+v"(a1.z),
-                   "+v"(a2.x), "+v"(a2.y), "+v"(a2.z));
-      asm volatile("" : "+v"(a3.x), "+v"(a3.y), "+v"(a3.z), "+v"(a3.w), "+v"(a4.x), "+v"(a4.y), "+v"(a4.z),
-                   "+v"(a5.x), "+v"(a5.y), "+v"(a5.z));
-      asm volatile("" : "+v"(b0.x), "+v"(b0.y), "+v"(b0.z), "+v"(b0.w), "+v"(b1.x), "+v"(b1.y), "+v"(b1.z),
-                   "+v"(b2.x), "+v"(b2.y), "+v"(b2.z));
-      asm volatile("" : "+v"(b3.x), "+v"(b3.y), "+v"(b3.z), "+v"(b3.w), "+v"(b4.x), "+v"(b4.y), "+v"(b4.z),
-                   "+v"(b5.x), "+v"(b5.y), "+v"(b5.z));
-      if (nd_a) pop_a = node_step(wa, ha, oa, da, ja, a0, a1, a2, a3, a4, a5);
-      if (nd_b) pop_b = node_step(wb, hb, ob, db, jb, b0, b1, b2, b3, b4, b5);
-    }
-    if (pop_a) pop(wa, run_a);
-    if (pop_b) pop(wb, run_b);
-    const int n = walks();
-    if (n <= exit && n < n0) return;
-  }
-}
 
 // walk_run for scenes with mesh instances.  The reference runs an instance's whole mesh DFS
 // (Mesh_intersect raytracer_func.frag:642-678) inside the scene DFS's leaf visit; nested that
@@ -1076,78 +940,8 @@ __device__ __forceinline__ float schlick(float r0, f3 I, f3 N) {   // :91-98
   return gclamp(r0 + ((((1.0f - r0) * x) * x * x) * x) * x, 0.0f, 1.0f);
 }
 
-// ------------------------------------------------------------------------------------
-// random_ray job compaction (north star: ray compaction via wavefront primitives)
-// ------------------------------------------------------------------------------------
 __device__ __forceinline__ int mbcnt64(uint64_t m) {
   return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-__device__ __forceinline__ uint32_t bperm(int lane, uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_ds_bpermute(lane << 2, (int)v);
-}
-__device__ __forceinline__ float bpermf(int lane, float v) { return __uint_as_float(bperm(lane, __float_as_uint(v))); }
-
-// One shading round of montecarlo.frag draws up to two random_ray per lane: `ray`
-// (:122, every non-emissive hit) and the reflect branch's new direction (:136 / :155, the
-// reflective branch and the mixed branch's reflect half).  Issued as two call sites, the wave
-// pays for both whenever any lane reflects, each with part of its lanes.  Both are pure
-// functions of (direction, roughness, RNG state), and the state of the second is the first's
-// plus a known number of draws (rng_skip: 2, or 3 after the mixed branch's coin), so they
-// are independent jobs: compacted here into consecutive job slots (ballot + mbcnt), run by
-// the wave's active lanes in batches (the lane of active rank r takes slot base + r and pulls
-// its owner's inputs with ds_bpermute), and pulled back by their owners.  Per lane the values
-// are those of the two calls in order (bit-exact); the wave runs ceil(jobs / active lanes)
-// random_ray bodies instead of two.  own / wl: this wave's 128 + 64 bytes of LDS (job slot ->
-// owner lane, active rank -> lane).  Called at a point every active lane reaches.
-#ifdef MCPT_RR_STATS
-struct RrStats { unsigned long long calls = 0, batches = 0, jobs = 0, active = 0, over = 0, jobs1 = 0; };
-#define MCPT_RR_STATS_ARG , RrStats& st
-#else
-#define MCPT_RR_STATS_ARG
-#endif
-__device__ __forceinline__ void rr_jobs(bool need1, bool need2, const Rng& rng, uint32_t k2, f3 N, f3 D, float mx,
-                                        float my, f3& ray, f3& rd, unsigned char* own, unsigned char* wl,
-                                        int lane MCPT_RR_STATS_ARG) {
-  const uint64_t act = __ballot(1), m1 = __ballot(need1), m2 = __ballot(need2);
-  const int n_act = __builtin_popcountll(act), rank = mbcnt64(act);
-  const int n1 = __builtin_popcountll(m1), n_jobs = n1 + __builtin_popcountll(m2);
-#ifdef MCPT_RR_STATS   // diagnostic build only: per-wave job statistics (wave-uniform values)
-  st.calls++; st.batches += (n_jobs + n_act - 1) / n_act; st.jobs += n_jobs; st.active += n_act;
-  st.over += n_jobs > n_act; st.jobs1 += n1;
-#endif
-  const int s1 = mbcnt64(m1), s2 = n1 + mbcnt64(m2);
-  if (need1) own[s1] = (unsigned char)lane;
-  if (need2) own[s2] = (unsigned char)lane;
-  wl[rank] = (unsigned char)lane;
-  __builtin_amdgcn_wave_barrier();
-  for (int base = 0; base < n_jobs; base += n_act) {   // wave-uniform
-    const int sl = base + rank;
-    const bool job = sl < n_jobs;
-    const int o = job ? (int)own[sl] : lane;
-    Rng r;
-    r.x = bperm(o, rng.x); r.y = bperm(o, rng.y); r.z = bperm(o, rng.z);
-    const uint32_t k = bperm(o, k2);
-    const f3 Nj = mk(bpermf(o, N.x), bpermf(o, N.y), bpermf(o, N.z));
-    const f3 Dj = mk(bpermf(o, D.x), bpermf(o, D.y), bpermf(o, D.z));
-    const float xj = bpermf(o, mx), yj = bpermf(o, my);
-    f3 out = mk(0.0f, 0.0f, 0.0f);
-    if (job) {
-      if (sl >= n1) {   // the reflect branch's direction: random_ray(reflect(D,N), 1-mat.r*mat.g)
-        rng_skip(r, k);
-        out = random_ray(r, greflect(Dj, Nj), 1.0f - xj * yj);
-      } else {          // ray = random_ray(N, 1-mat.g)
-        out = random_ray(r, Nj, 1.0f - yj);
-      }
-    }
-    const bool in1 = need1 && s1 >= base && s1 < base + n_act;
-    const bool in2 = need2 && s2 >= base && s2 < base + n_act;
-    const int w1 = in1 ? (int)wl[s1 - base] : lane, w2 = in2 ? (int)wl[s2 - base] : lane;
-    const f3 o1 = mk(bpermf(w1, out.x), bpermf(w1, out.y), bpermf(w1, out.z));
-    const f3 o2 = mk(bpermf(w2, out.x), bpermf(w2, out.y), bpermf(w2, out.z));
-    if (in1) ray = o1;
-    if (in2) rd = o2;
-  }
-  __builtin_amdgcn_wave_barrier();
 }
 
 // ------------------------------------------------------------------------------------
@@ -1205,13 +999,8 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
   // segment-fastest item order: the pass segments of one tile are consecutive workgroups
   // (tile-fastest order was 1-12 % slower on one GPU and 7 % on a 1/8-row shard's launch:
   // profiles/r01_ab42_item_order.jsonl)
-  // A work item runs K = seg_per_item consecutive segments of its tile.  Each wave holds a
-  // pool of 64 x K units (pixel of its 8x8 block, segment): a lane starts with its own pixel's
-  // first segment and, whenever its unit ends, takes the next unclaimed unit of the pool
-  // (ballot + mbcnt at the end of a round), so a lane whose pixel is cheap (sky) works on
-  // the expensive pixels' other segments instead of idling until the wave's slowest lane
-  // is done.  A unit is one accumulation chunk of one pixel, summed in pass order and written
-  // to its segment slot when it ends: the bits do not depend on which lane runs it.
+  // A work item runs K = seg_per_item consecutive segments of its tile; a lane runs its pixel's
+  // segments one after another (each summed from 0 in pass order, written when it ends).
   const int K = p.seg_per_item > 1 ? p.seg_per_item : 1;
   const int n_groups = (p.n_segments + K - 1) / K;
   const int tile = item / n_groups, seg_lo = (item % n_groups) * K;
@@ -1220,8 +1009,8 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
   const int tiles_x = (p.W + kTileW - 1) / kTileW;
   const int bx0 = (tile % tiles_x) * kTileW + (wave % (kTileW / 8)) * 8;   // this wave's 8x8 block
   const int by0 = (tile / tiles_x) * kTileH + (wave / (kTileW / 8)) * 8;
-  int x = bx0 + (lane & 7);
-  int lr = by0 + (lane >> 3);
+  const int x = bx0 + (lane & 7);
+  const int lr = by0 + (lane >> 3);
   const bool live = x < p.W && lr < p.n_local_rows;   // (no early return: LDS staging barrier)
   const int cbase = floordiv(p.first_pass - 1, kPassChunk);   // chunk of the launch's first pass
   const int c0 = cbase + seg_lo;
@@ -1231,8 +1020,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
     pass_begin = p.first_pass + seg_lo;
     pass_end = pass_begin + 1;
   }
-  int y = live ? p.rows[lr] : 0;   // this shard's local row -> image row (mcpt_set_target*)
-  int pslot = tid;                 // LDS slot of this unit's pixel (per-pixel rows of s_pix, s_hit0)
+  const int y = live ? p.rows[lr] : 0;   // this shard's local row -> image row (mcpt_set_target*)
 
   SceneT<MESH, LDSS> s{p.nodes, p.leaves, p.ptype, p.prims, p.depth, p.minfo, p.mnodes, p.mleaves, p.mtris,
                        p.mverts, p.mnorms, p.flat_face};
@@ -1265,18 +1053,9 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
   // 19 KB per workgroup, + the staged scene (LDSS, <= kLdsSceneBytes): 7 workgroups/CU.
   __shared__ float s_pix[18][kTileThreads];
   __shared__ int s_hit0[kTileThreads];
-#if MCPT_UNIT_POOL
-  __shared__ unsigned int s_unext[kTileThreads / 64];   // next unclaimed unit of each wave's pool
-#endif
-#if MCPT_RR_COMPACT
-  __shared__ unsigned char s_own[kTileThreads / 64][128], s_wl[kTileThreads / 64][64];   // rr_jobs
-#endif
   const f3 Dcam0 = camera_dir(p, u, v);
-  s_pix[0][pslot] = Dcam0.x; s_pix[1][pslot] = Dcam0.y; s_pix[2][pslot] = Dcam0.z;
+  s_pix[0][tid] = Dcam0.x; s_pix[1][tid] = Dcam0.y; s_pix[2][tid] = Dcam0.z;
   s_pix[12][tid] = 0.0f; s_pix[13][tid] = 0.0f; s_pix[14][tid] = 0.0f;   // this segment's sum
-#if MCPT_UNIT_POOL
-  if (lane == 0) s_unext[wave] = 64u;
-#endif
   const f3 Ocam = mk(p.ox, p.oy, p.oz);
 
 
@@ -1310,9 +1089,9 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
     key0 = hit_key(h);
     if (h.hit()) geom_info<COUNT>(s, h, N0, P0, ev);
   }
-  s_pix[3][pslot] = N0.x; s_pix[4][pslot] = N0.y; s_pix[5][pslot] = N0.z;
-  s_pix[6][pslot] = P0.x; s_pix[7][pslot] = P0.y; s_pix[8][pslot] = P0.z;
-  s_hit0[pslot] = key0;   // shape << 28 | index, -1: miss
+  s_pix[3][tid] = N0.x; s_pix[4][tid] = N0.y; s_pix[5][tid] = N0.z;
+  s_pix[6][tid] = P0.x; s_pix[7][tid] = P0.y; s_pix[8][tid] = P0.z;
+  s_hit0[tid] = key0;   // shape << 28 | index, -1: miss
 
 #ifdef MCPT_STAMPS
   const unsigned long long st_p = __builtin_amdgcn_s_memtime() - st_k0;
@@ -1332,15 +1111,12 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
       part[0] = s_pix[12][tid]; part[1] = s_pix[13][tid]; part[2] = s_pix[14][tid];
     }
   };
-  // after pass++: the unit's last pass closes it (its sum to the segment slot) and the lane
-  // takes its next unit: its own pixel's next segment, or (MCPT_UNIT_POOL) the next unclaimed
-  // unit of its wave's pool (an LDS counter per wave: units 0..63 are the lanes' own first
-  // segments; units of pixels outside the shard are skipped).  With none left, pass stays at
+  // after pass++: the segment's last pass closes it (its sum to the segment slot) and the lane
+  // goes on with its pixel's next segment of the work item.  With none left, pass stays at
   // pass_end and the lane leaves the loop.
   auto next_chunk = [&]() {
     if (pass >= pass_end) {
       flush_sum();
-#if !MCPT_UNIT_POOL
       if (seg + 1 < seg_lo + seg_n) {
         seg++;
         const int c = c0 + (seg - seg_lo);
@@ -1348,33 +1124,10 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
         pass_end = min(p.first_pass + p.n_passes, (c + 1) * kPassChunk + 1);
         s_pix[12][tid] = 0.0f; s_pix[13][tid] = 0.0f; s_pix[14][tid] = 0.0f;
       }
-#else
-      const int n_units = 64 * seg_n;
-      for (;;) {
-        const int cu = (int)atomicAdd(&s_unext[wave], 1u);
-        if (cu >= n_units) break;
-        const int up = cu & 63;
-        x = bx0 + (up & 7);
-        lr = by0 + (up >> 3);
-        if (x < p.W && lr < p.n_local_rows) {
-          pslot = wave * 64 + up;
-          y = p.rows[lr];
-          seg = seg_lo + (cu >> 6);
-          const int c = c0 + (cu >> 6);
-          pass = max(p.first_pass, c * kPassChunk + 1);
-          pass_end = min(p.first_pass + p.n_passes, (c + 1) * kPassChunk + 1);
-          s_pix[12][tid] = 0.0f; s_pix[13][tid] = 0.0f; s_pix[14][tid] = 0.0f;
-          break;
-        }
-      }
-#endif
     }
   };
   Walk walk;
   walk.invD = mk(0.0f, 0.0f, 0.0f); walk.node = 0; walk.level = 0; walk.pending = 0;
-#ifdef MCPT_RR_STATS
-  RrStats rrst;
-#endif
   bool walking = false;   // a suspended per-lane walk is waiting to be continued
   while (pass < pass_end) {
 #ifdef MCPT_STAMPS
@@ -1389,7 +1142,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
       done = true;   // for(i=0; i<NB_BOUNCES ...) never runs: black
     } else {
       if (first) {
-        h.code = s_hit0[pslot];
+        h.code = s_hit0[tid];
       } else if (WAVE) {
         traverse<COUNT, WAVE>(s, O, D, h, ev);
       } else {
@@ -1447,52 +1200,15 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
       next_chunk();
       if (pass < pass_end) {
         rng = seed_for(((float)x + 0.5f) / (float)p.W, ((float)y + 0.5f) / (float)p.H, pass, p.date);
-        O = Ocam; D = mk(s_pix[0][pslot], s_pix[1][pslot], s_pix[2][pslot]);
+        O = Ocam; D = mk(s_pix[0][tid], s_pix[1][tid], s_pix[2][tid]);
         att = mk(0.8f, 0.8f, 0.8f); total = mk(0.0f, 0.0f, 0.0f);
         bounce = 0;
-        h.code = s_hit0[pslot];
+        h.code = s_hit0[tid];
         first = true;
       } else {
         ready = false;   // unit finished: the lane claims another at the end of the round
       }
     }
-#endif
-#if MCPT_RR_COMPACT
-    // shading part A (montecarlo.frag:118-124): the hit's N, P, colour and material, and the
-    // random_ray jobs of this round — `ray` for a non-emissive hit, and the reflect branch's
-    // direction where the lane will take it (the mixed branch's coin is drawn ahead at its
-    // place in the sequence, rng + 2)
-    const bool shade0 = ready && run && p.variant == 0 && phase == 0 && h.hit();
-    float4 c4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), m4 = c4;
-    bool need1 = false, need2 = false, mixed = false;
-    if (shade0) {
-      if (first) {
-        N = mk(s_pix[3][pslot], s_pix[4][pslot], s_pix[5][pslot]);
-        P = mk(s_pix[6][pslot], s_pix[7][pslot], s_pix[8][pslot]);
-      } else {
-        geom_info<COUNT>(s, h, N, P, ev);
-      }
-      ev.inc(EV_COLMAT);
-      c4 = s.prims[(size_t)h.index() * 8 + 6];
-      m4 = s.prims[(size_t)h.index() * 8 + 7];
-      if (m4.z <= 0.5f) {
-        need1 = true;
-        if (m4.x > 0.0f && c4.w == 1.0f) {
-          need2 = true;
-        } else if (c4.w < 1.0f && m4.x > 0.0f) {
-          mixed = true;
-          Rng t = rng;
-          rng_skip(t, 2);
-          need2 = rnd(t) > 0.5f;
-        }
-      }
-    }
-    f3 ray = mk(0.0f, 0.0f, 0.0f), rdir = ray;
-    rr_jobs(need1, need2, rng, mixed ? 3u : 2u, N, D, m4.x, m4.y, ray, rdir, s_own[wave], s_wl[wave], lane
-#ifdef MCPT_RR_STATS
-            , rrst
-#endif
-    );
 #endif
     if (ready && run) {
       if (p.variant != 0) {
@@ -1501,8 +1217,8 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
           res = mk(0.0f, 0.0f, 0.2f);
         } else {
           if (first) {
-            N = mk(s_pix[3][pslot], s_pix[4][pslot], s_pix[5][pslot]);
-            P = mk(s_pix[6][pslot], s_pix[7][pslot], s_pix[8][pslot]);
+            N = mk(s_pix[3][tid], s_pix[4][tid], s_pix[5][tid]);
+            P = mk(s_pix[6][tid], s_pix[7][tid], s_pix[8][tid]);
           }
           else geom_info<COUNT>(s, h, N, P, ev);
           ev.inc(EV_COLMAT);
@@ -1523,20 +1239,15 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
           res = add(total, mulv(att, gmix3(mk(0.5f, 0.5f, 0.9f), mk(1.0f, 1.0f, 0.8f), a)));
           done = true;
         } else {
-#if MCPT_RR_COMPACT
-          // part C: the rest of the shading with this lane's random_ray results
-          if (need1) rng_skip(rng, 2);   // the draws of `ray`
-#else
           if (first) {
-            N = mk(s_pix[3][pslot], s_pix[4][pslot], s_pix[5][pslot]);
-            P = mk(s_pix[6][pslot], s_pix[7][pslot], s_pix[8][pslot]);
+            N = mk(s_pix[3][tid], s_pix[4][tid], s_pix[5][tid]);
+            P = mk(s_pix[6][tid], s_pix[7][tid], s_pix[8][tid]);
           }
           else geom_info<COUNT>(s, h, N, P, ev);
           ev.inc(EV_COLMAT);
           const float4 c4 = s.prims[(size_t)h.index() * 8 + 6];
           const float4 m4 = s.prims[(size_t)h.index() * 8 + 7];
           f3 ray = random_ray(rng, N, 1.0f - m4.y);
-#endif
           const f3 col = mk(c4.x, c4.y, c4.z);
           const float alpha = c4.w;
           float rs = schlick(p.schlick_r0, D, N);
@@ -1558,13 +1269,8 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
               O = sub(P, muls(N, kBIAS));
               D = grefract(D, N, ior);
             } else if (alpha < 1.0f && m4.x > 0.0f) {
-#if MCPT_RR_COMPACT
-              rng_skip(rng, 1);   // the coin, drawn in part A
-              if (need2) {
-#else
               float r = rnd(rng);
               if (r > 0.5f) {
-#endif
                 reflect_push = true;
               } else {
                 inner = true;
@@ -1579,12 +1285,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
             }
             if (reflect_push) {
               f3 na = add(base, mulv(muls(muls(muls(att, alpha), rs), spec), mx));
-#if MCPT_RR_COMPACT
-              rng_skip(rng, 2);   // the draws of the new direction (rr_jobs)
-              const f3 rd = rdir;
-#else
               f3 rd = random_ray(rng, greflect(D, N), 1.0f - m4.x * m4.y);
-#endif
               att = na;
               O = add(P, muls(N, kBIAS));
               D = rd;
@@ -1626,7 +1327,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
       pass++;
       next_chunk();
       rng = seed_for(((float)x + 0.5f) / (float)p.W, ((float)y + 0.5f) / (float)p.H, pass, p.date);   // = (u, v)
-      O = Ocam; D = mk(s_pix[0][pslot], s_pix[1][pslot], s_pix[2][pslot]);
+      O = Ocam; D = mk(s_pix[0][tid], s_pix[1][tid], s_pix[2][tid]);
       att = mk(0.8f, 0.8f, 0.8f); total = mk(0.0f, 0.0f, 0.0f);
       bounce = 0; phase = 0;
     }
@@ -1662,19 +1363,6 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
       atomicAdd(p.events + 12, nw);
       atomicAdd(p.events + 13, ll);
       atomicAdd(p.events + 14, lw);
-    }
-  }
-#endif
-#ifdef MCPT_RR_STATS
-  // the wave's counters are uniform per lane; lanes leave the loop at different rounds, so the
-  // last lane out holds the wave's totals (max over lanes)
-  {
-    unsigned long long v[6] = {rrst.calls, rrst.batches, rrst.jobs, rrst.active, rrst.over, rrst.jobs1};
-    for (int off = 32; off > 0; off >>= 1)
-      for (int k = 0; k < 6; ++k) { unsigned long long o = __shfl_xor(v[k], off); v[k] = v[k] > o ? v[k] : o; }
-    if ((int)__lane_id() == __builtin_ffsll((long long)__ballot(1)) - 1 && p.events) {
-      for (int k = 0; k < 6; ++k) atomicAdd(p.events + k, v[k]);
-      atomicAdd(p.events + 6, 1ull);
     }
   }
 #endif
@@ -1875,14 +1563,8 @@ template <> struct TraceCfg<true> {
 // LDS of the LDSN trace kernel besides its scene copy: the waves' staged rays
 constexpr int kTraceLdsStaging = TraceCfg<true>::kWaves * TraceCfg<true>::kChunk * 32;
 
-// DUAL (MCPT_STREAM_DUAL=1, L1/L2 nodes only): each lane walks two staged rays at once
-// (walk_run2), at MCPT_MIN_WAVES_STREAM_DUAL waves per SIMD.
-#ifndef MCPT_MIN_WAVES_STREAM_DUAL
-#define MCPT_MIN_WAVES_STREAM_DUAL 5
-#endif
-template <bool LDSN, bool DUAL = false>
-__global__ __launch_bounds__(TraceCfg<LDSN>::kBlock, DUAL ? MCPT_MIN_WAVES_STREAM_DUAL : TraceCfg<LDSN>::kMinWaves)
-void stream_trace_kernel(StreamParams q) {
+template <bool LDSN>
+__global__ __launch_bounds__(TraceCfg<LDSN>::kBlock, TraceCfg<LDSN>::kMinWaves) void stream_trace_kernel(StreamParams q) {
   typedef TraceCfg<LDSN> C;
   constexpr int kChunkT = C::kChunk;
   const RenderParams& p = q.r;
@@ -1988,30 +1670,14 @@ void stream_trace_kernel(StreamParams q) {
   h.pl = O; h.dist = kFLTMAX; h.clear(); h.tri = 0; h.cull2 = 0.0;
   Walk w;
   w.invD = O; w.node = 0; w.level = 0; w.pending = 0;
-  if constexpr (!DUAL) {
-    for (;;) {
-      take(r, O, D, h, w);
-      if (__ballot(r >= 0) == 0) break;   // nothing staged and nothing left to claim
-      if (r >= 0) {
-        if (walk_run<false, true>(s, O, D, h, w, ev, q.refill, p.leaf_batch)) {
-          put_hit(r, h);
-          r = -1;
-        }
+  for (;;) {
+    take(r, O, D, h, w);
+    if (__ballot(r >= 0) == 0) break;   // nothing staged and nothing left to claim
+    if (r >= 0) {
+      if (walk_run<false, true>(s, O, D, h, w, ev, q.refill, p.leaf_batch)) {
+        put_hit(r, h);
+        r = -1;
       }
-    }
-  } else {
-    int r2 = -1;             // the lane's second ray
-    f3 O2 = O, D2 = O;
-    Hit h2 = h;
-    Walk w2 = w;
-    for (;;) {
-      take(r, O, D, h, w);
-      take(r2, O2, D2, h2, w2);
-      bool run_a = r >= 0, run_b = r2 >= 0;
-      if (__ballot(run_a || run_b) == 0) break;
-      if (run_a || run_b) walk_run2(s, O, D, h, w, run_a, O2, D2, h2, w2, run_b, 2 * q.refill, p.leaf_batch);
-      if (r >= 0 && !run_a) { put_hit(r, h); r = -1; }
-      if (r2 >= 0 && !run_b) { put_hit(r2, h2); r2 = -1; }
     }
   }
 #ifdef MCPT_STAMPS
@@ -2369,13 +2035,9 @@ bool mcpt_stream_lds_nodes_fit(int depth) {
   return depth <= 12 && mcpt_stream_lds_nodes_bytes(depth) + mcpt::kTraceLdsStaging <= 160 * 1024;
 }
 
-hipError_t mcpt_launch_stream_iter(const mcpt::StreamParams& q, int n_cu, bool lds_nodes, bool dual,
-                                   hipStream_t stream) {
+hipError_t mcpt_launch_stream_iter(const mcpt::StreamParams& q, int n_cu, bool lds_nodes, hipStream_t stream) {
   hipError_t e;
-  if (dual && !lds_nodes) {   // persistent: MCPT_MIN_WAVES_STREAM_DUAL workgroups of 4 waves per CU
-    hipLaunchKernelGGL((mcpt::stream_trace_kernel<false, true>), dim3((unsigned)n_cu * MCPT_MIN_WAVES_STREAM_DUAL),
-                       dim3(mcpt::kStreamBlock), 0, stream, q);
-  } else if (lds_nodes) {
+  if (lds_nodes) {
     const size_t shm = (size_t)mcpt_stream_lds_nodes_bytes(q.r.depth);
     // above the default 64 KiB of dynamic LDS (set on the calling thread's current device)
     e = hipFuncSetAttribute((const void*)mcpt::stream_trace_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -481,13 +481,14 @@ def test_gather_rows_then_render_again(mcpt_mod):
         r.close()
 
 
-@pytest.mark.parametrize("scene_id,n_cand", [(6, 4), (8, 7)])
+@pytest.mark.parametrize("scene_id,n_cand", [(6, 4), (8, 5)])
 def test_auto_two_round_trials_settle(mcpt_mod, renderer, scene_id, n_cand):
     """AUTO times each applicable candidate twice (candidate order, then reverse) on launches of
     one shape and then settles (mcpt_get_schedule reports it); mcpt.AUTO_TRIALS launches are
     enough; the image equals a fixed per-lane render of the same launches.  Candidates: per-lane,
-    wave-coherent, per-lane with 2 and 4 segments per item, and (BVH depth >= 8: scene 8) the
-    stream schedule and the deep-knob walks at 4 and 8 segments per item."""
+    wave-coherent (BVH depth < 8 only), per-lane with 2 and 4 segments per item, and (BVH depth
+    >= 8: scene 8) the deep-knob walks at 4 and 8 segments per item.  The stream schedule is never
+    timed by AUTO, nor is the wave-coherent walk on a deep BVH (its trial cost 8.4 s on C4)."""
     W, H, S = 1920, 1080, 256   # 8 pass segments: the segment-group candidates apply
     ipv, iv = mcpt_mod.camera_canonical(W, H)
 
@@ -508,9 +509,10 @@ def test_auto_two_round_trials_settle(mcpt_mod, renderer, scene_id, n_cand):
     assert not any(s["settled"] for s in sched[:2 * n_cand]), sched
     assert all(s["settled"] for s in sched[2 * n_cand:]), sched
     assert sched[-1]["seg_per_item"] in (1, 2, 4, 8), sched
-    assert sched[-1]["traversal"] in (("lane", "wave", "stream") if n_cand == 7 else ("lane", "wave"))
-    if n_cand == 7:
-        assert "stream" in {s["traversal"] for s in sched[:2 * n_cand]}, sched   # it was tried
+    tried = {s["traversal"] for s in sched[:2 * n_cand]}
+    assert "stream" not in tried, sched
+    assert ("wave" in tried) == (scene_id != 8), sched
+    assert sched[-1]["traversal"] in (("lane",) if scene_id == 8 else ("lane", "wave"))
     lane, n_l, fixed = run(1, mcpt_mod.AUTO_TRIALS + 1)
     renderer.set_traversal(0)
     assert all(s["settled"] and s["traversal"] == "lane" for s in fixed)

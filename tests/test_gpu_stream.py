@@ -134,17 +134,3 @@ def test_stream_lds_nodes_variant(mcpt_mod, oracle_mod, renderer, monkeypatch, s
     ref = _oracle(oracle_mod, sc, 40, 24, 20, 50, B)
     assert it > 0
     assert np.array_equal(_bits(gpu), _bits(ref.reshape(gpu.shape)))
-
-
-@pytest.mark.parametrize("scene_id,B", [(8, 12), (3, 8), (6, 8)])
-@pytest.mark.parametrize("slots", [1, 300])
-def test_stream_dual_walk_variant(mcpt_mod, oracle_mod, renderer, monkeypatch, scene_id, B, slots):
-    """The trace kernel with two walks per lane (MCPT_STREAM_DUAL=1, walk_run2; measured slower
-    and off by default) gives the same bits, including a pool of one slot
-    (every lane's second walk idle)."""
-    monkeypatch.setenv("MCPT_STREAM_DUAL", "1")
-    sc = mcpt_mod.Scene.reference(scene_id)
-    gpu, it = _render(mcpt_mod, renderer, sc, 40, 24, 20, 50, B, slots=slots)
-    ref = _oracle(oracle_mod, sc, 40, 24, 20, 50, B)
-    assert it > 0
-    assert np.array_equal(_bits(gpu), _bits(ref.reshape(gpu.shape)))
