@@ -294,20 +294,32 @@ def host_cpu():
     return os.cpu_count() or 1, model
 
 
-def cpu_threads() -> int:
-    """Threads for the CPU baseline: the host share of one GPU where the box sets it
-    (OMP_NUM_THREADS, 16 on the GPU box), else every logical CPU."""
-    n = os.cpu_count() or 1
-    t = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or n
-    return max(1, min(t, n))
+def cpus_available() -> int:
+    """CPUs this process may run on (its affinity mask): the host cores the CPU baseline uses."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
 
 
-def cpu_baseline(args, seconds: float, rough=None):
+def cpu_quota():
+    """CPUs' worth of time the process's cgroup grants (cpu.max quota / period), or None."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(args, seconds: float, rough=None, threads=None):
     """Oracle (C++ restatement, same arithmetic) on a bounded sample of the workload: every
     2nd row of the frame (every row for C1), 1-pass launches of increasing pass number
-    (1..spp) until the budget is spent (≈10 s), std::thread over rows."""
+    (1..spp) until the budget is spent (≈10 s), std::thread over rows on `threads` workers
+    (default: every CPU of the process's affinity mask)."""
     from oracle import oracle as orc
-    threads = cpu_threads()
+    avail = cpus_available()
+    threads = threads or avail
     nproc, model = host_cpu()
     prims, nodes, leaves, depth, _ = orc.scene(args.scene, args.light)
     if rough is not None:   # build_scene's override: material .y of every non-emissive record
@@ -328,9 +340,10 @@ def cpu_baseline(args, seconds: float, rough=None):
         if dt >= seconds or p > args.spp:
             break
     return {"value": round(samples / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "threads_used": threads, "cores_available": avail, "cgroup_cpu_quota": cpu_quota(),
             "host_logical_cpus": nproc, "cpu_model": model,
-            "threads_note": "std::thread workers = OMP_NUM_THREADS (the host share of one GPU on the box) "
-                            "capped at the host's logical CPUs",
+            "threads_note": "std::thread workers over rows; cores_available = the process's CPU affinity "
+                            "(os.sched_getaffinity), cgroup_cpu_quota = cpu.max quota/period if one is set",
             "sample": f"oracle/oracle.cpp, scene {args.scene} {W}x{H} "
                       f"{'every row' if row_step == 1 else f'every {row_step}nd row'} ({rows} rows), "
                       f"passes 1..{p - 1} ({samples} samples, {dt:.3g} s), B={args.bounces}, IOR {args.ior:g}"
@@ -468,8 +481,10 @@ def run_point(args, sr, rough, S, world, barrier, stat_dev):
     bytes_local = float((ev_local.astype(np.float64) * mcpt.Renderer.event_bytes()).sum())
     avg_trace_ms = float(np.mean([a for a, _ in kernel_ms]))
     avg_combine_ms = float(np.mean([b for _, b in kernel_ms]))
+    props = torch.cuda.get_device_properties(sr.device)
     stats = torch.tensor([bytes_local, avg_trace_ms, avg_combine_ms, float(ev_local[6]), gather_ms,
-                          float(sr.g.n_local)], dtype=torch.float64, device=stat_dev)
+                          float(sr.g.n_local), float(props.pci_domain_id), float(props.pci_bus_id),
+                          float(props.pci_device_id), float(sr.device.index)], dtype=torch.float64, device=stat_dev)
     if world > 1:
         allstats = [torch.zeros_like(stats) for _ in range(world)]
         dist.all_gather(allstats, stats)
@@ -586,6 +601,12 @@ def main():
                           "per_rank_trace_avg": [round(float(x), 3) for x in a[:, 1]],
                           "per_rank_rows": [int(x) for x in a[:, 5]],
                           "schedule_rank0": main_pt["sched"]},
+            # which physical GPU each rank rendered on (PCI domain:bus:device, from torch's device
+            # properties) and the process group's size: an N-GPU line names N devices
+            "devices": {"world_size": dist.get_world_size() if dist.is_initialized() else 1,
+                        "per_rank_pci": [f"{int(x[6]):04x}:{int(x[7]):02x}:{int(x[8]):02x}" for x in a],
+                        "per_rank_device_index": [int(x[9]) for x in a],
+                        "distinct_devices": len({(int(x[6]), int(x[7]), int(x[8])) for x in a})},
             "roofline": main_pt["roof"],
             "self_check": (None if not checks else
                            {"rows": checks[0]["rows"], "passes": checks[0]["passes"],
@@ -594,7 +615,13 @@ def main():
                             "points": len(checks)}),
         }
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds, main_pt["rough"])
+            # every available host core; beside it the 16-thread figure of rounds 1-3 (the host
+            # share of one GPU that the box's OMP_NUM_THREADS names), on a shorter sample
+            cb = cpu_baseline(args, args.cpu_seconds, main_pt["rough"])
+            if cb["threads_used"] > 16:
+                c16 = cpu_baseline(args, args.cpu_seconds / 2, main_pt["rough"], threads=16)
+                cb["at_16_threads"] = {k: c16[k] for k in ("value", "threads_used", "sample")}
+            out["cpu_baseline"] = cb
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

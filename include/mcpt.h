@@ -142,7 +142,7 @@ int mcpt_render_counted(mcpt_ctx* ctx, const float* invPV, const float* invV, in
                         unsigned long long* events);
 int mcpt_event_bytes(int event);
 
-#define MCPT_DEBUG_SLOTS 16
+#define MCPT_DEBUG_SLOTS 64
 /* Diagnostics: read (and optionally zero) the context's MCPT_DEBUG_SLOTS device counter slots
  * (the first MCPT_EV_COUNT are the event counters).
  * Only the counting launches and diagnostic builds (-DMCPT_STAMPS: wave-cycle section
@@ -344,17 +344,33 @@ int mcpt_write_png(const char* path, const float* rgb, int W, int H);
  * the same bits, because a pass's samples depend only on (pixel, pass, date) and the
  * accumulator is additive.  A file holds the accumulator sums (rows × W × RGB f32, as
  * mcpt_read_accum returns them), the passes they hold, the first pass of the next render call,
- * and a caller tag (scene and render parameters) that the reader compares.
- * Layout, little endian: "MCPTCKP1", int32 W, rows, pass_count, next_pass, tag bytes, the tag,
- * then the floats.  The write goes to `path`.tmp and is renamed over `path`, so an
- * interrupted write leaves the previous checkpoint intact. */
+ * a caller tag (scene and render parameters) that the reader compares, and the target's
+ * identity: the image height H and a hash of the context's image row ids (so a shard's
+ * checkpoint cannot be loaded into another shard or another frame of the same local size).
+ * Layout, little endian: "MCPTCKP2", int32 W, rows, pass_count, next_pass, tag bytes, H, uint64
+ * row-list hash, the tag, then the floats (H = hash = 0: no identity).  The write goes to a
+ * temporary file unique to the writer, is flushed to the device (fsync) and renamed over
+ * `path`, so an interrupted write or a host crash leaves the previous checkpoint intact.
+ * A resumed render equals the uninterrupted one bit for bit when its calls split the pass range
+ * at the same points (a call adds its own partial sum of a 32-pass chunk: DESIGN.md §3.3), e.g.
+ * the same --chunk in mcpt_render, or call boundaries on multiples of 32 passes. */
 #define MCPT_CHECKPOINT_TAG_MAX 1024
+/* The context's accumulator, pass count, `next_pass`, `tag` (may be NULL) and target identity.
+ * Synchronizes the context's stream. */
+int mcpt_checkpoint_save(mcpt_ctx* ctx, const char* path, int next_pass, const char* tag);
+/* Resume: loads a file written by mcpt_checkpoint_save for THIS target (W, local rows, H and
+ * row ids must match; MCPT_ERR_INVALID_ARG otherwise, and for a file without identity) and,
+ * when `tag` is not NULL, with this tag; sets the accumulator and pass count and returns the
+ * next call's first pass in *next_pass (may be NULL). */
+int mcpt_checkpoint_load(mcpt_ctx* ctx, const char* path, const char* tag, int* next_pass);
+/* File-level access without a context (no target identity: H = hash = 0). */
 int mcpt_checkpoint_write(const char* path, const float* rgb, int W, int rows, int pass_count, int next_pass,
                           const char* tag);
 /* Reads the header into W, rows, pass_count, next_pass (any may be NULL) and the tag into tag_out
  * (MCPT_CHECKPOINT_TAG_MAX bytes, NUL-terminated; may be NULL); the sums into rgb_out
  * (rows × W × 3 floats, at most `capacity` floats) unless it is NULL.  MCPT_ERR_INVALID_ARG for
- * a missing, foreign or truncated file, or sums larger than `capacity`. */
+ * a missing, foreign or truncated file, or sums larger than `capacity`.  Reads "MCPTCKP1" files
+ * (round 3, no identity) too. */
 int mcpt_checkpoint_read(const char* path, float* rgb_out, long long capacity, int* W, int* rows, int* pass_count,
                          int* next_pass, char* tag_out);
 

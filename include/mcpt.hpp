@@ -355,26 +355,17 @@ class Renderer {
     if (rgb.size() != (size_t)rows_ * W_ * 3) throw Error("write_accum: wrong size", MCPT_ERR_INVALID_ARG);
     check(mcpt_write_accum(c_, rgb.data(), passes), "mcpt_write_accum");
   }
-  // checkpoint / resume of a progressive render (mcpt_checkpoint_write / _read): the file holds
-  // the sums, their pass count, the next call's first pass and a tag of the render parameters
+  // checkpoint / resume of a progressive render (mcpt_checkpoint_save / _load): the file holds
+  // the sums, their pass count, the next call's first pass, a tag of the render parameters and
+  // the target's identity (H, row ids)
   void save_checkpoint(const std::string& path, int next_pass, const std::string& tag) const {
-    std::vector<float> acc;
-    const int n = read_accum(acc);
-    check(mcpt_checkpoint_write(path.c_str(), acc.data(), W_, rows_, n, next_pass, tag.c_str()),
-          "mcpt_checkpoint_write");
+    check(mcpt_checkpoint_save(c_, path.c_str(), next_pass, tag.c_str()), "mcpt_checkpoint_save");
   }
-  // returns the next first pass; throws if the file's shape or tag differs from this render's
+  // returns the next first pass; throws if the file belongs to another target / shard or its
+  // tag differs from this render's
   int load_checkpoint(const std::string& path, const std::string& tag) {
-    int w = 0, rows = 0, n = 0, next = 0;
-    std::vector<char> t(MCPT_CHECKPOINT_TAG_MAX);
-    check(mcpt_checkpoint_read(path.c_str(), nullptr, 0, &w, &rows, nullptr, nullptr, nullptr), "mcpt_checkpoint_read");
-    if (w != W_ || rows != rows_) throw Error("checkpoint: framebuffer shape differs", MCPT_ERR_INVALID_ARG);
-    std::vector<float> acc((size_t)rows * w * 3);
-    check(mcpt_checkpoint_read(path.c_str(), acc.data(), (long long)acc.size(), &w, &rows, &n, &next, t.data()),
-          "mcpt_checkpoint_read");
-    if (w != W_ || rows != rows_) throw Error("checkpoint: framebuffer shape differs", MCPT_ERR_INVALID_ARG);
-    if (tag != t.data()) throw Error("checkpoint: render parameters differ (" + std::string(t.data()) + ")", MCPT_ERR_INVALID_ARG);
-    write_accum(acc, n);
+    int next = 0;
+    check(mcpt_checkpoint_load(c_, path.c_str(), tag.c_str(), &next), "mcpt_checkpoint_load");
     return next;
   }
   // fs_frag: the averaged image (single-shard target)

@@ -133,8 +133,11 @@ int main(int argc, char** argv) {
       // spp - 1); a resumed run continues at the checkpoint's next pass with its sums loaded,
       // and the tag makes a resume with other render parameters fail
       char tag[256];
-      std::snprintf(tag, sizeof(tag), "scene=%d W=%d H=%d bounces=%d ior=%a light=%a date=%a variant=%d first=%d",
-                    a.scene, W, H, a.bounces, a.ior, a.light, a.date, a.variant, a.first_pass);
+      // (the chunk too: a call that splits a 32-pass accumulation chunk adds its own partial sum,
+      // so the resumed bits equal the uninterrupted run's only with the same call boundaries)
+      std::snprintf(tag, sizeof(tag),
+                    "scene=%d W=%d H=%d bounces=%d ior=%a light=%a date=%a variant=%d first=%d chunk=%d", a.scene, W,
+                    H, a.bounces, a.ior, a.light, a.date, a.variant, a.first_pass, a.chunk);
       int next = a.first_pass;
       if (!a.resume.empty()) next = r.load_checkpoint(a.resume, tag);
       const auto t0 = std::chrono::steady_clock::now();

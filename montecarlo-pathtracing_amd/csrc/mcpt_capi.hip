@@ -19,13 +19,21 @@
 #include "mcpt_internal.h"
 #include "mcpt_math.h"
 
+// The detail of the calling thread's last failed call (set_err), with its status.  "fresh"
+// until mcpt_error_string hands it out once, so a detail is never attached to a later error that
+// did not set one (HIP errors keep theirs: mcpt_error_string(MCPT_ERR_HIP) always returns it).
 static thread_local char g_last_error[256] = "";
+static thread_local char g_detail[320] = "";
+static thread_local int g_last_status = 0;
+static thread_local bool g_fresh = false;
 
 static int set_err(int status, const char* what, hipError_t e = hipSuccess) {
   if (e != hipSuccess)
     std::snprintf(g_last_error, sizeof(g_last_error), "%s: %s", what, hipGetErrorString(e));
   else
     std::snprintf(g_last_error, sizeof(g_last_error), "%s", what);
+  g_last_status = status;
+  g_fresh = true;
   return status;
 }
 
@@ -275,6 +283,16 @@ constexpr double kTuneMinSamples = 1 << 24;   // launches smaller than this are 
 extern "C" {
 
 const char* mcpt_error_string(int status) {
+  if (status != MCPT_ERR_HIP && status != MCPT_OK && g_fresh && g_last_status == status) {
+    g_fresh = false;
+    const char* base = status == MCPT_ERR_INVALID_ARG ? "invalid argument"
+                       : status == MCPT_ERR_NO_SCENE  ? "no scene uploaded"
+                       : status == MCPT_ERR_NO_TARGET ? "no render target"
+                       : status == MCPT_ERR_BAD_SCENE ? "malformed scene buffers"
+                                                      : "error";
+    std::snprintf(g_detail, sizeof(g_detail), "%s (%s)", base, g_last_error);
+    return g_detail;
+  }
   switch (status) {
     case MCPT_OK: return "ok";
     case MCPT_ERR_INVALID_ARG: return "invalid argument";
@@ -990,6 +1008,63 @@ int mcpt_write_accum(mcpt_ctx* c, const float* rgb, int pass_count) {
     HIP_OR_RETURN(hipMemcpyAsync(c->d_accum, rgb, c->accum_bytes, hipMemcpyHostToDevice, c->stream));
   HIP_OR_RETURN(hipStreamSynchronize(c->stream));
   c->pass_count = pass_count;
+  return MCPT_OK;
+}
+
+namespace mcpt {
+namespace host {
+int checkpoint_write_ex(const char* path, const float* rgb, int W, int rows, int pass_count, int next_pass,
+                        const char* tag, int H, unsigned long long rows_hash);
+int checkpoint_read_ex(const char* path, float* rgb_out, long long capacity, int* W, int* rows, int* pass_count,
+                       int* next_pass, char* tag_out, int* H, unsigned long long* rows_hash);
+}  // namespace host
+}  // namespace mcpt
+
+// identity of a context's target for its checkpoints: FNV-1a (64 bit) over its image row ids
+static unsigned long long rows_hash(const mcpt_ctx* c) {
+  unsigned long long h = 1469598103934665603ULL;
+  for (int y : c->rows)
+    for (int b = 0; b < 4; ++b) {
+      h ^= (unsigned long long)(((uint32_t)y >> (8 * b)) & 0xFFu);
+      h *= 1099511628211ULL;
+    }
+  return h ? h : 1;   // 0 means "no identity" in the file
+}
+
+int mcpt_checkpoint_save(mcpt_ctx* c, const char* path, int next_pass, const char* tag) {
+  if (!c || !path) return MCPT_ERR_INVALID_ARG;
+  if (!c->has_target) return MCPT_ERR_NO_TARGET;
+  std::vector<float> acc((size_t)c->n_local_rows * c->W * 3);
+  int n = 0;
+  const int st = mcpt_read_accum(c, acc.data(), &n);
+  if (st != MCPT_OK) return st;
+  if (mcpt::host::checkpoint_write_ex(path, acc.data(), c->W, c->n_local_rows, n, next_pass, tag, c->H, rows_hash(c)) !=
+      MCPT_OK)
+    return set_err(MCPT_ERR_INVALID_ARG, "mcpt_checkpoint_save: cannot write the file");
+  return MCPT_OK;
+}
+
+int mcpt_checkpoint_load(mcpt_ctx* c, const char* path, const char* tag, int* next_pass) {
+  if (!c || !path) return MCPT_ERR_INVALID_ARG;
+  if (!c->has_target) return MCPT_ERR_NO_TARGET;
+  int w = 0, rows = 0, n = 0, nxt = 0, h = 0;
+  unsigned long long hash = 0;
+  std::vector<char> t(MCPT_CHECKPOINT_TAG_MAX);
+  std::vector<float> acc((size_t)c->n_local_rows * c->W * 3);
+  if (mcpt::host::checkpoint_read_ex(path, acc.data(), (long long)acc.size(), &w, &rows, &n, &nxt, t.data(), &h,
+                                     &hash) != MCPT_OK)
+    return set_err(MCPT_ERR_INVALID_ARG, "mcpt_checkpoint_load: missing, foreign or truncated file, or not this target's size");
+  if (h == 0 || hash == 0)
+    return set_err(MCPT_ERR_INVALID_ARG,
+                   "mcpt_checkpoint_load: the file carries no target identity (mcpt_checkpoint_write); "
+                   "read it with mcpt_checkpoint_read and load it with mcpt_write_accum");
+  if (w != c->W || rows != c->n_local_rows || h != c->H || hash != rows_hash(c))
+    return set_err(MCPT_ERR_INVALID_ARG, "mcpt_checkpoint_load: the checkpoint belongs to another target or shard");
+  if (tag && std::strcmp(tag, t.data()) != 0)
+    return set_err(MCPT_ERR_INVALID_ARG, "mcpt_checkpoint_load: the render parameters differ (tag)");
+  const int st = mcpt_write_accum(c, acc.data(), n);
+  if (st != MCPT_OK) return st;
+  if (next_pass) *next_pass = nxt;
   return MCPT_OK;
 }
 

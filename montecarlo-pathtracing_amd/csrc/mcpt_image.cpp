@@ -9,7 +9,8 @@
 //    converted to 8-bit unorm by round(255·c) (GL float→unorm rule, no gamma), written as an
 //    8-bit RGB PNG (top row first) with stored (uncompressed) deflate blocks.
 //  * mcpt_checkpoint_write / _read: a progressive render's accumulator, pass count and next
-//    first pass in one file, so the pass loop (montecarlo.cpp:454-466) can stop and resume.
+//    first pass in one file, so the pass loop (montecarlo.cpp:454-466) can stop and resume;
+//    mcpt_checkpoint_save / _load (mcpt_capi.hip) add the target's identity (H, row-list hash).
 //  * mcpt_transfo_*, mcpt_mat4_mul: easycppogl Transfo (gl_eigen.cpp:29-105, degrees) and
 //    Eigen's float product, evaluated with the same arithmetic as the scene producer, so a
 //    C++ caller composing transforms gets the reference's matrices bit for bit.
@@ -18,8 +19,13 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <string>
+#include <thread>
 #include <vector>
+
+#include <fcntl.h>
+#include <unistd.h>
 
 #include "../../include/mcpt.h"
 
@@ -130,41 +136,67 @@ int mcpt_write_png(const char* path, const float* rgb, int W, int H) {
   return (std::fclose(f) == 0 && ok) ? MCPT_OK : MCPT_ERR_INVALID_ARG;
 }
 
-// checkpoint file (mcpt.h): magic, 5 int32 (W, rows, pass_count, next_pass, tag bytes), tag, floats
-static const char kCkptMagic[8] = {'M', 'C', 'P', 'T', 'C', 'K', 'P', '1'};
+// checkpoint file (mcpt.h): magic, 6 int32 (W, rows, pass_count, next_pass, tag bytes, H),
+// uint64 row-list hash, tag, floats.  H = 0 / hash = 0: no target identity (mcpt_checkpoint_write).
+// "MCPTCKP1" files (round 3: 5 int32, no identity) are still read.
+static const char kCkptMagic[8] = {'M', 'C', 'P', 'T', 'C', 'K', 'P', '2'};
+static const char kCkptMagicV1[8] = {'M', 'C', 'P', 'T', 'C', 'K', 'P', '1'};
 
-int mcpt_checkpoint_write(const char* path, const float* rgb, int W, int rows, int pass_count, int next_pass,
-                          const char* tag) {
-  if (!path || !rgb || W <= 0 || rows <= 0 || pass_count < 0) return MCPT_ERR_INVALID_ARG;
+namespace mcpt {
+namespace host {
+// The file is written to a temporary name unique to this process and thread, flushed to the
+// device (fsync) and renamed over `path`: a killed process or a host crash leaves either the
+// previous checkpoint or the new one, and two writers never share a temporary file.
+int checkpoint_write_ex(const char* path, const float* rgb, int W, int rows, int pass_count, int next_pass,
+                        const char* tag, int H, unsigned long long rows_hash) {
+  if (!path || !rgb || W <= 0 || rows <= 0 || pass_count < 0 || H < 0) return MCPT_ERR_INVALID_ARG;
   const size_t tag_len = tag ? std::strlen(tag) : 0;
   if (tag_len >= MCPT_CHECKPOINT_TAG_MAX) return MCPT_ERR_INVALID_ARG;
-  const std::string tmp = std::string(path) + ".tmp";
+  char suffix[64];
+  std::snprintf(suffix, sizeof(suffix), ".tmp.%ld.%zx", (long)getpid(), std::hash<std::thread::id>()(std::this_thread::get_id()));
+  const std::string tmp = std::string(path) + suffix;
   FILE* f = std::fopen(tmp.c_str(), "wb");
   if (!f) return MCPT_ERR_INVALID_ARG;
-  const int32_t hdr[5] = {W, rows, pass_count, next_pass, (int32_t)tag_len};
+  const int32_t hdr[6] = {W, rows, pass_count, next_pass, (int32_t)tag_len, H};
+  const uint64_t hash = rows_hash;
   const size_t n = (size_t)W * rows * 3;
-  bool ok = std::fwrite(kCkptMagic, 1, 8, f) == 8 && std::fwrite(hdr, sizeof(int32_t), 5, f) == 5 &&
-            std::fwrite(tag ? tag : "", 1, tag_len, f) == tag_len && std::fwrite(rgb, sizeof(float), n, f) == n;
+  bool ok = std::fwrite(kCkptMagic, 1, 8, f) == 8 && std::fwrite(hdr, sizeof(int32_t), 6, f) == 6 &&
+            std::fwrite(&hash, sizeof(hash), 1, f) == 1 && std::fwrite(tag ? tag : "", 1, tag_len, f) == tag_len &&
+            std::fwrite(rgb, sizeof(float), n, f) == n;
+  ok = ok && std::fflush(f) == 0 && fsync(fileno(f)) == 0;
   ok = (std::fclose(f) == 0) && ok;
   if (!ok || std::rename(tmp.c_str(), path) != 0) {
     std::remove(tmp.c_str());
     return MCPT_ERR_INVALID_ARG;
   }
+  // the rename itself reaches the device with the directory's metadata
+  std::string dir(path);
+  const size_t slash = dir.find_last_of('/');
+  dir = slash == std::string::npos ? std::string(".") : (slash == 0 ? std::string("/") : dir.substr(0, slash));
+  const int dfd = open(dir.c_str(), O_RDONLY | O_DIRECTORY);
+  if (dfd >= 0) {
+    (void)fsync(dfd);
+    (void)close(dfd);
+  }
   return MCPT_OK;
 }
 
-int mcpt_checkpoint_read(const char* path, float* rgb_out, long long capacity, int* W, int* rows, int* pass_count,
-                         int* next_pass, char* tag_out) {
+int checkpoint_read_ex(const char* path, float* rgb_out, long long capacity, int* W, int* rows, int* pass_count,
+                       int* next_pass, char* tag_out, int* H, unsigned long long* rows_hash) {
   if (!path) return MCPT_ERR_INVALID_ARG;
   FILE* f = std::fopen(path, "rb");
   if (!f) return MCPT_ERR_INVALID_ARG;
   char magic[8];
-  int32_t hdr[5];
+  int32_t hdr[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t hash = 0;
   char tag[MCPT_CHECKPOINT_TAG_MAX];
-  bool ok = std::fread(magic, 1, 8, f) == 8 && std::memcmp(magic, kCkptMagic, 8) == 0 &&
-            std::fread(hdr, sizeof(int32_t), 5, f) == 5 && hdr[0] > 0 && hdr[1] > 0 && hdr[2] >= 0 &&
-            hdr[4] >= 0 && hdr[4] < MCPT_CHECKPOINT_TAG_MAX &&
-            std::fread(tag, 1, (size_t)hdr[4], f) == (size_t)hdr[4];
+  bool ok = std::fread(magic, 1, 8, f) == 8;
+  const bool v2 = ok && std::memcmp(magic, kCkptMagic, 8) == 0;
+  ok = ok && (v2 || std::memcmp(magic, kCkptMagicV1, 8) == 0) &&
+       std::fread(hdr, sizeof(int32_t), v2 ? 6 : 5, f) == (size_t)(v2 ? 6 : 5) &&
+       (!v2 || std::fread(&hash, sizeof(hash), 1, f) == 1) && hdr[0] > 0 && hdr[1] > 0 && hdr[2] >= 0 &&
+       hdr[4] >= 0 && hdr[4] < MCPT_CHECKPOINT_TAG_MAX && hdr[5] >= 0 &&
+       std::fread(tag, 1, (size_t)hdr[4], f) == (size_t)hdr[4];
   if (ok && rgb_out) {
     const size_t n = (size_t)hdr[0] * hdr[1] * 3;
     ok = capacity >= 0 && n <= (size_t)capacity && std::fread(rgb_out, sizeof(float), n, f) == n;
@@ -177,7 +209,22 @@ int mcpt_checkpoint_read(const char* path, float* rgb_out, long long capacity, i
   if (pass_count) *pass_count = hdr[2];
   if (next_pass) *next_pass = hdr[3];
   if (tag_out) std::memcpy(tag_out, tag, (size_t)hdr[4] + 1);
+  if (H) *H = hdr[5];
+  if (rows_hash) *rows_hash = hash;
   return MCPT_OK;
+}
+}  // namespace host
+}  // namespace mcpt
+
+int mcpt_checkpoint_write(const char* path, const float* rgb, int W, int rows, int pass_count, int next_pass,
+                          const char* tag) {
+  return mcpt::host::checkpoint_write_ex(path, rgb, W, rows, pass_count, next_pass, tag, 0, 0);
+}
+
+int mcpt_checkpoint_read(const char* path, float* rgb_out, long long capacity, int* W, int* rows, int* pass_count,
+                         int* next_pass, char* tag_out) {
+  return mcpt::host::checkpoint_read_ex(path, rgb_out, capacity, W, rows, pass_count, next_pass, tag_out, nullptr,
+                                        nullptr);
 }
 
 int mcpt_transfo_translate(float x, float y, float z, float* out16) {

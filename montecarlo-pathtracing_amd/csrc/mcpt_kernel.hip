@@ -178,6 +178,50 @@ struct Ev {
   __device__ __forceinline__ void inc(int e) { if (COUNT) c.v[e]++; }
 };
 
+#ifdef MCPT_LANESTATS
+// Diagnostic build only (tools/lanestats.py; never timed): per-wave lane accounting of the deep
+// walk.  The wave's first active lane adds wave-level values (ballot popcounts, iteration counts)
+// to its wave's LDS row; render_kernel flushes the rows to the debug slots at its end.
+enum {
+  LS_NODE_IT, LS_NODE_LN, LS_NE_WV, LS_NE_LN, LS_OUT_WV, LS_OUT_LN, LS_VAL_WV, LS_VAL_LN,
+  LS_LEAF_IT, LS_LEAF_LN, LS_PRIM_LN, LS_SPH_WV, LS_SPH_LN, LS_CUBE_WV, LS_CUBE_LN, LS_CYL_WV,
+  LS_CYL_LN, LS_QUAD_WV, LS_QUAD_LN, LS_WALK_IT, LS_WALK_LN, LS_WALK_CALLS, LS_ROUNDS, LS_ROUND_LN,
+  LS_SHADE_WV, LS_SHADE_LN, LS_RR2_WV, LS_RR2_LN, LS_WAVES, LS_COUNT
+};
+__device__ __forceinline__ unsigned* ls_row() {
+  __shared__ unsigned s_ls[16][LS_COUNT];
+  return s_ls[threadIdx.x >> 6];
+}
+__device__ __forceinline__ bool ls_lead() { return (int)__lane_id() == __builtin_ffsll((long long)__ballot(1)) - 1; }
+__device__ __forceinline__ void ls_add(int k, unsigned v) { if (ls_lead()) ls_row()[k] += v; }
+__device__ __forceinline__ unsigned ls_pop(bool b) { return (unsigned)__builtin_popcountll(__ballot(b)); }
+// (lanes, waves) of a per-lane condition: popcount and whether any lane holds it
+__device__ __forceinline__ void ls_cond(int k_wv, int k_ln, bool b) {
+  const unsigned n = ls_pop(b);
+  ls_add(k_wv, n ? 1u : 0u);
+  ls_add(k_ln, n);
+}
+// which stage of box_test a child reaches: 0 empty (not tested), 1 inside, 2 faces (no valid
+// face), 3 a valid face (cull compare)
+__device__ __forceinline__ int box_stage(float4 a0, float4 a1, float4 a2, f3 O, f3 D, f3 invD) {
+  if (a0.w == 0.0f) return 0;
+  f3 c = mk(a0.x, a0.y, a0.z), w = mk(a1.x, a1.y, a1.z), iw = mk(a2.x, a2.y, a2.z);
+  f3 Oi = mulv(sub(O, c), iw);
+  f3 Di = mulv(D, iw);
+  if (__builtin_fabsf(Oi.x) < 1.0f && __builtin_fabsf(Oi.y) < 1.0f && __builtin_fabsf(Oi.z) < 1.0f) return 1;
+  f3 rD = mulv(invD, w);
+  const bool dv[3] = {__builtin_fabsf(Di.x) > kEPS, __builtin_fabsf(Di.y) > kEPS, __builtin_fabsf(Di.z) > kEPS};
+  const float o[3] = {Oi.x, Oi.y, Oi.z}, d[3] = {Di.x, Di.y, Di.z}, r[3] = {rD.x, rD.y, rD.z};
+  for (int f = 0; f < 6; ++f) {
+    const int c0 = f / 2, c1 = (c0 + 1) % 3, c2 = (c0 + 2) % 3;
+    const float a = ((f % 2 ? 1.0f : -1.0f) - o[c0]) * r[c0];
+    if (dv[c0] && a > kEPS && __builtin_fabsf(o[c1] + a * d[c1]) <= 1.0f && __builtin_fabsf(o[c2] + a * d[c2]) <= 1.0f)
+      return 3;
+  }
+  return 2;
+}
+#endif
+
 // intersect_bv raytracer_func.frag:314-352; divisions as hoisted reciprocals (contract).
 // WAVE: the all-lanes-inside early out is taken wave-uniformly (big boxes such as the
 // ground's contain every ray origin).
@@ -261,6 +305,12 @@ __device__ __forceinline__ void node_tests(const SR& s, const float4* __restrict
                  "v"(r2.y), "v"(r2.z));
     hl = (COUNT || l0.w != 0.0f) && box_test<false>(l0, l1, l2, O, D, invD, cull2);
     hr = (COUNT || r0.w != 0.0f) && box_test<false>(r0, r1, r2, O, D, invD, cull2);
+#ifdef MCPT_LANESTATS
+    const int sl = box_stage(l0, l1, l2, O, D, invD), sr = box_stage(r0, r1, r2, O, D, invD);
+    ls_cond(LS_NE_WV, LS_NE_LN, sl >= 1); ls_cond(LS_NE_WV, LS_NE_LN, sr >= 1);
+    ls_cond(LS_OUT_WV, LS_OUT_LN, sl >= 2); ls_cond(LS_OUT_WV, LS_OUT_LN, sr >= 2);
+    ls_cond(LS_VAL_WV, LS_VAL_LN, sl >= 3); ls_cond(LS_VAL_WV, LS_VAL_LN, sr >= 3);
+#endif
   } else {
     const float4 l0 = nodes[j * 3], r0 = nodes[j * 3 + 3];
     hl = (COUNT || l0.w != 0.0f) && box_test<false>(l0, nodes[j * 3 + 1], nodes[j * 3 + 2], O, D, invD, cull2);
@@ -612,6 +662,9 @@ __device__ __forceinline__ bool walk_run(const SR& s, f3 O, f3 D, Hit& h, Walk& 
                                          int leaf_batch) {
   const int leaf0 = (1 << s.depth) - 1;
   const int n0 = SUSPEND ? __builtin_popcountll(__ballot(1)) : 0;
+#ifdef MCPT_LANESTATS
+  ls_add(LS_WALK_CALLS, 1u);
+#endif
   for (;;) {
     bool pop = true;
     bool is_leaf = w.node >= leaf0;
@@ -624,6 +677,22 @@ __device__ __forceinline__ bool walk_run(const SR& s, f3 O, f3 D, Hit& h, Walk& 
     }
 #ifdef MCPT_STAMPS
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();   // wave-uniform stamps
+#endif
+#ifdef MCPT_LANESTATS
+    ls_add(LS_WALK_IT, 1u);
+    ls_add(LS_WALK_LN, ls_pop(true));
+    {
+      const unsigned nn = ls_pop(do_node), nl = ls_pop(do_leaf);
+      ls_add(LS_NODE_IT, nn ? 1u : 0u); ls_add(LS_NODE_LN, nn);
+      ls_add(LS_LEAF_IT, nl ? 1u : 0u); ls_add(LS_LEAF_LN, nl);
+      int pp = do_leaf ? s.leaves[(uint32_t)(w.node - leaf0)] : -1;
+      const int ty = pp >= 0 ? (s.ptype[pp] & 15) : -1;
+      ls_add(LS_PRIM_LN, ls_pop(pp >= 0 && s.ptype[pp] >= 0));
+      ls_cond(LS_SPH_WV, LS_SPH_LN, ty == CODE_SPHERE);
+      ls_cond(LS_CUBE_WV, LS_CUBE_LN, ty == CODE_CUBE);
+      ls_cond(LS_CYL_WV, LS_CYL_LN, ty == CODE_CYLINDER);
+      ls_cond(LS_QUAD_WV, LS_QUAD_LN, ty == CODE_QUAD);
+    }
 #endif
     if (do_leaf) {
       ev.inc(EV_LEAF);
@@ -1041,7 +1110,13 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
   }
   Ev<COUNT> ev;
   ev.init();
+#ifdef MCPT_LANESTATS
+  for (int k = lane; k < LS_COUNT; k += 64) ls_row()[k] = 0u;
+  __builtin_amdgcn_wave_barrier();
+  if (!live) return;   // (diagnostic build: frames of whole tiles only)
+#else
   if (!live) return;
+#endif
 
   const float u = ((float)x + 0.5f) / (float)p.W;
   const float v = ((float)y + 0.5f) / (float)p.H;
@@ -1129,10 +1204,17 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
   Walk walk;
   walk.invD = mk(0.0f, 0.0f, 0.0f); walk.node = 0; walk.level = 0; walk.pending = 0;
   bool walking = false;   // a suspended per-lane walk is waiting to be continued
+#ifdef MCPT_LANESTATS
+  ls_add(LS_WAVES, 1u);
+#endif
   while (pass < pass_end) {
 #ifdef MCPT_STAMPS
     const unsigned long long st_a = __builtin_amdgcn_s_memtime();
     st_it++;
+#endif
+#ifdef MCPT_LANESTATS
+    ls_add(LS_ROUNDS, 1u);
+    ls_add(LS_ROUND_LN, ls_pop(true));
 #endif
     bool done = false;
     f3 res = mk(0.0f, 0.0f, 0.0f);
@@ -1247,6 +1329,9 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
           ev.inc(EV_COLMAT);
           const float4 c4 = s.prims[(size_t)h.index() * 8 + 6];
           const float4 m4 = s.prims[(size_t)h.index() * 8 + 7];
+#ifdef MCPT_LANESTATS
+          ls_cond(LS_SHADE_WV, LS_SHADE_LN, true);
+#endif
           f3 ray = random_ray(rng, N, 1.0f - m4.y);
           const f3 col = mk(c4.x, c4.y, c4.z);
           const float alpha = c4.w;
@@ -1285,6 +1370,9 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
             }
             if (reflect_push) {
               f3 na = add(base, mulv(muls(muls(muls(att, alpha), rs), spec), mx));
+#ifdef MCPT_LANESTATS
+              ls_cond(LS_RR2_WV, LS_RR2_LN, true);
+#endif
               f3 rd = random_ray(rng, greflect(D, N), 1.0f - m4.x * m4.y);
               att = na;
               O = add(P, muls(N, kBIAS));
@@ -1367,6 +1455,10 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
   }
 #endif
 
+#ifdef MCPT_LANESTATS
+  if (ls_lead() && p.events)
+    for (int k = 0; k < LS_COUNT; ++k) atomicAdd(p.events + 16 + k, (unsigned long long)ls_row()[k]);
+#endif
   if (COUNT) {
 #pragma unroll
     for (int e = 0; e < EV_COUNT; ++e) {

@@ -42,7 +42,7 @@ SCENE_KEYS = {1: "Q", 2: "W", 3: "E", 4: "R", 5: "T", 6: "Y", 7: "U", 8: "I"}
 _HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-DEBUG_SLOTS = 16   # MCPT_DEBUG_SLOTS
+DEBUG_SLOTS = 64   # MCPT_DEBUG_SLOTS
 
 
 class MCPTError(RuntimeError):
@@ -144,6 +144,8 @@ def _declare(L: ctypes.CDLL) -> None:
         "mcpt_write_png": (i, [ctypes.c_char_p, fp, i, i]),
         "mcpt_write_accum": (i, [_vp, fp, i]),
         "mcpt_checkpoint_write": (i, [ctypes.c_char_p, fp, i, i, i, i, ctypes.c_char_p]),
+        "mcpt_checkpoint_save": (i, [_vp, ctypes.c_char_p, i, ctypes.c_char_p]),
+        "mcpt_checkpoint_load": (i, [_vp, ctypes.c_char_p, ctypes.c_char_p, ip]),
         "mcpt_checkpoint_read": (i, [ctypes.c_char_p, fp, ctypes.c_longlong, ip, ip, ip, ip, ctypes.c_char_p]),
     }
     for name, (res, args) in sig.items():
@@ -558,20 +560,19 @@ class Renderer:
         _check(lib().mcpt_write_accum(self._h, _fp(a), int(pass_count)), "mcpt_write_accum")
 
     def save_checkpoint(self, path: str, next_pass: int, tag: str = "") -> None:
-        """Write this context's accumulator, its pass count and `next_pass` to `path`."""
-        acc, n = self.read_accum()
-        checkpoint_write(path, acc, n, next_pass, tag)
+        """mcpt_checkpoint_save: this context's accumulator, its pass count, `next_pass`, `tag` and
+        the target's identity (H, row ids) to `path`."""
+        _check(lib().mcpt_checkpoint_save(self._h, str(path).encode(), int(next_pass), tag.encode()),
+               "mcpt_checkpoint_save")
 
     def load_checkpoint(self, path: str, tag: Optional[str] = None) -> int:
-        """Resume from `path`: checks the target shape (and `tag`, if given), loads the sums and
-        pass count, returns the first pass of the next render call."""
-        acc, n, nxt, t = checkpoint_read(path)
-        if acc.shape != (self.n_local_rows, self.W, 3):
-            raise MCPTError(f"load_checkpoint: checkpoint is {acc.shape}, target {(self.n_local_rows, self.W, 3)}")
-        if tag is not None and t != tag:
-            raise MCPTError(f"load_checkpoint: tag {t!r} != {tag!r}")
-        self.write_accum(acc, n)
-        return nxt
+        """mcpt_checkpoint_load: resume from `path` — it must have been saved for this target
+        (W, H, row ids) and, if `tag` is given, with that tag; loads the sums and pass count and
+        returns the first pass of the next render call."""
+        nxt = ctypes.c_int()
+        _check(lib().mcpt_checkpoint_load(self._h, str(path).encode(), None if tag is None else tag.encode(),
+                                          ctypes.byref(nxt)), "mcpt_checkpoint_load")
+        return nxt.value
 
     def accum_device_ptr(self) -> Tuple[int, int]:
         p = _vp()

@@ -76,10 +76,16 @@ class FrameGather:
 
     ``gather(local)``: local is [n_local_rows, W, 3] on this rank's device; returns the
     assembled [H, W, 3] frame on `dst` (None on other ranks).
+
+    At world 1 the send buffer is the frame and no collective runs, unless
+    ``force_collective``: then the world-1 gather goes through the process group like any other
+    (the test that drives the RCCL branch on a one-GPU box, tests/test_gpu_dist.py).
     """
 
     def __init__(self, H: int, W: int, band_rows: int, world: int, rank: int, device: torch.device,
-                 dst: int = 0, group=None, use_gather: bool = True, partition: str = "bands"):
+                 dst: int = 0, group=None, use_gather: bool = True, partition: str = "bands",
+                 force_collective: bool = False):
+        self.collective = world > 1 or force_collective
         self.H, self.W, self.band_rows, self.world, self.rank = H, W, band_rows, world, rank
         self.dst, self.group, self.device, self.partition = dst, group, device, partition
         self.m = max_local_rows(H, band_rows, world, partition)
@@ -93,12 +99,12 @@ class FrameGather:
             self.recv, self.recv_list = None, None
         self.index = torch.as_tensor(frame_row_index(H, band_rows, world, partition), device=device)
         self.frame = (torch.empty((H, W, 3), dtype=torch.float32, device=device)
-                      if rank == dst and world > 1 else None)
+                      if rank == dst and self.collective else None)
 
     def gather(self, local: Optional[torch.Tensor] = None) -> Optional[torch.Tensor]:
         if local is not None:
             self.send[: self.n_local].copy_(local)
-        if self.world == 1:
+        if not self.collective:
             return self.send
         staged = self.device.type != "cpu" and dist.get_backend(self.group) == "gloo"
         if staged:   # rehearsal of the N>1 path on one GPU (gloo collectives need host tensors)
@@ -126,7 +132,7 @@ class ShardedRenderer:
     """
 
     def __init__(self, W: int, H: int, band_rows: int = 8, world: int = 1, rank: int = 0,
-                 local_rank: int = 0, group=None, partition: str = "balanced"):
+                 local_rank: int = 0, group=None, partition: str = "balanced", force_collective: bool = False):
         import mcpt
         self.device = torch.device("cuda", local_rank)
         self.r = mcpt.Renderer(local_rank)
@@ -142,7 +148,8 @@ class ShardedRenderer:
             self.r.set_target_rows(W, H, local_rows(H, band_rows, world, rank, partition))
         self.W, self.H, self.band_rows, self.world, self.rank = W, H, band_rows, world, rank
         self.partition = partition
-        self.g = FrameGather(H, W, band_rows, world, rank, self.device, group=group, partition=partition)
+        self.g = FrameGather(H, W, band_rows, world, rank, self.device, group=group, partition=partition,
+                             force_collective=force_collective)
         # the gather buffers were allocated (and zero-filled) on the caller's stream
         self.stream.wait_stream(torch.cuda.current_stream(self.device))
 

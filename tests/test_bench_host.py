@@ -140,4 +140,17 @@ def test_host_cpu_statement():
     n, model = bench.host_cpu()
     assert n == os.cpu_count()
     assert model is None or isinstance(model, str)
-    assert 1 <= bench.cpu_threads() <= n
+    assert bench.cpus_available() == len(os.sched_getaffinity(0))
+    q = bench.cpu_quota()
+    assert q is None or q > 0
+
+
+def test_cpu_baseline_uses_available_cores():
+    """The CPU baseline runs one worker per CPU of the process's affinity mask (verdict r03:
+    not OMP_NUM_THREADS) and states it; a bounded C1 sample keeps this a quick CPU test."""
+    args = bench.parse(["--config", "c1"])
+    cb = bench.cpu_baseline(args, 0.2)
+    assert cb["threads_used"] == cb["cores"] == cb["cores_available"] == len(os.sched_getaffinity(0))
+    assert cb["value"] > 0 and cb["kind"] == "port"
+    c1 = bench.cpu_baseline(args, 0.2, threads=1)
+    assert c1["threads_used"] == 1

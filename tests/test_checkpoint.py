@@ -20,7 +20,7 @@ def test_checkpoint_file_roundtrip(mcpt_mod, tmp_path):
     acc[0, 0] = [np.nan, np.inf, -0.0]
     p = str(tmp_path / "a.ckpt")
     mcpt_mod.checkpoint_write(p, acc, 96, 97, "scene=6 bounces=8")
-    assert not os.path.exists(p + ".tmp")
+    assert sorted(f.name for f in tmp_path.iterdir()) == ["a.ckpt"]   # no temporary file left
     back, n, nxt, tag = mcpt_mod.checkpoint_read(p)
     assert np.array_equal(back.view(np.uint32), acc.view(np.uint32))
     assert (n, nxt, tag) == (96, 97, "scene=6 bounces=8")
@@ -95,13 +95,46 @@ def test_resume_bit_equal_to_uninterrupted(mcpt_mod, tmp_path):
     c = renderer()
     c.render(ipv, iv, 1, 64, 0.0, B, 1.0, mcpt_mod.MONTECARLO)
     assert np.array_equal(c.read_accum()[0].view(np.uint32), want.view(np.uint32))
-    with pytest.raises(mcpt_mod.MCPTError):
+    with pytest.raises(mcpt_mod.MCPTError, match="tag"):
         renderer().load_checkpoint(p, "scene=7")
     small = mcpt_mod.Renderer(0)
     small.upload_scene(sc)
     small.set_target(W // 2, H)
     with pytest.raises(mcpt_mod.MCPTError):
         small.load_checkpoint(p)
+
+
+@pytest.mark.gpu
+def test_checkpoint_refuses_other_shard_or_frame(mcpt_mod, tmp_path):
+    """A checkpoint carries its target's identity (H and the row ids): a shard's file does not
+    load into another shard with the same row count, nor into a taller frame whose shard has the
+    same local size, nor does a file written without identity (mcpt_checkpoint_write) load into a
+    context (advisor r03)."""
+    W, H = 64, 48
+    sc = mcpt_mod.Scene.reference(6)
+    ipv, iv = mcpt_mod.camera_canonical(W, H)
+
+    def shard(h, rows):
+        r = mcpt_mod.Renderer(0)
+        r.upload_scene(sc)
+        r.set_target_rows(W, h, rows)
+        return r
+
+    rows0, rows1 = list(range(0, H, 2)), list(range(1, H, 2))   # same local row count
+    a = shard(H, rows0)
+    a.render(ipv, iv, 1, 4, 0.0, 8, 1.0, mcpt_mod.MONTECARLO)
+    p = str(tmp_path / "shard0.ckpt")
+    a.save_checkpoint(p, 5, "s6")
+    assert shard(H, rows0).load_checkpoint(p, "s6") == 5
+    with pytest.raises(mcpt_mod.MCPTError, match="another target or shard"):
+        shard(H, rows1).load_checkpoint(p, "s6")
+    with pytest.raises(mcpt_mod.MCPTError, match="another target or shard"):
+        shard(2 * H, rows0).load_checkpoint(p, "s6")
+    raw = str(tmp_path / "raw.ckpt")
+    acc, n = a.read_accum()
+    mcpt_mod.checkpoint_write(raw, acc, n, 5, "s6")
+    with pytest.raises(mcpt_mod.MCPTError, match="no target identity"):
+        shard(H, rows0).load_checkpoint(raw, "s6")
 
 
 @pytest.mark.gpu

@@ -68,3 +68,48 @@ def test_sharded_renderer_gather_ordered(world):
     diff, n = q.get(timeout=120)
     assert n == steps * S
     assert diff == 0, f"{diff} channels of the gathered frame differ from the one-context render"
+
+
+def _nccl_worker(rank, port, W, H, S, steps, q):
+    """World 1 over RCCL: init_process_group("nccl", device_id=cuda:0) and FrameGather's
+    collective branch (force_collective skips the world-1 shortcut), so the code path the
+    driver's 8-GPU run takes executes here: the gathered frame must equal the renderer's own
+    accumulator bit for bit."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "montecarlo-pathtracing_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        import mcpt
+        from mcpt.dist import ShardedRenderer
+        ipv, iv = mcpt.camera_canonical(W, H)
+        sr = ShardedRenderer(W, H, 8, 1, 0, 0, force_collective=True)
+        sr.upload_scene(mcpt.Scene.reference(6))
+        frame = None
+        for k in range(steps):
+            sr.render(ipv, iv, k * S + 1, S, 0.0, 8, 1.0, mcpt.MONTECARLO)
+            frame = sr.gather()
+        got = frame.cpu().numpy()
+        want, n = sr.r.read_accum()
+        props = torch.cuda.get_device_properties(0)
+        q.put((dist.get_backend(), dist.get_world_size(), frame.data_ptr() != sr.g.send.data_ptr(),
+               int((got.view(np.uint32) != want.view(np.uint32)).sum()), n, props.pci_bus_id))
+        sr.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_gather_world1_collective():
+    """The RCCL branch of FrameGather.gather (dist.gather over the nccl backend) and
+    init_process_group("nccl", device_id=...) run on the one GPU of the box."""
+    W, H, S, steps = 640, 360, 64, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    mp.start_processes(_nccl_worker, args=(_free_port(), W, H, S, steps, q), nprocs=1, join=True,
+                       start_method="spawn")
+    backend, world, separate, diff, n, bus = q.get(timeout=120)
+    assert backend == "nccl" and world == 1
+    assert separate, "the frame must come out of the collective, not alias the send buffer"
+    assert n == steps * S
+    assert diff == 0, f"{diff} channels of the RCCL-gathered frame differ from the accumulator"
