@@ -66,11 +66,11 @@ __device__ __forceinline__ float wlength3(f3 a) {
 }
 template <bool FAST>
 __device__ __forceinline__ float wsqrt(float x) {
-  if constexpr (FAST) return sqrt_rn(x); else return __builtin_sqrtf(x);
+  if constexpr (FAST || kDriverRoots) return sqrt_rn(x); else return __builtin_sqrtf(x);
 }
 template <bool FAST>
 __device__ __forceinline__ float wrcp(float x) {
-  if constexpr (FAST) return rcp_rn(x); else return 1.0f / x;
+  if constexpr (FAST || kDriverRoots) return rcp_rn(x); else return 1.0f / x;
 }
 
 // Closest-hit record.  The world-space hit point is not kept: it is xpoint(transform of
@@ -488,14 +488,14 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
     float delta4 = OD * OD - D2 * (OO - 1.0f);
     if (delta4 > 0.0f) {
       float sq = wsqrt<SR::kFastSqrt>(delta4);
-      float a = -(OD + sq) / D2;
+      float a = fdiv(-(OD + sq), D2);
       if (a > kEPS) accept(CODE_SPHERE, 0, add(O, muls(D, a)));
-      a = -(OD - sq) / D2;
+      a = fdiv(-(OD - sq), D2);
       if (a > kEPS) accept(CODE_SPHERE, 0, add(O, muls(D, a)));
     }
   } else if (t == CODE_QUAD) {
     if (D.z > -kEPS) return;
-    float a = -O.z / D.z;
+    float a = fdiv(-O.z, D.z);
     f3 Pl = add(O, muls(D, a));
     if (__builtin_fabsf(Pl.x) > 1.0f || __builtin_fabsf(Pl.y) > 1.0f) return;
     accept(CODE_QUAD, 0, Pl);
@@ -507,7 +507,7 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
       const int c0 = f / 2, c1 = (c0 + 1) % 3, c2 = (c0 + 2) % 3;
       if (__builtin_fabsf(d[c0]) > kEPS) {
         const float cd = (f % 2) ? 1.0f : -1.0f;
-        float a = (cd - o[c0]) / d[c0];
+        float a = fdiv(cd - o[c0], d[c0]);
         if ((a > kEPS) && (__builtin_fabsf(o[c1] + a * d[c1]) <= 1.0f) && (__builtin_fabsf(o[c2] + a * d[c2]) <= 1.0f))
           if (a < al) { al = a; cl = f; }
       }
@@ -516,12 +516,12 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
   } else if (t == CODE_CYLINDER) {
     int cl = -1; float al = kFLTMAX;
     if (__builtin_fabsf(D.z) > kEPS) {
-      float a = (-1.0f - O.z) / D.z;
+      float a = fdiv(-1.0f - O.z, D.z);
       if (a > kEPS) {
         float rx = O.x + a * D.x, ry = O.y + a * D.y;
         if ((__builtin_fmaf(ry, ry, rx * rx) < 1.0f) && (a < al)) { cl = 0; al = a; }
       }
-      a = (1.0f - O.z) / D.z;
+      a = fdiv(1.0f - O.z, D.z);
       if (a > kEPS) {
         float rx = O.x + a * D.x, ry = O.y + a * D.y;
         if ((__builtin_fmaf(ry, ry, rx * rx) < 1.0f) && (a < al)) { cl = 1; al = a; }
@@ -532,7 +532,7 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
     float D2 = __builtin_fmaf(D.y, D.y, D.x * D.x);
     float delta4 = OD * OD - D2 * (O2 - 1.0f);
     if (delta4 > 0.0f) {
-      float a = -(OD + wsqrt<SR::kFastSqrt>(delta4)) / D2;
+      float a = fdiv(-(OD + wsqrt<SR::kFastSqrt>(delta4)), D2);
       if ((a > kEPS) && (a < al)) {
         float z = O.z + a * D.z;
         if (__builtin_fabsf(z) < 1.0f) { cl = 2; al = a; }
@@ -542,7 +542,7 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
   } else if (t == CODE_CONE) {
     int cl = -1; float tl = kFLTMAX;
     if (__builtin_fabsf(D.z) > kEPS) {
-      float t0 = (-1.0f - O.z) / D.z;
+      float t0 = fdiv(-1.0f - O.z, D.z);
       if (t0 > kEPS) {
         float rx = O.x + t0 * D.x, ry = O.y + t0 * D.y;
         if ((__builtin_fmaf(ry, ry, rx * rx) < 1.0f) && (t0 < tl)) { cl = 0; tl = t0; }
@@ -555,9 +555,9 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
     float det = b * b - (4.0f * a) * cc;
     if (det > 0.0f) {
       det = wsqrt<SR::kFastSqrt>(det);
-      float t1 = (-b - det) / (2.0f * a);
+      float t1 = fdiv(-b - det, 2.0f * a);
       if (__builtin_fabsf(O.z + t1 * D.z) > 1.0f) t1 = kFLTMAX;
-      float t2 = (-b + det) / (2.0f * a);
+      float t2 = fdiv(-b + det, 2.0f * a);
       if (__builtin_fabsf(O.z + t2 * D.z) > 1.0f) t2 = kFLTMAX;
       float tt = gmin(t1, t2);
       if (tt < tl) { cl = 2; tl = tt; }

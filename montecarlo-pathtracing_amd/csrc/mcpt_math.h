@@ -19,7 +19,22 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// MCPT_DRIVER_MATH (diagnostic builds only, never shipped: results differ from the oracle):
+// the arithmetic a GL driver's shader compiler emits for the pieces GLSL leaves
+// implementation-defined, so that the deviation of an *executed* GLSL render from the shipped
+// contract can be measured at equal RNG seeds (tests/test_gpu_driver_math.py).
+// Bits: 1 = raw v_sqrt_f32 / v_rcp_f32 / v_rsq_f32 for sqrt, 1/x, inversesqrt (normalize,
+// length); 2 = hardware v_sin_f32 / v_cos_f32 / v_log_f32 / v_exp_f32 for sin, cos, log, exp2
+// and pow = exp2(y log2 x); 4 = a / b as a * v_rcp_f32(b) in the primitive tests.
+#ifndef MCPT_DRIVER_MATH
+#define MCPT_DRIVER_MATH 0
+#endif
+
 namespace mcpt {
+
+constexpr bool kDriverRoots = (MCPT_DRIVER_MATH & 1) != 0;
+constexpr bool kDriverTrans = (MCPT_DRIVER_MATH & 2) != 0;
+constexpr bool kDriverDiv = (MCPT_DRIVER_MATH & 4) != 0;
 
 struct f3 { float x, y, z; };
 __device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
@@ -43,6 +58,7 @@ __device__ __attribute__((noinline)) inline float rcp_ieee(float x) { return 1.0
 // The *_rn wrappers route the other inputs to the generic expansions, wave-uniformly.
 __device__ __forceinline__ float sqrt_core(float x) {
   const float s = __builtin_amdgcn_sqrtf(x);
+  if constexpr (kDriverRoots) return s;
   const float sd = __uint_as_float(__float_as_uint(s) - 1u), su = __uint_as_float(__float_as_uint(s) + 1u);
   float r = s;
   if (__builtin_fmaf(-sd, s, x) <= 0.0f) r = sd;
@@ -51,6 +67,7 @@ __device__ __forceinline__ float sqrt_core(float x) {
 }
 __device__ __forceinline__ float rcp_core(float x) {
   const float y = __builtin_amdgcn_rcpf(x);
+  if constexpr (kDriverRoots) return y;
   return __builtin_fmaf(__builtin_fmaf(-x, y, 1.0f), y, y);
 }
 __device__ __forceinline__ bool sqrt_core_ok(float x) { return !(__builtin_fabsf(x) < 0x1p-96f) || x == 0.0f; }
@@ -59,6 +76,7 @@ __device__ __forceinline__ bool rcp_core_ok(float x) {
   return ax >= 0x1p-126f && ax < 0x1p126f;
 }
 __device__ __forceinline__ float sqrt_rn(float x) {
+  if constexpr (kDriverRoots) return __builtin_amdgcn_sqrtf(x);
   float r = sqrt_core(x);
   const bool ok = sqrt_core_ok(x);
   if (__builtin_expect(__ballot(!ok) != 0, 0)) {
@@ -67,6 +85,7 @@ __device__ __forceinline__ float sqrt_rn(float x) {
   return r;
 }
 __device__ __forceinline__ float rcp_rn(float x) {
+  if constexpr (kDriverRoots) return __builtin_amdgcn_rcpf(x);
   float r = rcp_core(x);
   const bool ok = rcp_core_ok(x);
   if (__builtin_expect(__ballot(!ok) != 0, 0)) {
@@ -77,6 +96,7 @@ __device__ __forceinline__ float rcp_rn(float x) {
 // RN(1/RN(sqrt(x))), the factor of normalize: for 2^-96 <= x < 2^126 both cores are exact
 // (the root lies in [2^-48, 2^63)): one range test for the pair
 __device__ __forceinline__ float rsqrt_rn(float x) {
+  if constexpr (kDriverRoots) return __builtin_amdgcn_rsqf(x);
   float r = rcp_core(sqrt_core(x));
   const bool ok = x >= 0x1p-96f && x < 0x1p126f;
   if (__builtin_expect(__ballot(!ok) != 0, 0)) {
@@ -90,8 +110,20 @@ __device__ __forceinline__ f3 normalize3(f3 a) { return muls(a, rsqrt_rn(dot3(a,
 __device__ __forceinline__ float length3(f3 a) { return sqrt_rn(dot3(a, a)); }
 // the same with the generic expansions inline (for code inside the BVH walk loop, where the
 // short sequences' fallback branches cost more registers than they save instructions)
-__device__ __forceinline__ f3 normalize3_g(f3 a) { float r = 1.0f / __builtin_sqrtf(dot3(a, a)); return muls(a, r); }
-__device__ __forceinline__ float length3_g(f3 a) { return __builtin_sqrtf(dot3(a, a)); }
+__device__ __forceinline__ f3 normalize3_g(f3 a) {
+  if constexpr (kDriverRoots) return muls(a, __builtin_amdgcn_rsqf(dot3(a, a)));
+  float r = 1.0f / __builtin_sqrtf(dot3(a, a));
+  return muls(a, r);
+}
+__device__ __forceinline__ float length3_g(f3 a) {
+  if constexpr (kDriverRoots) return __builtin_amdgcn_sqrtf(dot3(a, a));
+  return __builtin_sqrtf(dot3(a, a));
+}
+// the primitive tests' divisions (correctly rounded; MCPT_DRIVER_MATH & 4: a * rcp(b))
+__device__ __forceinline__ float fdiv(float a, float b) {
+  if constexpr (kDriverDiv) return a * __builtin_amdgcn_rcpf(b);
+  return a / b;
+}
 __device__ __forceinline__ f3 cross3(f3 a, f3 b) {
   return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
@@ -132,6 +164,12 @@ constexpr float kFLTMAX = 3.402823e38f;       // FLT_MAX raytracer_func.frag:8
 
 // sin/cos: Cody-Waite reduction by pi/2, minimax polynomials on [-pi/4, pi/4]
 __device__ __forceinline__ void mc_sincos(float x, float& s_out, float& c_out) {
+  if constexpr (kDriverTrans) {   // v_sin / v_cos take revolutions
+    const float rev = x * 0.159154943091895336f;
+    s_out = __builtin_amdgcn_sinf(rev);
+    c_out = __builtin_amdgcn_cosf(rev);
+    return;
+  }
   float t = x * 0.636619746685028076f;
   float qf = __builtin_floorf(t + 0.5f);
   int q = (int)qf;
@@ -176,6 +214,7 @@ __device__ __forceinline__ float mc_log_core(uint32_t b, int e) {
 }
 // natural log (x > 0 finite expected; 0 -> -inf, <0/NaN -> NaN)
 __device__ __forceinline__ float mc_log(float x) {
+  if constexpr (kDriverTrans) return __builtin_amdgcn_logf(x) * 0.693147182464599609f;
   if (!(x > 0.0f)) return (x == 0.0f) ? -__builtin_inff() : __builtin_nanf("");
   if (x == __builtin_inff()) return x;
   uint32_t b = fbits(x);
@@ -187,9 +226,13 @@ __device__ __forceinline__ float mc_log(float x) {
 // multiple of 2^-23 in [0, 1 - 2^-23], so 1 - u is exact, normal and positive): mc_log with
 // its zero / negative / inf / subnormal cases dropped, none of which that domain reaches —
 // same bits
-__device__ __forceinline__ float mc_log_unit(float x) { return mc_log_core(fbits(x), 0); }
+__device__ __forceinline__ float mc_log_unit(float x) {
+  if constexpr (kDriverTrans) return __builtin_amdgcn_logf(x) * 0.693147182464599609f;
+  return mc_log_core(fbits(x), 0);
+}
 
 __device__ __forceinline__ float mc_exp2(float x) {
+  if constexpr (kDriverTrans) return __builtin_amdgcn_exp2f(x);
   if (x != x) return x;
   if (x >= 128.0f) return __builtin_inff();
   if (x < -150.0f) return 0.0f;
@@ -210,6 +253,7 @@ __device__ __forceinline__ float mc_exp2(float x) {
 // pow for x in [0, 1 + a few ulp] (the specular term: max(0, dot) of unit vectors, NaN -> 0):
 // mc_log's inf test is unreachable there; same bits as mc_pow
 __device__ __forceinline__ float mc_pow_le1(float x, float y) {
+  if constexpr (kDriverTrans) return __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
   float l;
   if (!(x > 0.0f)) l = (x == 0.0f) ? -__builtin_inff() : __builtin_nanf("");
   else {
@@ -221,6 +265,7 @@ __device__ __forceinline__ float mc_pow_le1(float x, float y) {
   return mc_exp2(y * (l * 1.44269502162933350f));
 }
 __device__ __forceinline__ float mc_pow(float x, float y) {
+  if constexpr (kDriverTrans) return __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
   return mc_exp2(y * (mc_log(x) * 1.44269502162933350f));
 }
 
