@@ -186,7 +186,7 @@ enum {
   LS_NODE_IT, LS_NODE_LN, LS_NE_WV, LS_NE_LN, LS_OUT_WV, LS_OUT_LN, LS_VAL_WV, LS_VAL_LN,
   LS_LEAF_IT, LS_LEAF_LN, LS_PRIM_LN, LS_SPH_WV, LS_SPH_LN, LS_CUBE_WV, LS_CUBE_LN, LS_CYL_WV,
   LS_CYL_LN, LS_QUAD_WV, LS_QUAD_LN, LS_WALK_IT, LS_WALK_LN, LS_WALK_CALLS, LS_ROUNDS, LS_ROUND_LN,
-  LS_SHADE_WV, LS_SHADE_LN, LS_RR2_WV, LS_RR2_LN, LS_WAVES, LS_COUNT
+  LS_SHADE_WV, LS_SHADE_LN, LS_RR2_WV, LS_RR2_LN, LS_WAVES, LS_FIT_IT, LS_TWO_IT, LS_COUNT
 };
 __device__ __forceinline__ unsigned* ls_row() {
   __shared__ unsigned s_ls[16][LS_COUNT];
@@ -262,6 +262,43 @@ __device__ __forceinline__ bool box_test(float4 a0, float4 a1, float4 a2, f3 O, 
   return false;
 }
 
+// box_test without branches (MCPT_BOX_SELECT): the same operations for every lane, the outcome
+// chosen by selects.  Returns the key the cull compares: -1 when the origin is inside the box
+// (always pushed), the squared distance to the entry point when a face is valid, +inf when
+// none is; (double)key < cull2 is box_test's result bit for bit (same operations on the lanes
+// box_test runs them on; cull2 > 0).  No exec-mask branches: the deep walk's node block keeps
+// every lane in one instruction stream (SALU / branch bookkeeping, verdict r03).
+__device__ __forceinline__ float box_key(float4 a0, float4 a1, float4 a2, f3 O, f3 D, f3 invD) {
+  f3 c = mk(a0.x, a0.y, a0.z), w = mk(a1.x, a1.y, a1.z), iw = mk(a2.x, a2.y, a2.z);
+  f3 Oi = mulv(sub(O, c), iw);
+  f3 Di = mulv(D, iw);
+  const bool inside = (__builtin_fabsf(Oi.x) < 1.0f) & (__builtin_fabsf(Oi.y) < 1.0f) & (__builtin_fabsf(Oi.z) < 1.0f);
+  f3 rD = mulv(invD, w);
+  const bool dx = __builtin_fabsf(Di.x) > kEPS, dy = __builtin_fabsf(Di.y) > kEPS, dz = __builtin_fabsf(Di.z) > kEPS;
+  float al = kFLTMAX;
+#define MCPT_FACE(CD, OA, DV, RA, OB, DB, OC, DC)                                              \
+  {                                                                                            \
+    const float a = ((CD) - (OA)) * (RA);                                                      \
+    const bool ok = (DV) & (a > kEPS) & (__builtin_fabsf(OB + a * DB) <= 1.0f) &               \
+                    (__builtin_fabsf(OC + a * DC) <= 1.0f);                                    \
+    al = __builtin_fminf(al, ok ? a : kFLTMAX);                                                \
+  }
+  MCPT_FACE(-1.0f, Oi.x, dx, rD.x, Oi.y, Di.y, Oi.z, Di.z)
+  MCPT_FACE(1.0f, Oi.x, dx, rD.x, Oi.y, Di.y, Oi.z, Di.z)
+  MCPT_FACE(-1.0f, Oi.y, dy, rD.y, Oi.z, Di.z, Oi.x, Di.x)
+  MCPT_FACE(1.0f, Oi.y, dy, rD.y, Oi.z, Di.z, Oi.x, Di.x)
+  MCPT_FACE(-1.0f, Oi.z, dz, rD.z, Oi.x, Di.x, Oi.y, Di.y)
+  MCPT_FACE(1.0f, Oi.z, dz, rD.z, Oi.x, Di.x, Oi.y, Di.y)
+#undef MCPT_FACE
+  f3 Pg = add(mulv(add(muls(Di, al), Oi), w), c);
+  f3 v = sub(O, Pg);
+  const float d2 = dot3(v, v);
+  return inside ? -1.0f : (al < kFLTMAX ? d2 : __builtin_inff());
+}
+#ifndef MCPT_BOX_SELECT
+#define MCPT_BOX_SELECT 0
+#endif
+
 // A node visit's two child records (rows: centre + has-prim flag, half-width, 1/half-width)
 // and their box tests: (hl, hr) = the reference's push decisions for the left and right child.
 // A child whose subtree holds no primitive (flag 0) cannot change the hit and is never tested
@@ -303,8 +340,14 @@ __device__ __forceinline__ void node_tests(const SR& s, const float4* __restrict
                  "v"(l2.y), "v"(l2.z));
     MCPT_ROWS_IN("v"(r0.x), "v"(r0.y), "v"(r0.z), "v"(r0.w), "v"(r1.x), "v"(r1.y), "v"(r1.z), "v"(r2.x),
                  "v"(r2.y), "v"(r2.z));
-    hl = (COUNT || l0.w != 0.0f) && box_test<false>(l0, l1, l2, O, D, invD, cull2);
-    hr = (COUNT || r0.w != 0.0f) && box_test<false>(r0, r1, r2, O, D, invD, cull2);
+    if constexpr (MCPT_BOX_SELECT && !COUNT) {
+      const float kl = box_key(l0, l1, l2, O, D, invD), kr = box_key(r0, r1, r2, O, D, invD);
+      hl = (l0.w != 0.0f) & ((double)kl < cull2);
+      hr = (r0.w != 0.0f) & ((double)kr < cull2);
+    } else {
+      hl = (COUNT || l0.w != 0.0f) && box_test<false>(l0, l1, l2, O, D, invD, cull2);
+      hr = (COUNT || r0.w != 0.0f) && box_test<false>(r0, r1, r2, O, D, invD, cull2);
+    }
 #ifdef MCPT_LANESTATS
     const int sl = box_stage(l0, l1, l2, O, D, invD), sr = box_stage(r0, r1, r2, O, D, invD);
     ls_cond(LS_NE_WV, LS_NE_LN, sl >= 1); ls_cond(LS_NE_WV, LS_NE_LN, sr >= 1);
@@ -681,6 +724,17 @@ __device__ __forceinline__ bool walk_run(const SR& s, f3 O, f3 D, Hit& h, Walk& 
 #ifdef MCPT_LANESTATS
     ls_add(LS_WALK_IT, 1u);
     ls_add(LS_WALK_LN, ls_pop(true));
+    if (__ballot(do_node)) {   // face jobs of this node iteration (both children's face stages)
+      int jobs = 0;
+      if (do_node) {
+        const float4* q = node_rows(s.nodes, 2 * (size_t)w.node + 1);
+        jobs = (box_stage(q[0], q[1], q[2], O, D, w.invD) >= 2) + (box_stage(q[3], q[4], q[5], O, D, w.invD) >= 2);
+      }
+      unsigned tot = 0;
+      for (int k = 1; k <= 2; ++k) tot += (unsigned)k * ls_pop(jobs == k);
+      ls_add(LS_FIT_IT, tot <= ls_pop(true) ? 1u : 0u);   // one round of the walking lanes would do
+      ls_add(LS_TWO_IT, ls_pop(jobs == 2) ? 1u : 0u);     // some lane needs both children's faces
+    }
     {
       const unsigned nn = ls_pop(do_node), nl = ls_pop(do_leaf);
       ls_add(LS_NODE_IT, nn ? 1u : 0u); ls_add(LS_NODE_LN, nn);

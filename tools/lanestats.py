@@ -20,7 +20,7 @@ import mcpt  # noqa: E402
 NAMES = ["node_it", "node_ln", "ne_wv", "ne_ln", "out_wv", "out_ln", "val_wv", "val_ln",
          "leaf_it", "leaf_ln", "prim_ln", "sph_wv", "sph_ln", "cube_wv", "cube_ln", "cyl_wv",
          "cyl_ln", "quad_wv", "quad_ln", "walk_it", "walk_ln", "walk_calls", "rounds", "round_ln",
-         "shade_wv", "shade_ln", "rr2_wv", "rr2_ln", "waves"]
+         "shade_wv", "shade_ln", "rr2_wv", "rr2_ln", "waves", "fit_it", "two_it"]
 
 
 def util(ln, wv):
@@ -52,6 +52,9 @@ def run(sid, B, spp, seg, leaf_batch, walk_exit, W=1920, H=1080):
                     "sphere": util(d["sph_ln"], d["sph_wv"]), "cube": util(d["cube_ln"], d["cube_wv"]),
                     "cylinder": util(d["cyl_ln"], d["cyl_wv"]), "quad": util(d["quad_ln"], d["quad_wv"]),
                     "shade": util(d["shade_ln"], d["shade_wv"]), "reflect_rr": util(d["rr2_ln"], d["rr2_wv"])},
+           "node_it_share": {"face_jobs_fit_one_round": round(d["fit_it"] / max(d["node_it"], 1), 3),
+                             "some_lane_two_face_jobs": round(d["two_it"] / max(d["node_it"], 1), 3),
+                             "face_jobs_per_walking_lane": round(d["out_ln"] / max(d["walk_ln"] * d["node_it"] / max(d["walk_it"], 1), 1), 3)},
            "child_tests_per_node_it": {"nonempty_wv": round(d["ne_wv"] / max(d["node_it"], 1), 3),
                                        "face_wv": round(d["out_wv"] / max(d["node_it"], 1), 3),
                                        "cull_wv": round(d["val_wv"] / max(d["node_it"], 1), 3)},
