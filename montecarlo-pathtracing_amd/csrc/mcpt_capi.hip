@@ -856,6 +856,7 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   p.wave_traversal = (mode == MCPT_TRAVERSAL_WAVE) ? 1 : 0;
   p.walk_exit = resolve_walk_exit(c);
   p.leaf_batch = resolve_leaf_batch(c);
+  p.walk_min_done = std::max(1, env_int("MCPT_WALK_MIN_DONE", 1));   // tuning hook (same bits for any value)
   if (cand_deep_knobs(cand)) {   // the deep candidates' knobs, unless set explicitly
     if (c->walk_exit < 0) p.walk_exit = kDeepWalkExit;
     if (c->leaf_batch < 0) p.leaf_batch = kDeepLeafBatch;

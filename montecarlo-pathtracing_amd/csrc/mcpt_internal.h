@@ -81,6 +81,7 @@ struct RenderParams {
   int wave_traversal;           // 1: wave-coherent BVH walk (traverse_wave), 0: per lane
   int walk_exit;                // per-lane walks: leave the loop at <= this many walking lanes
   int leaf_batch;               // deep-BVH walk: run the leaf block once >= this many lanes wait
+  int walk_min_done;            // per-lane walks: ... and once >= this many lanes finished in the call (>= 1)
   int first_pass, n_passes, bounces, variant;
   float date, ior;
   // wave-uniform constants computed on the host (same binary32/binary64 operations as the

@@ -298,6 +298,68 @@ __device__ __forceinline__ float box_key(float4 a0, float4 a1, float4 a2, f3 O, 
 #ifndef MCPT_BOX_SELECT
 #define MCPT_BOX_SELECT 0
 #endif
+#ifndef MCPT_FACE_PAIR
+#define MCPT_FACE_PAIR 0
+#endif
+
+// The face loop of intersect_bv (raytracer_func.frag:330-343) on a box-local ray: the smallest
+// valid face parameter, kFLTMAX when no face is valid (box_test's operations).
+__device__ __forceinline__ float face_min(f3 Oi, f3 Di, f3 rD) {
+  const bool dx = __builtin_fabsf(Di.x) > kEPS, dy = __builtin_fabsf(Di.y) > kEPS, dz = __builtin_fabsf(Di.z) > kEPS;
+  float al = kFLTMAX;
+#define MCPT_FACE(CD, OA, DV, RA, OB, DB, OC, DC)                                              \
+  {                                                                                            \
+    const float a = ((CD) - (OA)) * (RA);                                                      \
+    const bool ok = (DV) & (a > kEPS) & (__builtin_fabsf(OB + a * DB) <= 1.0f) &               \
+                    (__builtin_fabsf(OC + a * DC) <= 1.0f);                                    \
+    al = __builtin_fminf(al, ok ? a : kFLTMAX);                                                \
+  }
+  MCPT_FACE(-1.0f, Oi.x, dx, rD.x, Oi.y, Di.y, Oi.z, Di.z)
+  MCPT_FACE(1.0f, Oi.x, dx, rD.x, Oi.y, Di.y, Oi.z, Di.z)
+  MCPT_FACE(-1.0f, Oi.y, dy, rD.y, Oi.z, Di.z, Oi.x, Di.x)
+  MCPT_FACE(1.0f, Oi.y, dy, rD.y, Oi.z, Di.z, Oi.x, Di.x)
+  MCPT_FACE(-1.0f, Oi.z, dz, rD.z, Oi.x, Di.x, Oi.y, Di.y)
+  MCPT_FACE(1.0f, Oi.z, dz, rD.z, Oi.x, Di.x, Oi.y, Di.y)
+#undef MCPT_FACE
+  return al;
+}
+__device__ __forceinline__ f3 sel3(bool c, f3 a, f3 b) { return mk(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z); }
+
+// MCPT_FACE_PAIR: a node visit's two box tests with their face loops paired up per lane.  A lane
+// needs the face loop for a child that holds a primitive and whose box does not contain the ray
+// origin; the wave ran the left child's loop for the lanes that need it and then the right
+// child's, whenever any lane needed either.  Here every lane runs its first needed loop (left,
+// else right) in one pass, and a second pass runs only when some lane needs both.  Each child's
+// decision uses box_test's operations on the same values (same bits).
+__device__ __forceinline__ void node_tests_paired(float4 l0, float4 l1, float4 l2, float4 r0, float4 r1, float4 r2,
+                                                  f3 O, f3 D, f3 invD, double cull2, bool& hl, bool& hr) {
+  const f3 cl = mk(l0.x, l0.y, l0.z), wl = mk(l1.x, l1.y, l1.z), iwl = mk(l2.x, l2.y, l2.z);
+  const f3 cr = mk(r0.x, r0.y, r0.z), wr = mk(r1.x, r1.y, r1.z), iwr = mk(r2.x, r2.y, r2.z);
+  const f3 Oil = mulv(sub(O, cl), iwl), Dil = mulv(D, iwl);
+  const f3 Oir = mulv(sub(O, cr), iwr), Dir = mulv(D, iwr);
+  const bool in_l = (__builtin_fabsf(Oil.x) < 1.0f) & (__builtin_fabsf(Oil.y) < 1.0f) & (__builtin_fabsf(Oil.z) < 1.0f);
+  const bool in_r = (__builtin_fabsf(Oir.x) < 1.0f) & (__builtin_fabsf(Oir.y) < 1.0f) & (__builtin_fabsf(Oir.z) < 1.0f);
+  const bool ne_l = l0.w != 0.0f, ne_r = r0.w != 0.0f;
+  const bool need_l = ne_l & !in_l, need_r = ne_r & !in_r;
+  float al_l = kFLTMAX, al_r = kFLTMAX;
+  if (__ballot(need_l | need_r)) {
+    const f3 rDl = mulv(invD, wl), rDr = mulv(invD, wr);
+    const float a1 = face_min(sel3(need_l, Oil, Oir), sel3(need_l, Dil, Dir), sel3(need_l, rDl, rDr));
+    al_l = need_l ? a1 : kFLTMAX;
+    al_r = (!need_l & need_r) ? a1 : kFLTMAX;
+    if (__ballot(need_l & need_r)) {
+      const float a2 = face_min(Oir, Dir, rDr);
+      if (need_l & need_r) al_r = a2;
+    }
+  }
+  auto cull = [&](float al, f3 Oi, f3 Di, f3 w, f3 c) {
+    f3 Pg = add(mulv(add(muls(Di, al), Oi), w), c);
+    f3 v = sub(O, Pg);
+    return (al < kFLTMAX) & ((double)dot3(v, v) < cull2);
+  };
+  hl = ne_l & (in_l | cull(al_l, Oil, Dil, wl, cl));
+  hr = ne_r & (in_r | cull(al_r, Oir, Dir, wr, cr));
+}
 
 // A node visit's two child records (rows: centre + has-prim flag, half-width, 1/half-width)
 // and their box tests: (hl, hr) = the reference's push decisions for the left and right child.
@@ -340,7 +402,9 @@ __device__ __forceinline__ void node_tests(const SR& s, const float4* __restrict
                  "v"(l2.y), "v"(l2.z));
     MCPT_ROWS_IN("v"(r0.x), "v"(r0.y), "v"(r0.z), "v"(r0.w), "v"(r1.x), "v"(r1.y), "v"(r1.z), "v"(r2.x),
                  "v"(r2.y), "v"(r2.z));
-    if constexpr (MCPT_BOX_SELECT && !COUNT) {
+    if constexpr (MCPT_FACE_PAIR && !COUNT) {
+      node_tests_paired(l0, l1, l2, r0, r1, r2, O, D, invD, cull2, hl, hr);
+    } else if constexpr (MCPT_BOX_SELECT && !COUNT) {
       const float kl = box_key(l0, l1, l2, O, D, invD), kr = box_key(r0, r1, r2, O, D, invD);
       hl = (l0.w != 0.0f) & ((double)kl < cull2);
       hr = (r0.w != 0.0f) & ((double)kr < cull2);
@@ -499,6 +563,9 @@ __device__ __forceinline__ void mesh_test(const SR& s, int mesh, int index, f3 O
   }
 }
 
+#ifndef MCPT_ONE_ACCEPT
+#define MCPT_ONE_ACCEPT 0
+#endif
 // intersect_prim raytracer_func.frag:681-705 + Sphere/Cube/Cylinder/Cone/OrientedQuad :398-640
 template <bool COUNT, bool UNI, bool ANY = false, class SR>
 __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit& h, Ev<COUNT>& ev) {
@@ -521,7 +588,22 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
   } else {
     r0 = ld4<U>(s.prims, b); r1 = ld4<U>(s.prims, b + 1); r2 = ld4<U>(s.prims, b + 2);
   }
-  auto accept = [&](int shape, int dir, f3 Pl) { accept_cand<COUNT, UNI>(s, i, shape, dir, Pl, Ow, h, ev); };
+  // MCPT_ONE_ACCEPT: the type branches only record their candidate (the sphere's near and far
+  // roots: two) and one accept site after the switch tests it against the hit record, so a leaf
+  // block whose lanes hold several primitive types runs the candidate code (transform rows,
+  // world point, length, compare, record update) once instead of once per type.  Each lane's
+  // candidates reach the hit record in the same order (same bits).
+  bool has1 = false, has2 = false;
+  int shape1 = 0, dir1 = 0;
+  f3 P1 = mk(0.0f, 0.0f, 0.0f), P2 = P1;
+  auto accept = [&](int shape, int dir, f3 Pl) {
+    if constexpr (MCPT_ONE_ACCEPT) { has1 = true; shape1 = shape; dir1 = dir; P1 = Pl; }
+    else accept_cand<COUNT, UNI>(s, i, shape, dir, Pl, Ow, h, ev);
+  };
+  auto accept_far = [&](f3 Pl) {   // the sphere's far root, after its near root
+    if constexpr (MCPT_ONE_ACCEPT) { has2 = true; P2 = Pl; }
+    else accept_cand<COUNT, UNI>(s, i, CODE_SPHERE, 0, Pl, Ow, h, ev);
+  };
   if (pt < 0) return;
   const int t = pt & 15;
   f3 O = xpoint(r0, r1, r2, Ow);
@@ -534,14 +616,14 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
       float a = fdiv(-(OD + sq), D2);
       if (a > kEPS) accept(CODE_SPHERE, 0, add(O, muls(D, a)));
       a = fdiv(-(OD - sq), D2);
-      if (a > kEPS) accept(CODE_SPHERE, 0, add(O, muls(D, a)));
+      if (a > kEPS) accept_far(add(O, muls(D, a)));
     }
   } else if (t == CODE_QUAD) {
-    if (D.z > -kEPS) return;
-    float a = fdiv(-O.z, D.z);
-    f3 Pl = add(O, muls(D, a));
-    if (__builtin_fabsf(Pl.x) > 1.0f || __builtin_fabsf(Pl.y) > 1.0f) return;
-    accept(CODE_QUAD, 0, Pl);
+    if (!(D.z > -kEPS)) {
+      float a = fdiv(-O.z, D.z);
+      f3 Pl = add(O, muls(D, a));
+      if (!(__builtin_fabsf(Pl.x) > 1.0f || __builtin_fabsf(Pl.y) > 1.0f)) accept(CODE_QUAD, 0, Pl);
+    }
   } else if (t == CODE_CUBE) {
     float al = kFLTMAX; int cl = 0;
     float o[3] = {O.x, O.y, O.z}, d[3] = {D.x, D.y, D.z};
@@ -608,6 +690,10 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
     if (tl < kFLTMAX) accept(CODE_CONE, cl, add(O, muls(D, tl)));
   } else if (t == CODE_MESH) {
     if constexpr (SR::kMesh) mesh_test<COUNT, ANY>(s, pt >> 4, i, O, D, Ow, h, ev);
+  }
+  if constexpr (MCPT_ONE_ACCEPT) {
+    if (has1) accept_cand<COUNT, UNI>(s, i, shape1, dir1, P1, Ow, h, ev);
+    if (has2) accept_cand<COUNT, UNI>(s, i, CODE_SPHERE, 0, P2, Ow, h, ev);
   }
 }
 
@@ -702,7 +788,7 @@ __device__ __forceinline__ void walk_begin(const SR& s, f3 D, Hit& h, Walk& w, E
 // visit sequence is unchanged (the cull reads its own hit record only).
 template <bool COUNT, bool SUSPEND, class SR>
 __device__ __forceinline__ bool walk_run(const SR& s, f3 O, f3 D, Hit& h, Walk& w, Ev<COUNT>& ev, int exit,
-                                         int leaf_batch) {
+                                         int leaf_batch, int min_done = 1) {
   const int leaf0 = (1 << s.depth) - 1;
   const int n0 = SUSPEND ? __builtin_popcountll(__ballot(1)) : 0;
 #ifdef MCPT_LANESTATS
@@ -787,7 +873,7 @@ __device__ __forceinline__ bool walk_run(const SR& s, f3 O, f3 D, Hit& h, Walk& 
     }
     if (SUSPEND) {   // wave-uniform
       const int n = __builtin_popcountll(__ballot(1));
-      if (n <= exit && n < n0) return false;
+      if (n <= exit && n0 - n >= min_done) return false;
     }
   }
 }
@@ -1284,7 +1370,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
       } else {
         if (!walking) { walk_begin<COUNT>(s, D, h, walk, ev, p.cull2_max); walking = true; }
         if constexpr (MESH) walking = !walk_run_mesh<COUNT, SUSPEND>(s, O, D, h, walk, ev, p.walk_exit);
-        else walking = !walk_run<COUNT, SUSPEND>(s, O, D, h, walk, ev, p.walk_exit, p.leaf_batch);
+        else walking = !walk_run<COUNT, SUSPEND>(s, O, D, h, walk, ev, p.walk_exit, p.leaf_batch, p.walk_min_done);
         ready = !walking;
       }
     }
