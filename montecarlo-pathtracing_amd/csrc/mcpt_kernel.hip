@@ -161,6 +161,14 @@ __device__ __forceinline__ int ld1(const int* p, size_t i) {
   return p[i];
 }
 
+__device__ __forceinline__ int mbcnt64(uint64_t m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ uint32_t bperm(int lane, uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute(lane << 2, (int)v);
+}
+__device__ __forceinline__ float bpermf(int lane, float v) { return __uint_as_float(bperm(lane, __float_as_uint(v))); }
+
 struct Counters {
   uint32_t v[EV_COUNT];
   __device__ __forceinline__ void inc(int e) { v[e]++; }
@@ -300,6 +308,9 @@ __device__ __forceinline__ float box_key(float4 a0, float4 a1, float4 a2, f3 O, 
 #endif
 #ifndef MCPT_FACE_PAIR
 #define MCPT_FACE_PAIR 0
+#endif
+#ifndef MCPT_FACE_JOBS
+#define MCPT_FACE_JOBS 0
 #endif
 
 // The face loop of intersect_bv (raytracer_func.frag:330-343) on a box-local ray: the smallest
@@ -879,6 +890,121 @@ __device__ __forceinline__ bool walk_run(const SR& s, f3 O, f3 D, Hit& h, Walk& 
 }
 
 
+// MCPT_FACE_JOBS: walk_run for the deep kernel with the box tests' face loops compacted across
+// the wave (north star: ray compaction through wavefront primitives).  In a node iteration a
+// lane needs the face loop of a child that holds a primitive and whose box does not contain the
+// ray origin (lane accounting, scene 8: 28.7 lanes per face block, 1.97 face blocks per node
+// iteration).  Here those (lane, child) face jobs are numbered by ballot + mbcnt and run by
+// ALL lanes of the call -- the lanes waiting on a leaf and the lanes whose walk has ended stay in
+// the loop as workers -- in ceil(jobs / lanes) passes instead of one pass per child.  A worker
+// pulls its job owner's ray (O, D, 1/D), node pair and cull bound with ds_bpermute, loads the
+// child's rows itself, runs intersect_bv's face loop and cull, and the owner pulls the push
+// decision back.  Every decision is box_test's, on the same values, at the same point of the
+// owner's walk (same bits).  LDS: rank -> lane and job -> owner tables, 192 B per wave.
+__device__ __forceinline__ unsigned char* jobs_lds() {
+  __shared__ unsigned char s_jobs[kTileThreads / 64][192];
+  return s_jobs[threadIdx.x >> 6];
+}
+template <class SR>
+__device__ __forceinline__ bool walk_run_jobs(const SR& s, f3 O, f3 D, Hit& h, Walk& w, int exit, int leaf_batch,
+                                              int min_done) {
+  Ev<false> ev;
+  const int leaf0 = (1 << s.depth) - 1;
+  const int lane = (int)__lane_id();
+  const uint64_t A = __ballot(1);
+  const int n0 = __builtin_popcountll(A), rank = mbcnt64(A);
+  unsigned char* wl = jobs_lds();        // [0, 64): rank -> lane
+  unsigned char* own = jobs_lds() + 64;  // [64, 192): job -> owner lane
+  wl[rank] = (unsigned char)lane;
+  __builtin_amdgcn_wave_barrier();
+  bool alive = true;
+  for (;;) {
+    const bool is_leaf = alive && w.node >= leaf0;
+    const uint64_t on_leaf = __ballot(is_leaf), walking = __ballot(alive);
+    const bool leaves = __builtin_popcountll(on_leaf) >= leaf_batch || on_leaf == walking;   // wave-uniform
+    bool pop = false;
+    if (leaves) {
+      if (is_leaf) {
+        const int p = s.leaves[(uint32_t)(w.node - leaf0)];
+        if (p >= 0) prim_test<false, false, false>(s, p, O, D, h, ev);
+        pop = true;
+      }
+    } else {
+      const bool do_node = alive && !is_leaf;
+      const uint32_t jn = 2u * (uint32_t)(do_node ? w.node : 0) + 1u;
+      const float4* q = node_rows(s.nodes, jn);
+      const float4 l0 = q[0], l1 = q[2], r0 = q[3], r1 = q[5];   // centre + flag, 1/half-width
+      MCPT_ROWS_IN("v"(l0.x), "v"(l0.y), "v"(l0.z), "v"(l0.w), "v"(l1.x), "v"(l1.y), "v"(l1.z), "v"(r0.x),
+                   "v"(r0.y), "v"(r0.z), "v"(r0.w), "v"(r1.x), "v"(r1.y), "v"(r1.z));
+      const f3 Oil = mulv(sub(O, mk(l0.x, l0.y, l0.z)), mk(l1.x, l1.y, l1.z));
+      const f3 Oir = mulv(sub(O, mk(r0.x, r0.y, r0.z)), mk(r1.x, r1.y, r1.z));
+      const bool in_l = (__builtin_fabsf(Oil.x) < 1.0f) & (__builtin_fabsf(Oil.y) < 1.0f) & (__builtin_fabsf(Oil.z) < 1.0f);
+      const bool in_r = (__builtin_fabsf(Oir.x) < 1.0f) & (__builtin_fabsf(Oir.y) < 1.0f) & (__builtin_fabsf(Oir.z) < 1.0f);
+      const bool ne_l = l0.w != 0.0f, ne_r = r0.w != 0.0f;
+      const bool need_l = do_node & ne_l & !in_l, need_r = do_node & ne_r & !in_r;
+      const uint64_t mL = __ballot(need_l), mR = __ballot(need_r);
+      const int nL = __builtin_popcountll(mL), nJ = nL + __builtin_popcountll(mR);
+      const int sL = mbcnt64(mL), sR = nL + mbcnt64(mR);
+      if (need_l) own[sL] = (unsigned char)lane;
+      if (need_r) own[sR] = (unsigned char)lane;
+      __builtin_amdgcn_wave_barrier();
+      bool pass_l = false, pass_r = false;
+      for (int base = 0; base < nJ; base += n0) {   // wave-uniform
+        const int jj = base + rank;
+        const bool has = jj < nJ;
+        const int o = has ? (int)own[jj] : lane;
+        const bool right = jj >= nL;
+        const f3 Oo = mk(bpermf(o, O.x), bpermf(o, O.y), bpermf(o, O.z));
+        const f3 Do = mk(bpermf(o, D.x), bpermf(o, D.y), bpermf(o, D.z));
+        const f3 iDo = mk(bpermf(o, w.invD.x), bpermf(o, w.invD.y), bpermf(o, w.invD.z));
+        const uint32_t jo = bperm(o, jn) + (right ? 1u : 0u);   // the child's row triple
+        const uint64_t cb = __double_as_longlong(h.cull2);
+        const double c2o = __longlong_as_double((long long)(((uint64_t)bperm(o, (uint32_t)(cb >> 32)) << 32) |
+                                                            (uint64_t)bperm(o, (uint32_t)cb)));
+        const float4* qc = node_rows(s.nodes, jo);
+        const float4 a0 = qc[0], a1 = qc[1], a2 = qc[2];
+        MCPT_ROWS_IN("v"(a0.x), "v"(a0.y), "v"(a0.z), "v"(a1.x), "v"(a1.y), "v"(a1.z), "v"(a2.x), "v"(a2.y),
+                     "v"(a2.z));
+        const f3 c = mk(a0.x, a0.y, a0.z), wd = mk(a1.x, a1.y, a1.z), iw = mk(a2.x, a2.y, a2.z);
+        const f3 Oi = mulv(sub(Oo, c), iw), Di = mulv(Do, iw), rD = mulv(iDo, wd);
+        const float al = face_min(Oi, Di, rD);
+        const f3 Pg = add(mulv(add(muls(Di, al), Oi), wd), c);
+        const f3 v = sub(Oo, Pg);
+        const bool ok = has & (al < kFLTMAX) & ((double)dot3(v, v) < c2o);
+        // owners pull their jobs' decisions from the workers of this pass
+        const bool gl = need_l & (sL >= base) & (sL < base + n0), gr = need_r & (sR >= base) & (sR < base + n0);
+        const int wkl = gl ? (int)wl[sL - base] : lane, wkr = gr ? (int)wl[sR - base] : lane;
+        const uint32_t okl = bperm(wkl, ok ? 1u : 0u), okr = bperm(wkr, ok ? 1u : 0u);
+        if (gl) pass_l = okl != 0u;
+        if (gr) pass_r = okr != 0u;
+      }
+      __builtin_amdgcn_wave_barrier();   // own[] is rewritten next iteration
+      if (do_node) {
+        const bool hl = ne_l & (in_l | pass_l), hr = ne_r & (in_r | pass_r);
+        pop = !(hl || hr);
+        if (hr) {
+          if (hl) w.pending |= 1u << (w.level + 1);
+          w.node = (int)jn + 1; w.level++;
+        } else if (hl) {
+          w.node = (int)jn; w.level++;
+        }
+      }
+    }
+    if (pop) {
+      if (w.pending == 0) {
+        alive = false;
+      } else {
+        const int L = 31 - __builtin_clz(w.pending);
+        w.pending &= ~(1u << L);
+        w.node = ((w.node + 1) >> (w.level - L)) - 2;
+        w.level = L;
+      }
+    }
+    const int n = __builtin_popcountll(__ballot(alive));   // wave-uniform
+    if (n == 0 || (n <= exit && n0 - n >= min_done)) return !alive;
+  }
+}
+
 // walk_run for scenes with mesh instances.  The reference runs an instance's whole mesh DFS
 // (Mesh_intersect raytracer_func.frag:642-678) inside the scene DFS's leaf visit; nested that
 // way on the GPU, only the lanes sitting on a mesh leaf walk their (long, divergent) mesh
@@ -1149,9 +1275,6 @@ __device__ __forceinline__ float schlick(float r0, f3 I, f3 N) {   // :91-98
   return gclamp(r0 + ((((1.0f - r0) * x) * x * x) * x) * x, 0.0f, 1.0f);
 }
 
-__device__ __forceinline__ int mbcnt64(uint64_t m) {
-  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
 
 // ------------------------------------------------------------------------------------
 // the kernel
@@ -1370,7 +1493,12 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
       } else {
         if (!walking) { walk_begin<COUNT>(s, D, h, walk, ev, p.cull2_max); walking = true; }
         if constexpr (MESH) walking = !walk_run_mesh<COUNT, SUSPEND>(s, O, D, h, walk, ev, p.walk_exit);
-        else walking = !walk_run<COUNT, SUSPEND>(s, O, D, h, walk, ev, p.walk_exit, p.leaf_batch, p.walk_min_done);
+        else if constexpr (MCPT_FACE_JOBS && SUSPEND && !COUNT && !LDSS) {
+          if (p.leaf_batch > 0) walking = !walk_run_jobs(s, O, D, h, walk, p.walk_exit, p.leaf_batch, p.walk_min_done);
+          else walking = !walk_run<COUNT, SUSPEND>(s, O, D, h, walk, ev, p.walk_exit, p.leaf_batch, p.walk_min_done);
+        } else {
+          walking = !walk_run<COUNT, SUSPEND>(s, O, D, h, walk, ev, p.walk_exit, p.leaf_batch, p.walk_min_done);
+        }
         ready = !walking;
       }
     }
