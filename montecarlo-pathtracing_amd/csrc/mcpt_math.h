@@ -105,6 +105,36 @@ __device__ __forceinline__ float rsqrt_rn(float x) {
   return r;
 }
 
+// RN(a / b) from b's correctly rounded reciprocal y = RN(1/b) (rcp_core): q0 = RN(a y) is within
+// an ulp of a / b, so r = a - b q0 is exact in one fma and q1 = RN(q0 + r y) is the correctly
+// rounded quotient (Markstein's correction step; checked on all 2^46 significand pairs on gfx950,
+// tools/mathcheck/div_exhaustive.hip, tests/test_gpu_mathcheck.py).  5 VALU against the 11 of the
+// IEEE expansion, 3 of them shared by every division by the same b.  Exact for
+// 2^-60 <= |a|, |b| <= 2^60 and for a == 0 (div_core_ok): there y, q0, q1 are normal and r is 0
+// or at least |a| 2^-47; div_rn routes other operands to the IEEE expansion, wave-uniformly.
+__device__ __forceinline__ float div_core(float a, float b, float y) {
+  const float q = a * y;
+  return __builtin_fmaf(__builtin_fmaf(-b, q, a), y, q);
+}
+__device__ __forceinline__ bool div_b_ok(float b) {
+  const float ab = __builtin_fabsf(b);
+  return ab >= 0x1p-60f && ab <= 0x1p60f;
+}
+__device__ __forceinline__ bool div_a_ok(float a) {
+  const float aa = __builtin_fabsf(a);
+  return (aa >= 0x1p-60f && aa <= 0x1p60f) || a == 0.0f;
+}
+__device__ __forceinline__ bool div_core_ok(float a, float b) { return div_a_ok(a) && div_b_ok(b); }
+__device__ __attribute__((noinline)) inline float div_ieee(float a, float b) { return a / b; }
+__device__ __forceinline__ float div_rn(float a, float b) {
+  float q = div_core(a, b, rcp_core(b));
+  const bool ok = div_core_ok(a, b);
+  if (__builtin_expect(__ballot(!ok) != 0, 0)) {
+    if (!ok) q = div_ieee(a, b);
+  }
+  return q;
+}
+
 __device__ __forceinline__ float dot3(f3 a, f3 b) { return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x)); }
 __device__ __forceinline__ f3 normalize3(f3 a) { return muls(a, rsqrt_rn(dot3(a, a))); }
 __device__ __forceinline__ float length3(f3 a) { return sqrt_rn(dot3(a, a)); }
