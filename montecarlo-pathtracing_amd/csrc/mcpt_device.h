@@ -426,6 +426,22 @@ __device__ __forceinline__ void mesh_test(const SR& s, int mesh, int index, f3 O
 
 // 1: the L1/L2-read kernels (scene 8, C4 shape: +2.1 %; profiles/r04_ab_deep_walk.jsonl), 2: all,
 // 0: none (the LDS-scene C2 kernel: -0.6 % with it)
+// num / den from den's reciprocal y = rcp_core(den) by div_core (mcpt_math.h; exhaustively
+// checked), the IEEE division for the lanes whose operands leave div_core's exact range (ok false;
+// a wave-uniform branch, taken only when some lane is out of range).  Same bits as num / den.
+// MCPT_SHORT_DIV=0: the IEEE division everywhere.
+#ifndef MCPT_SHORT_DIV
+#define MCPT_SHORT_DIV 1
+#endif
+__device__ __forceinline__ float quot(float num, float den, float y, bool ok) {
+  if constexpr (!MCPT_SHORT_DIV || kDriverDiv) return fdiv(num, den);
+  float q = div_core(num, den, y);
+  if (__builtin_expect(__ballot(!ok) != 0, 0)) {
+    if (!ok) q = div_ieee(num, den);
+  }
+  return q;
+}
+
 #ifndef MCPT_ONE_ACCEPT
 #define MCPT_ONE_ACCEPT 1
 #endif
@@ -477,26 +493,32 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
     float delta4 = OD * OD - D2 * (OO - 1.0f);
     if (delta4 > 0.0f) {
       float sq = wsqrt<SR::kFastSqrt>(delta4);
-      float a = fdiv(-(OD + sq), D2);
+      // D2 = |D|^2 of a normalized D: within div_core's range
+      const float y = rcp_core(D2), n1 = -(OD + sq), n2 = -(OD - sq);
+      float a = quot(n1, D2, y, div_a_ok(n1));
       if (a > kEPS) accept(CODE_SPHERE, 0, add(O, muls(D, a)));
-      a = fdiv(-(OD - sq), D2);
+      a = quot(n2, D2, y, div_a_ok(n2));
       if (a > kEPS) accept_far(add(O, muls(D, a)));
     }
   } else if (t == CODE_QUAD) {
     if (!(D.z > -kEPS)) {
-      float a = fdiv(-O.z, D.z);
+      float a = quot(-O.z, D.z, rcp_core(D.z), div_a_ok(-O.z));   // D.z <= -kEPS
       f3 Pl = add(O, muls(D, a));
       if (!(__builtin_fabsf(Pl.x) > 1.0f || __builtin_fabsf(Pl.y) > 1.0f)) accept(CODE_QUAD, 0, Pl);
     }
   } else if (t == CODE_CUBE) {
     float al = kFLTMAX; int cl = 0;
     float o[3] = {O.x, O.y, O.z}, d[3] = {D.x, D.y, D.z};
+    // the two faces of an axis divide by the same d (one reciprocal); |d| > kEPS of a normalized
+    // D and, for |o| <= 2^59, the numerators cd - o (0 or >= 2^-24 in magnitude) are in range
+    const bool o_ok = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(O.x), __builtin_fabsf(O.y)), __builtin_fabsf(O.z)) <= 0x1p59f;
+    const float yd[3] = {rcp_core(D.x), rcp_core(D.y), rcp_core(D.z)};
 #pragma unroll
     for (int f = 0; f < 6; ++f) {
       const int c0 = f / 2, c1 = (c0 + 1) % 3, c2 = (c0 + 2) % 3;
       if (__builtin_fabsf(d[c0]) > kEPS) {
         const float cd = (f % 2) ? 1.0f : -1.0f;
-        float a = fdiv(cd - o[c0], d[c0]);
+        float a = quot(cd - o[c0], d[c0], yd[c0], o_ok);
         if ((a > kEPS) && (__builtin_fabsf(o[c1] + a * d[c1]) <= 1.0f) && (__builtin_fabsf(o[c2] + a * d[c2]) <= 1.0f))
           if (a < al) { al = a; cl = f; }
       }
@@ -505,12 +527,15 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
   } else if (t == CODE_CYLINDER) {
     int cl = -1; float al = kFLTMAX;
     if (__builtin_fabsf(D.z) > kEPS) {
-      float a = fdiv(-1.0f - O.z, D.z);
+      // the caps divide by D.z (one reciprocal; numerators as in the cube test)
+      const float yz = rcp_core(D.z);
+      const bool z_ok = __builtin_fabsf(O.z) <= 0x1p59f;
+      float a = quot(-1.0f - O.z, D.z, yz, z_ok);
       if (a > kEPS) {
         float rx = O.x + a * D.x, ry = O.y + a * D.y;
         if ((__builtin_fmaf(ry, ry, rx * rx) < 1.0f) && (a < al)) { cl = 0; al = a; }
       }
-      a = fdiv(1.0f - O.z, D.z);
+      a = quot(1.0f - O.z, D.z, yz, z_ok);
       if (a > kEPS) {
         float rx = O.x + a * D.x, ry = O.y + a * D.y;
         if ((__builtin_fmaf(ry, ry, rx * rx) < 1.0f) && (a < al)) { cl = 1; al = a; }
@@ -521,7 +546,8 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
     float D2 = __builtin_fmaf(D.y, D.y, D.x * D.x);
     float delta4 = OD * OD - D2 * (O2 - 1.0f);
     if (delta4 > 0.0f) {
-      float a = fdiv(-(OD + wsqrt<SR::kFastSqrt>(delta4)), D2);
+      const float n = -(OD + wsqrt<SR::kFastSqrt>(delta4));
+      float a = quot(n, D2, rcp_core(D2), div_a_ok(n) && div_b_ok(D2));
       if ((a > kEPS) && (a < al)) {
         float z = O.z + a * D.z;
         if (__builtin_fabsf(z) < 1.0f) { cl = 2; al = a; }
