@@ -46,8 +46,10 @@ enum mcpt_variant {
 /* BVH traversal strategy of the kernel (same results, different speed) */
 enum mcpt_traversal {
   MCPT_TRAVERSAL_AUTO = 0,   /* measured: after a scene upload, launches of >= 2^24 samples time
-                                the schedule candidates twice each (see mcpt_set_traversal);
-                                later launches of that shape use the fastest */
+                                the schedule candidates twice each (per-lane walks with 1/2/4 pass
+                                segments per work item, the wave-coherent walk for BVH depth < 8,
+                                the deep-BVH knobs at 4/8 segments for depth >= 8; never the stream
+                                schedule); later launches of that shape use the fastest */
   MCPT_TRAVERSAL_LANE = 1,   /* each lane walks its own DFS (divergent, vector loads) */
   MCPT_TRAVERSAL_WAVE = 2,   /* the wave walks the union of its lanes' DFS orders (scalar loads) */
   MCPT_TRAVERSAL_STREAM = 3, /* wavefront schedule: a pool of path slots in HBM, iterations of one
@@ -56,7 +58,8 @@ enum mcpt_traversal {
                                 Variant montecarlo.frag, scenes without meshes, bounces > 0; other
                                 renders run the per-lane walk.  mcpt_render returns once the
                                 iterations have been issued (it waits on the device while it issues
-                                them, to know when the slots are done) */
+                                them, to know when the slots are done).  Only when selected: AUTO
+                                never times it (5 % behind the megakernel on the deepest BVH) */
 };
 
 /* algorithmic-byte event counters, index order */
@@ -207,7 +210,9 @@ int mcpt_set_walk_exit(mcpt_ctx* ctx, int lanes);
 int mcpt_get_walk_exit(mcpt_ctx* ctx, int* resolved_lanes);
 
 /* Stream schedule (MCPT_TRAVERSAL_STREAM) knobs: path slots (0 = default 16 Mi; never more than
- * the launch's (pixel, pass segment) units; 248 B of device memory per slot, in two pools)
+ * the launch's (pixel, pass segment) units; 248 B of device memory per slot, in two pools: 4 GB
+ * per context at the default, allocated at the first stream render and freed when
+ * mcpt_set_traversal selects another schedule)
  * and the trace kernel's refill threshold (a wave takes new rays for its idle lanes once at
  * most `refill` lanes still walk; 0 = only when all are done; -1 = default 56).  Same results
  * for every value.  mcpt_stream_iterations: trace + shade iterations of the last stream launch
@@ -226,6 +231,9 @@ int mcpt_get_leaf_batch(mcpt_ctx* ctx, int* resolved_lanes);
  * cut at chunk boundaries (e.g. 84,000 passes at 4K in one call); the accumulator is
  * bit-identical for any budget.  Default 4 GiB (env MCPT_PARTIAL_BYTES at create). */
 int mcpt_set_partial_budget(mcpt_ctx* ctx, size_t bytes);
+/* (Device memory of a context: the accumulator (12 B per local pixel), the segment sums (up to
+ * this budget, allocated by the first launch that needs them) and, with the stream schedule,
+ * its pools; the scene buffers.) */
 /* Sub-launches the last render call was split into. */
 int mcpt_last_launch_count(mcpt_ctx* ctx, int* n_launches);
 /* 1 if the last render call ran one pass segment per pass: a call of 2..256 passes whose
