@@ -510,7 +510,8 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
     float al = kFLTMAX; int cl = 0;
     float o[3] = {O.x, O.y, O.z}, d[3] = {D.x, D.y, D.z};
     // the two faces of an axis divide by the same d (one reciprocal); |d| > kEPS of a normalized
-    // D and, for |o| <= 2^59, the numerators cd - o (0 or >= 2^-24 in magnitude) are in range
+    // D and, for |o| <= 2^59, the numerators cd - o (+0, never -0, or >= 2^-24 in magnitude) are
+    // in range
     const bool o_ok = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(O.x), __builtin_fabsf(O.y)), __builtin_fabsf(O.z)) <= 0x1p59f;
     const float yd[3] = {rcp_core(D.x), rcp_core(D.y), rcp_core(D.z)};
 #pragma unroll

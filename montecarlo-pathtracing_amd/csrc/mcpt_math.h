@@ -110,7 +110,7 @@ __device__ __forceinline__ float rsqrt_rn(float x) {
 // rounded quotient (Markstein's correction step; checked on all 2^46 significand pairs on gfx950,
 // tools/mathcheck/div_exhaustive.hip, tests/test_gpu_mathcheck.py).  5 VALU against the 11 of the
 // IEEE expansion, 3 of them shared by every division by the same b.  Exact for
-// 2^-60 <= |a|, |b| <= 2^60 and for a == 0 (div_core_ok): there y, q0, q1 are normal and r is 0
+// 2^-60 <= |a|, |b| <= 2^60 and for a == +0 (div_core_ok): there y, q0, q1 are normal and r is 0
 // or at least |a| 2^-47; div_rn routes other operands to the IEEE expansion, wave-uniformly.
 __device__ __forceinline__ float div_core(float a, float b, float y) {
   const float q = a * y;
@@ -120,9 +120,9 @@ __device__ __forceinline__ bool div_b_ok(float b) {
   const float ab = __builtin_fabsf(b);
   return ab >= 0x1p-60f && ab <= 0x1p60f;
 }
-__device__ __forceinline__ bool div_a_ok(float a) {
+__device__ __forceinline__ bool div_a_ok(float a) {   // (+0 only: div_core turns -0 / b into +0)
   const float aa = __builtin_fabsf(a);
-  return (aa >= 0x1p-60f && aa <= 0x1p60f) || a == 0.0f;
+  return (aa >= 0x1p-60f && aa <= 0x1p60f) || __float_as_uint(a) == 0u;
 }
 __device__ __forceinline__ bool div_core_ok(float a, float b) { return div_a_ok(a) && div_b_ok(b); }
 __device__ __attribute__((noinline)) inline float div_ieee(float a, float b) { return a / b; }

@@ -4,7 +4,7 @@
 // IEEE expansion, -fno-fast-math -- for every pair of binary32 significands: a, b in [1, 2),
 // 2^23 x 2^23 = 2^46 pairs.  Signs and exponents scale every step exactly (RN is symmetric and
 // commutes with powers of two) while no intermediate leaves the normal range, which
-// div_core_ok's bounds (2^-60 <= |a|, |b| <= 2^60, or a == 0) guarantee: there y, q0 and q1 are
+// div_core_ok's bounds (2^-60 <= |a|, |b| <= 2^60, or a == +0) guarantee: there y, q0 and q1 are
 // normal and r is 0 or at least |a| 2^-47.  A randomized pass over signs and exponents inside
 // those bounds (and around them) checks the wrapper div_rn, fallback included.
 // Prints one JSON object; exit status 0 iff no mismatch.
@@ -54,7 +54,8 @@ __global__ void check_random(unsigned long long seed, unsigned long long* bad, u
     const uint32_t ua = ((uint32_t)(r & 0x7FFFFFu)) | ((uint32_t)(ea + 127) << 23) | ((r >> 23) & 1u ? 0x80000000u : 0u);
     const uint32_t ub = ((uint32_t)((r >> 24) & 0x7FFFFFu)) | ((uint32_t)(eb + 127) << 23) | ((r >> 47) & 1u ? 0x80000000u : 0u);
     float a = __uint_as_float(ua), b = __uint_as_float(ub);
-    if ((r & 0xFFu) == 0u) a = 0.0f;   // zero dividends too
+    if ((r & 0xFFu) == 0u) a = 0.0f;    // zero dividends too, both signs
+    if ((r & 0xFFu) == 1u) a = -0.0f;
     n_in += mcpt::div_core_ok(a, b) ? 1u : 0u;
     const float got = mcpt::div_rn(a, b), want = a / b;
     if (__float_as_uint(got) != __float_as_uint(want)) ++n_bad;
