@@ -193,6 +193,10 @@ constexpr int kCandStream = MCPT_TRAVERSAL_STREAM, kCandLaneSeg2 = 4, kCandLaneS
 // r02_deep_knobs_sweep.jsonl): timed, not guessed
 constexpr int kCandDeepSeg4 = 6, kCandDeepSeg8 = 7, kCandLast = kCandDeepSeg8;
 constexpr int kDeepLeafBatch = 16, kDeepWalkExit = 40;
+// ... and they leave the walk loop only once at least 8 walks of the call have ended (shading
+// rounds with more lanes): C4 shape 593 -> 608 Msamples/s; 4 / 12 / 16: 603 / 605 / 604
+// (profiles/r04_ab_walk_min_done.jsonl)
+constexpr int kDeepMinDone = 8;
 // pass split (launch()): launches with fewer than this many work items per CU, of at most
 // kPassSplitMaxPasses passes
 constexpr int kPassSplitItemsPerCu = 4, kPassSplitMaxPasses = 256;
@@ -856,11 +860,14 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   p.wave_traversal = (mode == MCPT_TRAVERSAL_WAVE) ? 1 : 0;
   p.walk_exit = resolve_walk_exit(c);
   p.leaf_batch = resolve_leaf_batch(c);
-  p.walk_min_done = std::max(1, env_int("MCPT_WALK_MIN_DONE", 1));   // tuning hook (same bits for any value)
+  p.walk_min_done = 1;
   if (cand_deep_knobs(cand)) {   // the deep candidates' knobs, unless set explicitly
     if (c->walk_exit < 0) p.walk_exit = kDeepWalkExit;
     if (c->leaf_batch < 0) p.leaf_batch = kDeepLeafBatch;
+    p.walk_min_done = kDeepMinDone;
   }
+  // MCPT_WALK_MIN_DONE overrides (tuning hook; same bits for any value)
+  if (const int md = env_int("MCPT_WALK_MIN_DONE", 0); md > 0) p.walk_min_done = md;
   // pass segments per work item: candidate 3 of AUTO runs two; MCPT_SEG_PER_ITEM overrides
   const int env_seg = env_int("MCPT_SEG_PER_ITEM", 0);
   p.seg_per_item = env_seg > 0 ? env_seg : cand_seg_per_item(cand);
