@@ -442,6 +442,11 @@ __device__ __forceinline__ float quot(float num, float den, float y, bool ok) {
   return q;
 }
 
+// cube and cylinder tests sharing their z planes (see prim_test; 1: the L1/L2 kernels, 2: all)
+#ifndef MCPT_CUBE_CYL_SHARED
+#define MCPT_CUBE_CYL_SHARED 0
+#endif
+
 #ifndef MCPT_ONE_ACCEPT
 #define MCPT_ONE_ACCEPT 1
 #endif
@@ -473,6 +478,7 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
   // world point, length, compare, record update) once instead of once per type.  Each lane's
   // candidates reach the hit record in the same order (same bits).
   constexpr bool kOne = MCPT_ONE_ACCEPT == 2 || (MCPT_ONE_ACCEPT == 1 && !SR::kLds);
+  constexpr bool kCubeCyl = MCPT_CUBE_CYL_SHARED == 2 || (MCPT_CUBE_CYL_SHARED == 1 && !SR::kLds);
   bool has1 = false, has2 = false;
   int shape1 = 0, dir1 = 0;
   f3 P1 = mk(0.0f, 0.0f, 0.0f), P2 = P1;
@@ -506,6 +512,62 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
       f3 Pl = add(O, muls(D, a));
       if (!(__builtin_fabsf(Pl.x) > 1.0f || __builtin_fabsf(Pl.y) > 1.0f)) accept(CODE_QUAD, 0, Pl);
     }
+  } else if (kCubeCyl && (t == CODE_CUBE || t == CODE_CYLINDER)) {
+    // Cube and cylinder lanes share their z planes: the cube's z faces and the cylinder's caps
+    // are the same quotients (+-1 - O.z) / D.z with the same (O.x + a D.x, O.y + a D.y), tested
+    // against a square or a disc.  A leaf block whose lanes hold both types (scene 8: both in
+    // 99 % of the leaf blocks) then runs the z planes once.  Each type keeps its own order of
+    // candidates (cube: x-, x+, y-, y+, z-, z+; cylinder: caps -1, +1, then the side) and its
+    // strict `a < al` updates, so every lane's result is its own test's (same bits).
+    const bool cube = t == CODE_CUBE;
+    float al = kFLTMAX; int cl = cube ? 0 : -1;
+    if (cube) {
+      const float o[3] = {O.x, O.y, O.z}, d[3] = {D.x, D.y, D.z};
+      // the two faces of an axis divide by the same d (one reciprocal); |d| > kEPS of a
+      // normalized D and, for |o| <= 2^59, the numerators cd - o (+0, never -0, or >= 2^-24 in
+      // magnitude) are in range
+      const bool o_ok = __builtin_fmaxf(__builtin_fabsf(O.x), __builtin_fabsf(O.y)) <= 0x1p59f;
+      const float yd[2] = {rcp_core(D.x), rcp_core(D.y)};
+#pragma unroll
+      for (int f = 0; f < 4; ++f) {
+        const int c0 = f / 2, c1 = (c0 + 1) % 3, c2 = (c0 + 2) % 3;
+        if (__builtin_fabsf(d[c0]) > kEPS) {
+          const float cd = (f % 2) ? 1.0f : -1.0f;
+          float a = quot(cd - o[c0], d[c0], yd[c0], o_ok);
+          if ((a > kEPS) && (__builtin_fabsf(o[c1] + a * d[c1]) <= 1.0f) && (__builtin_fabsf(o[c2] + a * d[c2]) <= 1.0f))
+            if (a < al) { al = a; cl = f; }
+        }
+      }
+    }
+    if (__builtin_fabsf(D.z) > kEPS) {
+      const float yz = rcp_core(D.z);
+      const bool z_ok = __builtin_fabsf(O.z) <= 0x1p59f;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const float a = quot((k ? 1.0f : -1.0f) - O.z, D.z, yz, z_ok);
+        if (a > kEPS) {
+          const float rx = O.x + a * D.x, ry = O.y + a * D.y;
+          const bool in = cube ? (__builtin_fabsf(rx) <= 1.0f) & (__builtin_fabsf(ry) <= 1.0f)
+                               : __builtin_fmaf(ry, ry, rx * rx) < 1.0f;
+          if (in && (a < al)) { al = a; cl = cube ? 4 + k : k; }
+        }
+      }
+    }
+    if (!cube) {
+      float O2 = __builtin_fmaf(O.y, O.y, O.x * O.x);
+      float OD = __builtin_fmaf(O.y, D.y, O.x * D.x);
+      float D2 = __builtin_fmaf(D.y, D.y, D.x * D.x);
+      float delta4 = OD * OD - D2 * (O2 - 1.0f);
+      if (delta4 > 0.0f) {
+        const float n = -(OD + wsqrt<SR::kFastSqrt>(delta4));
+        float a = quot(n, D2, rcp_core(D2), div_a_ok(n) && div_b_ok(D2));
+        if ((a > kEPS) && (a < al)) {
+          float z = O.z + a * D.z;
+          if (__builtin_fabsf(z) < 1.0f) { cl = 2; al = a; }
+        }
+      }
+    }
+    if (al < kFLTMAX) accept(cube ? CODE_CUBE : CODE_CYLINDER, cl, add(O, muls(D, al)));
   } else if (t == CODE_CUBE) {
     float al = kFLTMAX; int cl = 0;
     float o[3] = {O.x, O.y, O.z}, d[3] = {D.x, D.y, D.z};
