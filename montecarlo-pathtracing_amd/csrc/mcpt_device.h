@@ -189,6 +189,23 @@ __device__ __forceinline__ int box_stage(float4 a0, float4 a1, float4 a2, f3 O, 
 }
 #endif
 
+// one face of intersect_bv's loop (raytracer_func.frag:322-345) folded into the running minimum
+// al: a = (cd - oa) / da as (cd - oa) * ra (hoisted reciprocal, contract), valid when the axis
+// divides (dv), a > EPSILON and the hit lies in the face (|ob + a db| <= 1, |oc + a dc| <= 1).
+// `if (a < al) al = a` == min(al, valid ? a : FLT_MAX) for the non-NaN a a valid face has;
+// bitwise & keeps the compares in SGPR masks instead of exec-mask branches (+5 %, r01_ab4).
+// The two in-face bounds are one compare of their NaN-propagating maximum (v_maximum3_f32):
+// maximum(|p|, |q|) <= 1 == (|p| <= 1) & (|q| <= 1) for every p, q, NaN included.  One SGPR
+// mask op fewer per face, same VALU count: C4 shape +2.3 %, C2 +1.2..1.7 %, scene 3 +0.5 %
+// (profiles/r04_ab_face_max3.jsonl).
+__device__ __forceinline__ float box_face(float al, float cd, float oa, bool dv, float ra, float ob, float db,
+                                          float oc, float dc) {
+  const float a = (cd - oa) * ra;
+  const bool ok = dv & (a > kEPS) &
+                  (__builtin_elementwise_maximum(__builtin_fabsf(ob + a * db), __builtin_fabsf(oc + a * dc)) <= 1.0f);
+  return __builtin_fminf(al, ok ? a : kFLTMAX);
+}
+
 // intersect_bv raytracer_func.frag:314-352; divisions as hoisted reciprocals (contract).
 // WAVE: the all-lanes-inside early out is taken wave-uniformly (big boxes such as the
 // ground's contain every ray origin).
@@ -197,30 +214,25 @@ __device__ __forceinline__ bool box_test(float4 a0, float4 a1, float4 a2, f3 O, 
   f3 c = mk(a0.x, a0.y, a0.z), w = mk(a1.x, a1.y, a1.z), iw = mk(a2.x, a2.y, a2.z);
   f3 Oi = mulv(sub(O, c), iw);
   f3 Di = mulv(D, iw);
+#if MCPT_INSIDE_MAX3
+  // all |Oi| < 1 as one compare of the NaN-propagating maximum (exact, as in box_face)
+  const bool inside = __builtin_elementwise_maximum(__builtin_elementwise_maximum(__builtin_fabsf(Oi.x), __builtin_fabsf(Oi.y)),
+                                                    __builtin_fabsf(Oi.z)) < 1.0f;
+#else
   const bool inside = __builtin_fabsf(Oi.x) < 1.0f && __builtin_fabsf(Oi.y) < 1.0f && __builtin_fabsf(Oi.z) < 1.0f;
+#endif
   if (WAVE && __ballot(!inside) == 0) return true;
   if (inside) return true;
   f3 rD = mulv(invD, w);
-  // faces in reference order: (x,-1) (x,+1) (y,-1) (y,+1) (z,-1) (z,+1).  Branch-free:
-  // every face is evaluated and the valid minimum kept with a select (`if (a < al) al = a`
-  // == min(al, valid ? a : FLT_MAX) for the non-NaN a a valid face has); bitwise & keeps
-  // the compares in SGPR masks instead of exec-mask branches (+5 % Msamples/s, r01_ab4).
+  // faces in reference order: (x,-1) (x,+1) (y,-1) (y,+1) (z,-1) (z,+1), branch-free (box_face)
   const bool dx = __builtin_fabsf(Di.x) > kEPS, dy = __builtin_fabsf(Di.y) > kEPS, dz = __builtin_fabsf(Di.z) > kEPS;
   float al = kFLTMAX;
-#define MCPT_FACE(CD, OA, DV, RA, OB, DB, OC, DC)                                              \
-  {                                                                                            \
-    const float a = ((CD) - (OA)) * (RA);                                                      \
-    const bool ok = (DV) & (a > kEPS) & (__builtin_fabsf(OB + a * DB) <= 1.0f) &               \
-                    (__builtin_fabsf(OC + a * DC) <= 1.0f);                                    \
-    al = __builtin_fminf(al, ok ? a : kFLTMAX);                                                \
-  }
-  MCPT_FACE(-1.0f, Oi.x, dx, rD.x, Oi.y, Di.y, Oi.z, Di.z)
-  MCPT_FACE(1.0f, Oi.x, dx, rD.x, Oi.y, Di.y, Oi.z, Di.z)
-  MCPT_FACE(-1.0f, Oi.y, dy, rD.y, Oi.z, Di.z, Oi.x, Di.x)
-  MCPT_FACE(1.0f, Oi.y, dy, rD.y, Oi.z, Di.z, Oi.x, Di.x)
-  MCPT_FACE(-1.0f, Oi.z, dz, rD.z, Oi.x, Di.x, Oi.y, Di.y)
-  MCPT_FACE(1.0f, Oi.z, dz, rD.z, Oi.x, Di.x, Oi.y, Di.y)
-#undef MCPT_FACE
+  al = box_face(al, -1.0f, Oi.x, dx, rD.x, Oi.y, Di.y, Oi.z, Di.z);
+  al = box_face(al, 1.0f, Oi.x, dx, rD.x, Oi.y, Di.y, Oi.z, Di.z);
+  al = box_face(al, -1.0f, Oi.y, dy, rD.y, Oi.z, Di.z, Oi.x, Di.x);
+  al = box_face(al, 1.0f, Oi.y, dy, rD.y, Oi.z, Di.z, Oi.x, Di.x);
+  al = box_face(al, -1.0f, Oi.z, dz, rD.z, Oi.x, Di.x, Oi.y, Di.y);
+  al = box_face(al, 1.0f, Oi.z, dz, rD.z, Oi.x, Di.x, Oi.y, Di.y);
   if (al < kFLTMAX) {
     f3 Pg = add(mulv(add(muls(Di, al), Oi), w), c);
     f3 v = sub(O, Pg);
@@ -298,20 +310,12 @@ __device__ __forceinline__ bool box_test_mesh(float4 a0, float4 a1, float4 a2, f
   f3 rD = mulv(invD, w);
   const bool dx = __builtin_fabsf(Di.x) > kEPS, dy = __builtin_fabsf(Di.y) > kEPS, dz = __builtin_fabsf(Di.z) > kEPS;
   float al = kFLTMAX;
-#define MCPT_FACE(CD, OA, DV, RA, OB, DB, OC, DC)                                              \
-  {                                                                                            \
-    const float a = ((CD) - (OA)) * (RA);                                                      \
-    const bool ok = (DV) & (a > kEPS) & (__builtin_fabsf(OB + a * DB) <= 1.0f) &               \
-                    (__builtin_fabsf(OC + a * DC) <= 1.0f);                                    \
-    al = __builtin_fminf(al, ok ? a : kFLTMAX);                                                \
-  }
-  MCPT_FACE(-1.0f, Oi.x, dx, rD.x, Oi.y, Di.y, Oi.z, Di.z)
-  MCPT_FACE(1.0f, Oi.x, dx, rD.x, Oi.y, Di.y, Oi.z, Di.z)
-  MCPT_FACE(-1.0f, Oi.y, dy, rD.y, Oi.z, Di.z, Oi.x, Di.x)
-  MCPT_FACE(1.0f, Oi.y, dy, rD.y, Oi.z, Di.z, Oi.x, Di.x)
-  MCPT_FACE(-1.0f, Oi.z, dz, rD.z, Oi.x, Di.x, Oi.y, Di.y)
-  MCPT_FACE(1.0f, Oi.z, dz, rD.z, Oi.x, Di.x, Oi.y, Di.y)
-#undef MCPT_FACE
+  al = box_face(al, -1.0f, Oi.x, dx, rD.x, Oi.y, Di.y, Oi.z, Di.z);
+  al = box_face(al, 1.0f, Oi.x, dx, rD.x, Oi.y, Di.y, Oi.z, Di.z);
+  al = box_face(al, -1.0f, Oi.y, dy, rD.y, Oi.z, Di.z, Oi.x, Di.x);
+  al = box_face(al, 1.0f, Oi.y, dy, rD.y, Oi.z, Di.z, Oi.x, Di.x);
+  al = box_face(al, -1.0f, Oi.z, dz, rD.z, Oi.x, Di.x, Oi.y, Di.y);
+  al = box_face(al, 1.0f, Oi.z, dz, rD.z, Oi.x, Di.x, Oi.y, Di.y);
   if (al < kFLTMAX) {
     f3 Pl = add(Oi, muls(Di, al));
     f3 Pg = xpoint(t0, t1, t2, add(mulv(Pl, w), c));
@@ -442,11 +446,6 @@ __device__ __forceinline__ float quot(float num, float den, float y, bool ok) {
   return q;
 }
 
-// cube and cylinder tests sharing their z planes (see prim_test; 1: the L1/L2 kernels, 2: all)
-#ifndef MCPT_CUBE_CYL_SHARED
-#define MCPT_CUBE_CYL_SHARED 0
-#endif
-
 #ifndef MCPT_ONE_ACCEPT
 #define MCPT_ONE_ACCEPT 1
 #endif
@@ -478,7 +477,6 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
   // world point, length, compare, record update) once instead of once per type.  Each lane's
   // candidates reach the hit record in the same order (same bits).
   constexpr bool kOne = MCPT_ONE_ACCEPT == 2 || (MCPT_ONE_ACCEPT == 1 && !SR::kLds);
-  constexpr bool kCubeCyl = MCPT_CUBE_CYL_SHARED == 2 || (MCPT_CUBE_CYL_SHARED == 1 && !SR::kLds);
   bool has1 = false, has2 = false;
   int shape1 = 0, dir1 = 0;
   f3 P1 = mk(0.0f, 0.0f, 0.0f), P2 = P1;
@@ -512,62 +510,6 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
       f3 Pl = add(O, muls(D, a));
       if (!(__builtin_fabsf(Pl.x) > 1.0f || __builtin_fabsf(Pl.y) > 1.0f)) accept(CODE_QUAD, 0, Pl);
     }
-  } else if (kCubeCyl && (t == CODE_CUBE || t == CODE_CYLINDER)) {
-    // Cube and cylinder lanes share their z planes: the cube's z faces and the cylinder's caps
-    // are the same quotients (+-1 - O.z) / D.z with the same (O.x + a D.x, O.y + a D.y), tested
-    // against a square or a disc.  A leaf block whose lanes hold both types (scene 8: both in
-    // 99 % of the leaf blocks) then runs the z planes once.  Each type keeps its own order of
-    // candidates (cube: x-, x+, y-, y+, z-, z+; cylinder: caps -1, +1, then the side) and its
-    // strict `a < al` updates, so every lane's result is its own test's (same bits).
-    const bool cube = t == CODE_CUBE;
-    float al = kFLTMAX; int cl = cube ? 0 : -1;
-    if (cube) {
-      const float o[3] = {O.x, O.y, O.z}, d[3] = {D.x, D.y, D.z};
-      // the two faces of an axis divide by the same d (one reciprocal); |d| > kEPS of a
-      // normalized D and, for |o| <= 2^59, the numerators cd - o (+0, never -0, or >= 2^-24 in
-      // magnitude) are in range
-      const bool o_ok = __builtin_fmaxf(__builtin_fabsf(O.x), __builtin_fabsf(O.y)) <= 0x1p59f;
-      const float yd[2] = {rcp_core(D.x), rcp_core(D.y)};
-#pragma unroll
-      for (int f = 0; f < 4; ++f) {
-        const int c0 = f / 2, c1 = (c0 + 1) % 3, c2 = (c0 + 2) % 3;
-        if (__builtin_fabsf(d[c0]) > kEPS) {
-          const float cd = (f % 2) ? 1.0f : -1.0f;
-          float a = quot(cd - o[c0], d[c0], yd[c0], o_ok);
-          if ((a > kEPS) && (__builtin_fabsf(o[c1] + a * d[c1]) <= 1.0f) && (__builtin_fabsf(o[c2] + a * d[c2]) <= 1.0f))
-            if (a < al) { al = a; cl = f; }
-        }
-      }
-    }
-    if (__builtin_fabsf(D.z) > kEPS) {
-      const float yz = rcp_core(D.z);
-      const bool z_ok = __builtin_fabsf(O.z) <= 0x1p59f;
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const float a = quot((k ? 1.0f : -1.0f) - O.z, D.z, yz, z_ok);
-        if (a > kEPS) {
-          const float rx = O.x + a * D.x, ry = O.y + a * D.y;
-          const bool in = cube ? (__builtin_fabsf(rx) <= 1.0f) & (__builtin_fabsf(ry) <= 1.0f)
-                               : __builtin_fmaf(ry, ry, rx * rx) < 1.0f;
-          if (in && (a < al)) { al = a; cl = cube ? 4 + k : k; }
-        }
-      }
-    }
-    if (!cube) {
-      float O2 = __builtin_fmaf(O.y, O.y, O.x * O.x);
-      float OD = __builtin_fmaf(O.y, D.y, O.x * D.x);
-      float D2 = __builtin_fmaf(D.y, D.y, D.x * D.x);
-      float delta4 = OD * OD - D2 * (O2 - 1.0f);
-      if (delta4 > 0.0f) {
-        const float n = -(OD + wsqrt<SR::kFastSqrt>(delta4));
-        float a = quot(n, D2, rcp_core(D2), div_a_ok(n) && div_b_ok(D2));
-        if ((a > kEPS) && (a < al)) {
-          float z = O.z + a * D.z;
-          if (__builtin_fabsf(z) < 1.0f) { cl = 2; al = a; }
-        }
-      }
-    }
-    if (al < kFLTMAX) accept(cube ? CODE_CUBE : CODE_CYLINDER, cl, add(O, muls(D, al)));
   } else if (t == CODE_CUBE) {
     float al = kFLTMAX; int cl = 0;
     float o[3] = {O.x, O.y, O.z}, d[3] = {D.x, D.y, D.z};
@@ -582,8 +524,15 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
       if (__builtin_fabsf(d[c0]) > kEPS) {
         const float cd = (f % 2) ? 1.0f : -1.0f;
         float a = quot(cd - o[c0], d[c0], yd[c0], o_ok);
+#if MCPT_CUBE_MAX3
+        if ((a > kEPS) & (a < al) &
+            (__builtin_elementwise_maximum(__builtin_fabsf(o[c1] + a * d[c1]), __builtin_fabsf(o[c2] + a * d[c2])) <= 1.0f)) {
+          al = a; cl = f;
+        }
+#else
         if ((a > kEPS) && (__builtin_fabsf(o[c1] + a * d[c1]) <= 1.0f) && (__builtin_fabsf(o[c2] + a * d[c2]) <= 1.0f))
           if (a < al) { al = a; cl = f; }
+#endif
       }
     }
     if (al < kFLTMAX) accept(CODE_CUBE, cl, add(O, muls(D, al)));
@@ -594,15 +543,29 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
       const float yz = rcp_core(D.z);
       const bool z_ok = __builtin_fabsf(O.z) <= 0x1p59f;
       float a = quot(-1.0f - O.z, D.z, yz, z_ok);
+#if MCPT_CYL_MASKS
+      {
+        float rx = O.x + a * D.x, ry = O.y + a * D.y;
+        if ((a > kEPS) & (__builtin_fmaf(ry, ry, rx * rx) < 1.0f) & (a < al)) { cl = 0; al = a; }
+      }
+#else
       if (a > kEPS) {
         float rx = O.x + a * D.x, ry = O.y + a * D.y;
         if ((__builtin_fmaf(ry, ry, rx * rx) < 1.0f) && (a < al)) { cl = 0; al = a; }
       }
+#endif
       a = quot(1.0f - O.z, D.z, yz, z_ok);
+#if MCPT_CYL_MASKS
+      {
+        float rx = O.x + a * D.x, ry = O.y + a * D.y;
+        if ((a > kEPS) & (__builtin_fmaf(ry, ry, rx * rx) < 1.0f) & (a < al)) { cl = 1; al = a; }
+      }
+#else
       if (a > kEPS) {
         float rx = O.x + a * D.x, ry = O.y + a * D.y;
         if ((__builtin_fmaf(ry, ry, rx * rx) < 1.0f) && (a < al)) { cl = 1; al = a; }
       }
+#endif
     }
     float O2 = __builtin_fmaf(O.y, O.y, O.x * O.x);
     float OD = __builtin_fmaf(O.y, D.y, O.x * D.x);
@@ -611,10 +574,14 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
     if (delta4 > 0.0f) {
       const float n = -(OD + wsqrt<SR::kFastSqrt>(delta4));
       float a = quot(n, D2, rcp_core(D2), div_a_ok(n) && div_b_ok(D2));
+#if MCPT_CYL_MASKS
+      if ((a > kEPS) & (a < al) & (__builtin_fabsf(O.z + a * D.z) < 1.0f)) { cl = 2; al = a; }
+#else
       if ((a > kEPS) && (a < al)) {
         float z = O.z + a * D.z;
         if (__builtin_fabsf(z) < 1.0f) { cl = 2; al = a; }
       }
+#endif
     }
     if (al < kFLTMAX) accept(CODE_CYLINDER, cl, add(O, muls(D, al)));
   } else if (t == CODE_CONE) {
