@@ -189,6 +189,9 @@ __device__ __forceinline__ int box_stage(float4 a0, float4 a1, float4 a2, f3 O, 
 }
 #endif
 
+#ifndef MCPT_FACE_FIRST
+#define MCPT_FACE_FIRST 0
+#endif
 // one face of intersect_bv's loop (raytracer_func.frag:322-345) folded into the running minimum
 // al: a = (cd - oa) / da as (cd - oa) * ra (hoisted reciprocal, contract), valid when the axis
 // divides (dv), a > EPSILON and the hit lies in the face (|ob + a db| <= 1, |oc + a dc| <= 1).
@@ -198,11 +201,17 @@ __device__ __forceinline__ int box_stage(float4 a0, float4 a1, float4 a2, f3 O, 
 // maximum(|p|, |q|) <= 1 == (|p| <= 1) & (|q| <= 1) for every p, q, NaN included.  One SGPR
 // mask op fewer per face, same VALU count: C4 shape +2.3 %, C2 +1.2..1.7 %, scene 3 +0.5 %
 // (profiles/r04_ab_face_max3.jsonl).
+template <bool FIRST = false>
 __device__ __forceinline__ float box_face(float al, float cd, float oa, bool dv, float ra, float ob, float db,
                                           float oc, float dc) {
   const float a = (cd - oa) * ra;
   const bool ok = dv & (a > kEPS) &
                   (__builtin_elementwise_maximum(__builtin_fabsf(ob + a * db), __builtin_fabsf(oc + a * dc)) <= 1.0f);
+  // MCPT_FACE_FIRST (A/B knob): the first face's candidate is al itself, without the min against
+  // the starting kFLTMAX.  Only a candidate above kFLTMAX (3.402823e38 < a <= +inf) differs, and
+  // either way al stays >= kFLTMAX until a smaller valid face: the box's result (al < kFLTMAX,
+  // then the entry point from al) is the same.
+  if constexpr (FIRST && MCPT_FACE_FIRST) return ok ? a : kFLTMAX;
   return __builtin_fminf(al, ok ? a : kFLTMAX);
 }
 
@@ -227,7 +236,7 @@ __device__ __forceinline__ bool box_test(float4 a0, float4 a1, float4 a2, f3 O, 
   // faces in reference order: (x,-1) (x,+1) (y,-1) (y,+1) (z,-1) (z,+1), branch-free (box_face)
   const bool dx = __builtin_fabsf(Di.x) > kEPS, dy = __builtin_fabsf(Di.y) > kEPS, dz = __builtin_fabsf(Di.z) > kEPS;
   float al = kFLTMAX;
-  al = box_face(al, -1.0f, Oi.x, dx, rD.x, Oi.y, Di.y, Oi.z, Di.z);
+  al = box_face<true>(al, -1.0f, Oi.x, dx, rD.x, Oi.y, Di.y, Oi.z, Di.z);
   al = box_face(al, 1.0f, Oi.x, dx, rD.x, Oi.y, Di.y, Oi.z, Di.z);
   al = box_face(al, -1.0f, Oi.y, dy, rD.y, Oi.z, Di.z, Oi.x, Di.x);
   al = box_face(al, 1.0f, Oi.y, dy, rD.y, Oi.z, Di.z, Oi.x, Di.x);
@@ -310,7 +319,7 @@ __device__ __forceinline__ bool box_test_mesh(float4 a0, float4 a1, float4 a2, f
   f3 rD = mulv(invD, w);
   const bool dx = __builtin_fabsf(Di.x) > kEPS, dy = __builtin_fabsf(Di.y) > kEPS, dz = __builtin_fabsf(Di.z) > kEPS;
   float al = kFLTMAX;
-  al = box_face(al, -1.0f, Oi.x, dx, rD.x, Oi.y, Di.y, Oi.z, Di.z);
+  al = box_face<true>(al, -1.0f, Oi.x, dx, rD.x, Oi.y, Di.y, Oi.z, Di.z);
   al = box_face(al, 1.0f, Oi.x, dx, rD.x, Oi.y, Di.y, Oi.z, Di.z);
   al = box_face(al, -1.0f, Oi.y, dy, rD.y, Oi.z, Di.z, Oi.x, Di.x);
   al = box_face(al, 1.0f, Oi.y, dy, rD.y, Oi.z, Di.z, Oi.x, Di.x);
@@ -521,6 +530,17 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
 #pragma unroll
     for (int f = 0; f < 6; ++f) {
       const int c0 = f / 2, c1 = (c0 + 1) % 3, c2 = (c0 + 2) % 3;
+#if MCPT_CUBE_MAX3 == 2
+      {   // branch-free: every face's quotient, the axis flag in the mask
+        const bool dv = __builtin_fabsf(d[c0]) > kEPS;
+        const float cd = (f % 2) ? 1.0f : -1.0f;
+        float a = quot(cd - o[c0], d[c0], yd[c0], o_ok);
+        if (dv & (a > kEPS) & (a < al) &
+            (__builtin_elementwise_maximum(__builtin_fabsf(o[c1] + a * d[c1]), __builtin_fabsf(o[c2] + a * d[c2])) <= 1.0f)) {
+          al = a; cl = f;
+        }
+      }
+#else
       if (__builtin_fabsf(d[c0]) > kEPS) {
         const float cd = (f % 2) ? 1.0f : -1.0f;
         float a = quot(cd - o[c0], d[c0], yd[c0], o_ok);
@@ -534,11 +554,27 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
           if (a < al) { al = a; cl = f; }
 #endif
       }
+#endif
     }
     if (al < kFLTMAX) accept(CODE_CUBE, cl, add(O, muls(D, al)));
   } else if (t == CODE_CYLINDER) {
     int cl = -1; float al = kFLTMAX;
+#if MCPT_CYL_MASKS == 2
+    {   // branch-free caps: the axis flag in the masks
+      const bool dz = __builtin_fabsf(D.z) > kEPS;
+      const float yz = rcp_core(D.z);
+      const bool z_ok = __builtin_fabsf(O.z) <= 0x1p59f;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const float a = quot((k ? 1.0f : -1.0f) - O.z, D.z, yz, z_ok);
+        const float rx = O.x + a * D.x, ry = O.y + a * D.y;
+        if (dz & (a > kEPS) & (__builtin_fmaf(ry, ry, rx * rx) < 1.0f) & (a < al)) { cl = k; al = a; }
+      }
+    }
+    if (false) {
+#else
     if (__builtin_fabsf(D.z) > kEPS) {
+#endif
       // the caps divide by D.z (one reciprocal; numerators as in the cube test)
       const float yz = rcp_core(D.z);
       const bool z_ok = __builtin_fabsf(O.z) <= 0x1p59f;
@@ -718,12 +754,24 @@ __device__ __forceinline__ bool walk_run(const SR& s, f3 O, f3 D, Hit& h, Walk& 
     bool pop = true;
     bool is_leaf = w.node >= leaf0;
     bool do_leaf = is_leaf, do_node = !is_leaf;
+#if MCPT_WALK_HEAD
+    if (SUSPEND) {   // wave-uniform choice of the block; the ballot taken where is_leaf is computed
+      const uint64_t on_leaf = __ballot(is_leaf);
+      const bool leaves = leaf_batch <= 0 || __builtin_popcountll(on_leaf) >= leaf_batch ||
+                          on_leaf == __builtin_amdgcn_read_exec();
+      if (leaf_batch > 0) {
+        do_leaf = leaves && is_leaf;
+        do_node = !leaves && !is_leaf;
+      }
+    }
+#else
     if (SUSPEND && leaf_batch > 0) {   // wave-uniform choice of the block
       const uint64_t on_leaf = __ballot(is_leaf), act = __ballot(1);
       const bool leaves = __builtin_popcountll(on_leaf) >= leaf_batch || on_leaf == act;
       do_leaf = leaves && is_leaf;
       do_node = !leaves && !is_leaf;
     }
+#endif
 #ifdef MCPT_STAMPS
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();   // wave-uniform stamps
 #endif
