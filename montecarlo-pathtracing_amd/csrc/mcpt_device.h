@@ -189,9 +189,6 @@ __device__ __forceinline__ int box_stage(float4 a0, float4 a1, float4 a2, f3 O, 
 }
 #endif
 
-#ifndef MCPT_FACE_FIRST
-#define MCPT_FACE_FIRST 0
-#endif
 // one face of intersect_bv's loop (raytracer_func.frag:322-345) folded into the running minimum
 // al: a = (cd - oa) / da as (cd - oa) * ra (hoisted reciprocal, contract), valid when the axis
 // divides (dv), a > EPSILON and the hit lies in the face (|ob + a db| <= 1, |oc + a dc| <= 1).
@@ -207,11 +204,11 @@ __device__ __forceinline__ float box_face(float al, float cd, float oa, bool dv,
   const float a = (cd - oa) * ra;
   const bool ok = dv & (a > kEPS) &
                   (__builtin_elementwise_maximum(__builtin_fabsf(ob + a * db), __builtin_fabsf(oc + a * dc)) <= 1.0f);
-  // MCPT_FACE_FIRST (A/B knob): the first face's candidate is al itself, without the min against
-  // the starting kFLTMAX.  Only a candidate above kFLTMAX (3.402823e38 < a <= +inf) differs, and
-  // either way al stays >= kFLTMAX until a smaller valid face: the box's result (al < kFLTMAX,
-  // then the entry point from al) is the same.
-  if constexpr (FIRST && MCPT_FACE_FIRST) return ok ? a : kFLTMAX;
+  // FIRST: the first face's candidate is al itself, without the min against the starting
+  // kFLTMAX.  Only a candidate above kFLTMAX (3.402823e38 < a <= +inf) differs, and either way
+  // al stays >= kFLTMAX until a smaller valid face: the box's result (al < kFLTMAX, then the
+  // entry point from al) is the same (tests/test_box_face_forms.py).
+  if constexpr (FIRST) return ok ? a : kFLTMAX;
   return __builtin_fminf(al, ok ? a : kFLTMAX);
 }
 
@@ -223,13 +220,9 @@ __device__ __forceinline__ bool box_test(float4 a0, float4 a1, float4 a2, f3 O, 
   f3 c = mk(a0.x, a0.y, a0.z), w = mk(a1.x, a1.y, a1.z), iw = mk(a2.x, a2.y, a2.z);
   f3 Oi = mulv(sub(O, c), iw);
   f3 Di = mulv(D, iw);
-#if MCPT_INSIDE_MAX3
   // all |Oi| < 1 as one compare of the NaN-propagating maximum (exact, as in box_face)
   const bool inside = __builtin_elementwise_maximum(__builtin_elementwise_maximum(__builtin_fabsf(Oi.x), __builtin_fabsf(Oi.y)),
                                                     __builtin_fabsf(Oi.z)) < 1.0f;
-#else
-  const bool inside = __builtin_fabsf(Oi.x) < 1.0f && __builtin_fabsf(Oi.y) < 1.0f && __builtin_fabsf(Oi.z) < 1.0f;
-#endif
   if (WAVE && __ballot(!inside) == 0) return true;
   if (inside) return true;
   f3 rD = mulv(invD, w);
@@ -530,78 +523,33 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
 #pragma unroll
     for (int f = 0; f < 6; ++f) {
       const int c0 = f / 2, c1 = (c0 + 1) % 3, c2 = (c0 + 2) % 3;
-#if MCPT_CUBE_MAX3 == 2
-      {   // branch-free: every face's quotient, the axis flag in the mask
-        const bool dv = __builtin_fabsf(d[c0]) > kEPS;
-        const float cd = (f % 2) ? 1.0f : -1.0f;
-        float a = quot(cd - o[c0], d[c0], yd[c0], o_ok);
-        if (dv & (a > kEPS) & (a < al) &
-            (__builtin_elementwise_maximum(__builtin_fabsf(o[c1] + a * d[c1]), __builtin_fabsf(o[c2] + a * d[c2])) <= 1.0f)) {
-          al = a; cl = f;
-        }
+      // branch-free: every face's quotient, the axis flag and the in-face bounds (one compare
+      // of their NaN-propagating maximum, as in box_face) in one mask; the strict a < al keeps
+      // the reference's first-minimum face.  A face of a non-dividing axis (|d| <= kEPS) gets a
+      // meaningless quotient that the mask drops.  C4 shape +0.5 %, scene 3 +4.4 % over the
+      // branching form (profiles/r04_ab_masks.jsonl).
+      const bool dv = __builtin_fabsf(d[c0]) > kEPS;
+      const float cd = (f % 2) ? 1.0f : -1.0f;
+      const float a = quot(cd - o[c0], d[c0], yd[c0], o_ok);
+      if (dv & (a > kEPS) & (a < al) &
+          (__builtin_elementwise_maximum(__builtin_fabsf(o[c1] + a * d[c1]), __builtin_fabsf(o[c2] + a * d[c2])) <= 1.0f)) {
+        al = a; cl = f;
       }
-#else
-      if (__builtin_fabsf(d[c0]) > kEPS) {
-        const float cd = (f % 2) ? 1.0f : -1.0f;
-        float a = quot(cd - o[c0], d[c0], yd[c0], o_ok);
-#if MCPT_CUBE_MAX3
-        if ((a > kEPS) & (a < al) &
-            (__builtin_elementwise_maximum(__builtin_fabsf(o[c1] + a * d[c1]), __builtin_fabsf(o[c2] + a * d[c2])) <= 1.0f)) {
-          al = a; cl = f;
-        }
-#else
-        if ((a > kEPS) && (__builtin_fabsf(o[c1] + a * d[c1]) <= 1.0f) && (__builtin_fabsf(o[c2] + a * d[c2]) <= 1.0f))
-          if (a < al) { al = a; cl = f; }
-#endif
-      }
-#endif
     }
     if (al < kFLTMAX) accept(CODE_CUBE, cl, add(O, muls(D, al)));
   } else if (t == CODE_CYLINDER) {
     int cl = -1; float al = kFLTMAX;
-#if MCPT_CYL_MASKS == 2
-    {   // branch-free caps: the axis flag in the masks
-      const bool dz = __builtin_fabsf(D.z) > kEPS;
+    if (__builtin_fabsf(D.z) > kEPS) {
+      // the caps divide by D.z (one reciprocal; numerators as in the cube test); each
+      // candidate's conditions in one mask
       const float yz = rcp_core(D.z);
       const bool z_ok = __builtin_fabsf(O.z) <= 0x1p59f;
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
         const float a = quot((k ? 1.0f : -1.0f) - O.z, D.z, yz, z_ok);
         const float rx = O.x + a * D.x, ry = O.y + a * D.y;
-        if (dz & (a > kEPS) & (__builtin_fmaf(ry, ry, rx * rx) < 1.0f) & (a < al)) { cl = k; al = a; }
+        if ((a > kEPS) & (__builtin_fmaf(ry, ry, rx * rx) < 1.0f) & (a < al)) { cl = k; al = a; }
       }
-    }
-    if (false) {
-#else
-    if (__builtin_fabsf(D.z) > kEPS) {
-#endif
-      // the caps divide by D.z (one reciprocal; numerators as in the cube test)
-      const float yz = rcp_core(D.z);
-      const bool z_ok = __builtin_fabsf(O.z) <= 0x1p59f;
-      float a = quot(-1.0f - O.z, D.z, yz, z_ok);
-#if MCPT_CYL_MASKS
-      {
-        float rx = O.x + a * D.x, ry = O.y + a * D.y;
-        if ((a > kEPS) & (__builtin_fmaf(ry, ry, rx * rx) < 1.0f) & (a < al)) { cl = 0; al = a; }
-      }
-#else
-      if (a > kEPS) {
-        float rx = O.x + a * D.x, ry = O.y + a * D.y;
-        if ((__builtin_fmaf(ry, ry, rx * rx) < 1.0f) && (a < al)) { cl = 0; al = a; }
-      }
-#endif
-      a = quot(1.0f - O.z, D.z, yz, z_ok);
-#if MCPT_CYL_MASKS
-      {
-        float rx = O.x + a * D.x, ry = O.y + a * D.y;
-        if ((a > kEPS) & (__builtin_fmaf(ry, ry, rx * rx) < 1.0f) & (a < al)) { cl = 1; al = a; }
-      }
-#else
-      if (a > kEPS) {
-        float rx = O.x + a * D.x, ry = O.y + a * D.y;
-        if ((__builtin_fmaf(ry, ry, rx * rx) < 1.0f) && (a < al)) { cl = 1; al = a; }
-      }
-#endif
     }
     float O2 = __builtin_fmaf(O.y, O.y, O.x * O.x);
     float OD = __builtin_fmaf(O.y, D.y, O.x * D.x);
@@ -610,14 +558,7 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
     if (delta4 > 0.0f) {
       const float n = -(OD + wsqrt<SR::kFastSqrt>(delta4));
       float a = quot(n, D2, rcp_core(D2), div_a_ok(n) && div_b_ok(D2));
-#if MCPT_CYL_MASKS
       if ((a > kEPS) & (a < al) & (__builtin_fabsf(O.z + a * D.z) < 1.0f)) { cl = 2; al = a; }
-#else
-      if ((a > kEPS) && (a < al)) {
-        float z = O.z + a * D.z;
-        if (__builtin_fabsf(z) < 1.0f) { cl = 2; al = a; }
-      }
-#endif
     }
     if (al < kFLTMAX) accept(CODE_CYLINDER, cl, add(O, muls(D, al)));
   } else if (t == CODE_CONE) {
@@ -754,8 +695,9 @@ __device__ __forceinline__ bool walk_run(const SR& s, f3 O, f3 D, Hit& h, Walk& 
     bool pop = true;
     bool is_leaf = w.node >= leaf0;
     bool do_leaf = is_leaf, do_node = !is_leaf;
-#if MCPT_WALK_HEAD
     if (SUSPEND) {   // wave-uniform choice of the block; the ballot taken where is_leaf is computed
+      // (computed under `leaf_batch > 0`, the compiler rebuilt the lane mask from a VGPR and
+      // chained ~18 scalar ops per iteration: C4 shape +0.7 %, profiles/r04_ab_masks.jsonl)
       const uint64_t on_leaf = __ballot(is_leaf);
       const bool leaves = leaf_batch <= 0 || __builtin_popcountll(on_leaf) >= leaf_batch ||
                           on_leaf == __builtin_amdgcn_read_exec();
@@ -764,14 +706,6 @@ __device__ __forceinline__ bool walk_run(const SR& s, f3 O, f3 D, Hit& h, Walk& 
         do_node = !leaves && !is_leaf;
       }
     }
-#else
-    if (SUSPEND && leaf_batch > 0) {   // wave-uniform choice of the block
-      const uint64_t on_leaf = __ballot(is_leaf), act = __ballot(1);
-      const bool leaves = __builtin_popcountll(on_leaf) >= leaf_batch || on_leaf == act;
-      do_leaf = leaves && is_leaf;
-      do_node = !leaves && !is_leaf;
-    }
-#endif
 #ifdef MCPT_STAMPS
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();   // wave-uniform stamps
 #endif

@@ -5,7 +5,7 @@
 # kernel-trace profile, and (full) the N>1 rehearsals: plain `bench.py --gpus N` with gloo
 # ranks sharing the one GPU (bench.py starts its own ranks).  Every GPU step has its own time
 # limit; the chain stops at the first failure.
-#   tools/gpu_check.sh TAG [full|notest|nopmc] [pmcall]
+#   tools/gpu_check.sh TAG [full|notest|nopmc|-] [pmcall|nobench]
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/${1:-run}
@@ -32,6 +32,7 @@ if [ "${3:-}" = "pmcall" ]; then   # PMC records for the C3 line's dominant poin
   python tools/pmc_summary.py $O/pmc_c1 scene1_256x256_4spp_B3 $O/pmc_records.json > /dev/null &&
   cp $O/pmc_records.json profiles/pmc_records.json || exit $?
 fi
+[ "${3:-}" = "nobench" ] && exit 0
 timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err && echo "bench ok" && cat $O/bench.json &&
 timeout -k 10 400 python bench.py --config c4 > $O/bench_c4.json 2> $O/bench_c4.err &&
 echo "bench c4 ok" && cat $O/bench_c4.json &&
