@@ -1,6 +1,7 @@
 """Host-side logic of bench.py (CPU): the self-check row choice covers every rank's shard, and
 PMC records are only used for the exact library build they were measured on."""
 import json
+import math
 import os
 import sys
 
@@ -146,11 +147,28 @@ def test_host_cpu_statement():
 
 
 def test_cpu_baseline_uses_available_cores():
-    """The CPU baseline runs one worker per CPU of the process's affinity mask (verdict r03:
-    not OMP_NUM_THREADS) and states it; a bounded C1 sample keeps this a quick CPU test."""
+    """The CPU baseline runs one worker per usable CPU: the process's affinity mask (verdict
+    r03: not OMP_NUM_THREADS), capped by the cgroup CPU quota when one is set (the GPU box
+    shows 256 CPUs under a 16-CPU quota); it states both.  A bounded C1 sample keeps this quick."""
     args = bench.parse(["--config", "c1"])
     cb = bench.cpu_baseline(args, 0.2)
-    assert cb["threads_used"] == cb["cores"] == cb["cores_available"] == len(os.sched_getaffinity(0))
+    avail, q = len(os.sched_getaffinity(0)), bench.cpu_quota()
+    want = min(avail, math.ceil(q)) if q else avail
+    assert cb["threads_used"] == cb["cores"] == bench.cpu_threads() == want
+    assert cb["cores_available"] == avail and cb["cgroup_cpu_quota"] == q
     assert cb["value"] > 0 and cb["kind"] == "port"
     c1 = bench.cpu_baseline(args, 0.2, threads=1)
     assert c1["threads_used"] == 1
+
+
+def test_cpu_threads_capped_by_quota(monkeypatch):
+    monkeypatch.setattr(bench, "cpus_available", lambda: 256)
+    monkeypatch.setattr(bench, "cpu_quota", lambda: 16.0)
+    assert bench.cpu_threads() == 16
+    monkeypatch.setattr(bench, "cpu_quota", lambda: 2.5)
+    assert bench.cpu_threads() == 3
+    monkeypatch.setattr(bench, "cpu_quota", lambda: None)
+    assert bench.cpu_threads() == 256
+    monkeypatch.setattr(bench, "cpus_available", lambda: 8)
+    monkeypatch.setattr(bench, "cpu_quota", lambda: 64.0)
+    assert bench.cpu_threads() == 8
