@@ -215,7 +215,13 @@ __device__ __forceinline__ float box_face(float al, float cd, float oa, bool dv,
 // intersect_bv raytracer_func.frag:314-352; divisions as hoisted reciprocals (contract).
 // WAVE: the all-lanes-inside early out is taken wave-uniformly (big boxes such as the
 // ground's contain every ray origin).
-template <bool WAVE>
+// FLAT (the L1/L2 kernels' per-lane walks): no exec-mask branches inside the test.  A wave
+// almost always holds lanes outside the box and lanes that reach the cull compare, so the
+// inside early-out and the cull branch only add scalar mask work; the result is the same
+// boolean.  L2 kernels: C4 shape +4.1 % (with node_tests' flat empty-child test), scenes 3 / 7
+// +2.6 / +5 %; the LDS kernels lose 6-8 % (their spill-free 72-VGPR budget), so they keep the
+// branches (profiles/r04_ab_box_flat.jsonl).
+template <bool WAVE, bool FLAT = false>
 __device__ __forceinline__ bool box_test(float4 a0, float4 a1, float4 a2, f3 O, f3 D, f3 invD, double cull2) {
   f3 c = mk(a0.x, a0.y, a0.z), w = mk(a1.x, a1.y, a1.z), iw = mk(a2.x, a2.y, a2.z);
   f3 Oi = mulv(sub(O, c), iw);
@@ -224,7 +230,8 @@ __device__ __forceinline__ bool box_test(float4 a0, float4 a1, float4 a2, f3 O, 
   const bool inside = __builtin_elementwise_maximum(__builtin_elementwise_maximum(__builtin_fabsf(Oi.x), __builtin_fabsf(Oi.y)),
                                                     __builtin_fabsf(Oi.z)) < 1.0f;
   if (WAVE && __ballot(!inside) == 0) return true;
-  if (inside) return true;
+  constexpr bool kFlat = FLAT && !WAVE;
+  if (!kFlat && inside) return true;
   f3 rD = mulv(invD, w);
   // faces in reference order: (x,-1) (x,+1) (y,-1) (y,+1) (z,-1) (z,+1), branch-free (box_face)
   const bool dx = __builtin_fabsf(Di.x) > kEPS, dy = __builtin_fabsf(Di.y) > kEPS, dz = __builtin_fabsf(Di.z) > kEPS;
@@ -235,6 +242,11 @@ __device__ __forceinline__ bool box_test(float4 a0, float4 a1, float4 a2, f3 O, 
   al = box_face(al, 1.0f, Oi.y, dy, rD.y, Oi.z, Di.z, Oi.x, Di.x);
   al = box_face(al, -1.0f, Oi.z, dz, rD.z, Oi.x, Di.x, Oi.y, Di.y);
   al = box_face(al, 1.0f, Oi.z, dz, rD.z, Oi.x, Di.x, Oi.y, Di.y);
+  if constexpr (kFlat) {
+    f3 Pg = add(mulv(add(muls(Di, al), Oi), w), c);
+    f3 v = sub(O, Pg);
+    return inside | ((al < kFLTMAX) & ((double)dot3(v, v) < cull2));
+  }
   if (al < kFLTMAX) {
     f3 Pg = add(mulv(add(muls(Di, al), Oi), w), c);
     f3 v = sub(O, Pg);
@@ -285,8 +297,13 @@ __device__ __forceinline__ void node_tests(const SR& s, const float4* __restrict
                  "v"(l2.y), "v"(l2.z));
     MCPT_ROWS_IN("v"(r0.x), "v"(r0.y), "v"(r0.z), "v"(r0.w), "v"(r1.x), "v"(r1.y), "v"(r1.z), "v"(r2.x),
                  "v"(r2.y), "v"(r2.z));
-    hl = (COUNT || l0.w != 0.0f) && box_test<false>(l0, l1, l2, O, D, invD, cull2);
-    hr = (COUNT || r0.w != 0.0f) && box_test<false>(r0, r1, r2, O, D, invD, cull2);
+    if constexpr (!COUNT) {   // flat: an empty child's test runs and is dropped (see box_test)
+      hl = (l0.w != 0.0f) & box_test<false, true>(l0, l1, l2, O, D, invD, cull2);
+      hr = (r0.w != 0.0f) & box_test<false, true>(r0, r1, r2, O, D, invD, cull2);
+    } else {
+      hl = box_test<false>(l0, l1, l2, O, D, invD, cull2);
+      hr = box_test<false>(r0, r1, r2, O, D, invD, cull2);
+    }
 #ifdef MCPT_LANESTATS
     const int sl = box_stage(l0, l1, l2, O, D, invD), sr = box_stage(r0, r1, r2, O, D, invD);
     ls_cond(LS_NE_WV, LS_NE_LN, sl >= 1); ls_cond(LS_NE_WV, LS_NE_LN, sr >= 1);
