@@ -287,7 +287,7 @@ __device__ __forceinline__ const float4* node_rows(const float4* __restrict__ no
   asm("v_lshl_add_u32 %0, %1, 1, %1" : "=v"(t) : "v"((uint32_t)j));
   return (const float4*)((const char*)nodes + (t << 4));
 }
-template <bool COUNT, class SR>
+template <bool COUNT, bool FLAT = false, class SR>
 __device__ __forceinline__ void node_tests(const SR& s, const float4* __restrict__ nodes, size_t j, f3 O, f3 D,
                                            f3 invD, double cull2, bool& hl, bool& hr) {
   if constexpr (!SR::kLds && !SR::kMesh) {
@@ -297,12 +297,12 @@ __device__ __forceinline__ void node_tests(const SR& s, const float4* __restrict
                  "v"(l2.y), "v"(l2.z));
     MCPT_ROWS_IN("v"(r0.x), "v"(r0.y), "v"(r0.z), "v"(r0.w), "v"(r1.x), "v"(r1.y), "v"(r1.z), "v"(r2.x),
                  "v"(r2.y), "v"(r2.z));
-    if constexpr (!COUNT) {   // flat: an empty child's test runs and is dropped (see box_test)
+    if constexpr (FLAT && !COUNT) {   // an empty child's test runs and is dropped (see box_test)
       hl = (l0.w != 0.0f) & box_test<false, true>(l0, l1, l2, O, D, invD, cull2);
       hr = (r0.w != 0.0f) & box_test<false, true>(r0, r1, r2, O, D, invD, cull2);
     } else {
-      hl = box_test<false>(l0, l1, l2, O, D, invD, cull2);
-      hr = box_test<false>(r0, r1, r2, O, D, invD, cull2);
+      hl = (COUNT || l0.w != 0.0f) && box_test<false>(l0, l1, l2, O, D, invD, cull2);
+      hr = (COUNT || r0.w != 0.0f) && box_test<false>(r0, r1, r2, O, D, invD, cull2);
     }
 #ifdef MCPT_LANESTATS
     const int sl = box_stage(l0, l1, l2, O, D, invD), sr = box_stage(r0, r1, r2, O, D, invD);
@@ -616,7 +616,7 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
 // exactly the reference's LIFO order (right child first, cull decided at push time).
 // ANY: just_hit_bvh (raytracer_func.frag:771-775) — stop at the first leaf whose primitive
 // produced a hit (hit_only, :756-757); the render path always uses traverse_all_bvh.
-template <bool COUNT, bool ANY = false, class SR>
+template <bool COUNT, bool ANY = false, bool FLAT = false, class SR>
 __device__ __forceinline__ void traverse_lane(const SR& s, f3 O, f3 D, Hit& h, Ev<COUNT>& ev) {
   ev.inc(EV_TRAV);
   h.clear(); h.dist = kFLTMAX; h.cull2 = cull_bound_sq(kFLTMAX);
@@ -645,7 +645,7 @@ __device__ __forceinline__ void traverse_lane(const SR& s, f3 O, f3 D, Hit& h, E
       ev.inc(EV_NODE);
       const size_t j = 2 * (size_t)node + 1;
       bool hl, hr;
-      node_tests<COUNT>(s, s.nodes, j, O, D, invD, h.cull2, hl, hr);
+      node_tests<COUNT, FLAT>(s, s.nodes, j, O, D, invD, h.cull2, hl, hr);
       pop = !(hl || hr);
       if (hr) {
         if (hl) pending |= 1u << (level + 1);
@@ -703,6 +703,11 @@ __device__ __forceinline__ void walk_begin(const SR& s, f3 D, Hit& h, Walk& w, E
 template <bool COUNT, bool SUSPEND, class SR>
 __device__ __forceinline__ bool walk_run(const SR& s, f3 O, f3 D, Hit& h, Walk& w, Ev<COUNT>& ev, int exit,
                                          int leaf_batch, int min_done = 1) {
+  // the suspendable L1/L2 walk (the deep-BVH kernel) runs its box tests and its push / pop
+  // without exec-mask branches (box_test FLAT): C4 shape +4.1 % and +2.5 %; the LDS, mesh and
+  // non-suspending kernels lose with it (-6..11 %: profiles/r04_ab_box_flat.jsonl,
+  // r04_ab_walk_flat.jsonl), so they keep the branches
+  constexpr bool kFlat = SUSPEND && !SR::kLds && !SR::kMesh;
   const int leaf0 = (1 << s.depth) - 1;
   const int n0 = SUSPEND ? __builtin_popcountll(__ballot(1)) : 0;
 #ifdef MCPT_LANESTATS
@@ -774,16 +779,33 @@ __device__ __forceinline__ bool walk_run(const SR& s, f3 O, f3 D, Hit& h, Walk& 
       ev.inc(EV_NODE);
       const size_t j = 2 * (size_t)w.node + 1;
       bool hl, hr;
-      node_tests<COUNT>(s, s.nodes, j, O, D, w.invD, h.cull2, hl, hr);
-      pop = !(hl || hr);
-      if (hr) {
-        if (hl) w.pending |= 1u << (w.level + 1);
-        w.node = (int)j + 1; w.level++;
-      } else if (hl) {
-        w.node = (int)j; w.level++;
+      node_tests<COUNT, kFlat>(s, s.nodes, j, O, D, w.invD, h.cull2, hl, hr);
+      if constexpr (kFlat) {   // the push as selects instead of exec-mask branches
+        const bool any = hl | hr;
+        w.pending |= (hl & hr) ? 1u << (w.level + 1) : 0u;
+        w.node = any ? (int)j + (hr ? 1 : 0) : w.node;
+        w.level += any ? 1 : 0;
+        pop = !any;
+      } else {
+        pop = !(hl || hr);
+        if (hr) {
+          if (hl) w.pending |= 1u << (w.level + 1);
+          w.node = (int)j + 1; w.level++;
+        } else if (hl) {
+          w.node = (int)j; w.level++;
+        }
       }
     }
-    if (pop && (do_leaf || do_node)) {
+    if constexpr (kFlat) {   // the pop as selects; only the walk's end leaves the loop per lane
+      if (pop & (do_leaf | do_node)) {
+        if (w.pending == 0) return true;
+      }
+      const bool p2 = pop & (do_leaf | do_node);
+      const int L = 31 - __builtin_clz(w.pending | 1u);
+      w.pending = p2 ? w.pending & ~(1u << L) : w.pending;
+      w.node = p2 ? ((w.node + 1) >> (w.level - L)) - 2 : w.node;
+      w.level = p2 ? L : w.level;
+    } else if (pop && (do_leaf || do_node)) {
       if (w.pending == 0) return true;
       int L = 31 - __builtin_clz(w.pending);
       w.pending &= ~(1u << L);
@@ -966,10 +988,11 @@ __device__ __forceinline__ void traverse_wave(const SR& s, f3 O, f3 D, Hit& h, E
   }
 }
 
-template <bool COUNT, bool WAVE, class SR>
+// FLAT: the box tests without exec-mask branches (box_test), as the walk of the same kernel
+template <bool COUNT, bool WAVE, bool FLAT = false, class SR>
 __device__ __forceinline__ void traverse(const SR& s, f3 O, f3 D, Hit& h, Ev<COUNT>& ev) {
   if (WAVE) traverse_wave<COUNT>(s, O, D, h, ev);
-  else traverse_lane<COUNT>(s, O, D, h, ev);
+  else traverse_lane<COUNT, false, FLAT>(s, O, D, h, ev);
 }
 
 // intersection_info raytracer_func.frag:812-897 (hit only; misses leave N,P untouched)

@@ -177,7 +177,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
   unsigned long long st_k0 = __builtin_amdgcn_s_memtime(), st_t = 0, st_s = 0, st_it = 0;
 #endif
   if (!COUNT && run) {
-    traverse<COUNT, WAVE>(s, Ocam, Dcam0, h, ev);
+    traverse<COUNT, WAVE, SUSPEND && !LDSS && !MESH>(s, Ocam, Dcam0, h, ev);
     key0 = hit_key(h);
     if (h.hit()) geom_info<COUNT>(s, h, N0, P0, ev);
   }
