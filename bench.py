@@ -96,7 +96,15 @@ CONFIGS = {   # BASELINE.json configs[0..4]
     "c4": dict(scene=8, width=1920, height=1080, spp=512, bounces=12, ior=1.0, scaling="strong"),
     "c5": dict(scene=6, width=3840, height=2160, spp=1024, bounces=8, ior=1.0, scaling="strong",
                target_spp=C5_TARGET_SPP),
+    # the HBM-roofline workload (verdict r04 #1; SURVEY §8f row 2, "the only route to HBM-sized
+    # scenes"): two instances of a 1 M-triangle UV sphere (mesh BVH depth 20, 2^21 - 1 mesh nodes,
+    # ~130 MB of device mesh records), 1080p, B 8 (mcpt.meshes.big_mesh_scene)
+    "mesh": dict(scene="mesh", width=1920, height=1080, spp=64, bounces=8, ior=1.0, scaling="strong",
+                 mesh_tris=1_000_000),
 }
+# the phases a rank stamps on stderr, in order (the launcher names the rank that stalls, and where)
+PHASES = ("start", "init", "upload", "auto", "warmup", "timed", "stats", "count", "self_check", "cpu_baseline",
+          "done")
 
 
 def parse(argv=None):
@@ -112,11 +120,32 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-count", action="store_true", help="skip the reference-byte counting launch")
     ap.add_argument("--no-check", action="store_true", help="skip rank 0's post-run self check")
+    ap.add_argument("--scaling", choices=("weak", "strong"), default=None,
+                    help="c2/c3: weak (default: one C2 frame of samples per GPU) or strong (one fixed frame "
+                         "split over the N GPUs)")
+    ap.add_argument("--deadline", type=float, default=480.0,
+                    help="wall-clock limit (s) of every rank (and of the launcher, +15 s): a rank past it names "
+                         "its phase on stderr and exits 124")
+    ap.add_argument("--drill-stall", default=None, metavar="RANK:PHASE[:SECONDS]",
+                    help="launcher drill (CPU only, MCPT_DIST_BACKEND=gloo): the ranks walk the phases with "
+                         "gloo barriers and no GPU work; RANK sleeps SECONDS (default 3600) before PHASE")
     a = ap.parse_args(argv)
     if a.gpus < 1:
         ap.error("--gpus must be >= 1")
+    scaling = a.scaling
     for k, v in CONFIGS[a.config].items():
         setattr(a, k, v)
+    if scaling is not None:
+        if a.config not in ("c2", "c3"):
+            ap.error("--scaling applies to --config c2 / c3 (c1 is weak, c4 / c5 / mesh are strong)")
+        a.scaling = scaling
+    if not hasattr(a, "mesh_tris"):
+        a.mesh_tris = 0
+    if a.drill_stall is not None:
+        parts = a.drill_stall.split(":")
+        if len(parts) not in (2, 3) or parts[1] not in PHASES:
+            ap.error(f"--drill-stall RANK:PHASE[:SECONDS], PHASE one of {PHASES}")
+        a.drill_stall = (int(parts[0]), parts[1], float(parts[2]) if len(parts) == 3 else 3600.0)
     if not hasattr(a, "target_spp"):
         a.target_spp = None
     if a.config == "c3":
@@ -144,15 +173,68 @@ def rank_env(base: dict, rank: int, world: int, port: int) -> dict:
     return env
 
 
-def spawn_ranks(cmd, world: int, base_env=None, poll_s: float = 0.2, grace_s: float = 10.0):
+PHASE_TAG = "bench-phase"
+
+
+def stamp(rank: int, phase: str, t0: float) -> None:
+    """One phase stamp on stderr: `bench-phase rank=R phase=P t=S` (S = seconds since the rank
+    started).  The launcher keeps each rank's last stamp to name the rank and phase that stall."""
+    print(f"{PHASE_TAG} rank={rank} phase={phase} t={time.time() - t0:.2f}", file=sys.stderr, flush=True)
+
+
+def parse_stamp(line: str):
+    """(rank, phase) of a phase-stamp line, else None."""
+    if not line.startswith(PHASE_TAG):
+        return None
+    kv = dict(f.split("=", 1) for f in line.split()[1:] if "=" in f)
+    try:
+        return int(kv["rank"]), kv["phase"]
+    except (KeyError, ValueError):
+        return None
+
+
+def stall_report(last: dict, alive: set, world: int) -> str:
+    """Which rank stalled in which phase: every rank's last stamp, and the rank(s) least advanced
+    in PHASES (a rank blocked in a collective waits for the least advanced one; a rank that
+    failed early is the least advanced too)."""
+    order = {p: i for i, p in enumerate(PHASES)}
+    parts = []
+    for r in range(world):
+        ph, t = last.get(r, ("(none)", None))
+        state = "running" if r in alive else "exited"
+        parts.append(f"rank {r} {state}, last phase {ph}" + (f" ({time.time() - t:.1f} s ago)" if t else ""))
+    idx = {r: order.get(last.get(r, ("", 0))[0], -1) for r in range(world)}
+    lo = min(idx.values())
+    slow = [r for r in range(world) if idx[r] == lo]
+    nxt = PHASES[lo + 1] if lo + 1 < len(PHASES) else "-"
+    return ("; ".join(parts) + f". Stalled: rank(s) {', '.join(map(str, slow))} in phase "
+            f"{PHASES[lo] if lo >= 0 else '(no stamp yet)'} (next: {nxt})")
+
+
+def spawn_ranks(cmd, world: int, base_env=None, poll_s: float = 0.2, grace_s: float = 10.0,
+                deadline_s: float = None):
     """Run `cmd` as `world` child processes (rank r gets RANK/LOCAL_RANK = r, WORLD_SIZE = world,
     MASTER_ADDR 127.0.0.1 and a free port).  Rank 0's stdout is captured; the others' stdout
-    and every stderr pass through.  As soon as one rank exits non-zero the others are stopped
-    (SIGTERM, then SIGKILL after `grace_s`), since they would block in a collective.
-    Returns (exit status: 0, or the first failing rank's non-zero status; rank 0's stdout)."""
+    passes through; every rank's stderr is relayed line by line, and its phase stamps kept.
+    As soon as one rank exits non-zero the others are stopped (SIGTERM, then SIGKILL after
+    `grace_s`), since they would block in a collective; so are all of them once `deadline_s`
+    passes (status 124).  Either way the stderr report names each rank's last phase and the
+    rank that stalled.  Returns (exit status: 0, the first failing rank's non-zero status or 124;
+    rank 0's stdout)."""
     base = dict(os.environ if base_env is None else base_env)
     port = free_port()
-    procs, out0 = [], []
+    procs, out0, readers = [], [], []
+    last = {}   # rank -> (phase, time of its stamp)
+    lock = threading.Lock()
+
+    def relay(r, pipe):
+        for ln in pipe:
+            st = parse_stamp(ln)
+            if st is not None:
+                with lock:
+                    last[st[0]] = (st[1], time.time())
+            sys.stderr.write(ln)
+            sys.stderr.flush()
 
     def stop_all():
         for p in procs:
@@ -171,25 +253,39 @@ def spawn_ranks(cmd, world: int, base_env=None, poll_s: float = 0.2, grace_s: fl
         sys.exit(128 + signum)
 
     old = signal.signal(signal.SIGTERM, on_term) if threading.current_thread() is threading.main_thread() else None
+    t_start = time.time()
     try:
         for r in range(world):
             procs.append(subprocess.Popen(cmd, env=rank_env(base, r, world, port),
-                                          stdout=subprocess.PIPE if r == 0 else None, text=True))
+                                          stdout=subprocess.PIPE if r == 0 else None,
+                                          stderr=subprocess.PIPE, text=True))
+            th = threading.Thread(target=relay, args=(r, procs[-1].stderr), daemon=True)
+            th.start()
+            readers.append(th)
         reader = threading.Thread(target=lambda: out0.append(procs[0].stdout.read()), daemon=True)
         reader.start()
-        status = 0
+        status, why = 0, None
         while True:
             codes = [p.poll() for p in procs]
-            bad = [c for c in codes if c not in (None, 0)]
+            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
             if bad:
-                status = bad[0]
+                status, why = bad[0][1], f"rank {bad[0][0]} exited with status {bad[0][1]}"
                 break
             if all(c == 0 for c in codes):
                 break
+            if deadline_s is not None and time.time() - t_start > deadline_s:
+                status, why = 124, f"deadline of {deadline_s:g} s passed"
+                break
             time.sleep(poll_s)
         if status:
+            alive = {r for r, p in enumerate(procs) if p.poll() is None}
+            with lock:
+                rep = stall_report(last, alive, world)
+            print(f"bench: {why}: {rep}", file=sys.stderr, flush=True)
             stop_all()
         reader.join(timeout=grace_s)
+        for th in readers:
+            th.join(timeout=grace_s)
     finally:
         if old is not None:
             signal.signal(signal.SIGTERM, old)
@@ -214,7 +310,9 @@ def launch(args) -> int:
     children are fresh processes, and this process only waits and relays rank 0's line."""
     cmd = [sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:]
     print(f"bench: starting {args.gpus} ranks (one process per GPU)", file=sys.stderr, flush=True)
-    status, out = spawn_ranks(cmd, args.gpus)
+    # the ranks stop themselves at --deadline (naming their phase); the launcher's own limit is a
+    # little later, for a rank that cannot
+    status, out = spawn_ranks(cmd, args.gpus, deadline_s=args.deadline + 15.0)
     if status:
         print(f"bench: a rank failed (exit {status}); no result", file=sys.stderr, flush=True)
         return status if status > 0 else 1
@@ -242,7 +340,8 @@ def check_world(gpus: int, world: int, backend: str, n_devices: int, local_world
 # workload
 # ------------------------------------------------------------------------------------------
 def workload_key(args, passes_per_step: int, rough=None) -> str:
-    k = f"scene{args.scene}_{args.width}x{args.height}_{passes_per_step}spp_B{args.bounces}"
+    scene = f"mesh{args.mesh_tris // 1000}k" if args.scene == "mesh" else f"scene{args.scene}"
+    k = f"{scene}_{args.width}x{args.height}_{passes_per_step}spp_B{args.bounces}"
     if getattr(args, "ior", 1.0) != 1.0:
         k += f"_ior{args.ior:g}"
     if rough is not None:
@@ -251,7 +350,11 @@ def workload_key(args, passes_per_step: int, rough=None) -> str:
 
 
 def build_scene(args, rough=None) -> "mcpt.Scene":
-    """The reference scene; for a C3 point, every non-emissive primitive's roughness = rough."""
+    """The reference scene (or the HBM-sized mesh scene); for a C3 point, every non-emissive
+    primitive's roughness = rough."""
+    if args.scene == "mesh":
+        from mcpt import meshes
+        return meshes.big_mesh_scene(args.mesh_tris)[0]
     sc = mcpt.Scene.reference(args.scene, args.light)
     if rough is not None:
         prims, _, _ = sc.buffers()
@@ -321,16 +424,19 @@ def cpu_threads() -> int:
     return max(1, min(avail, math.ceil(quota))) if quota else avail
 
 
-def cpu_baseline(args, seconds: float, rough=None, threads=None):
+def cpu_baseline_run(args, seconds: float, rough=None, threads=None, scene=None):
     """Oracle (C++ restatement, same arithmetic) on a bounded sample of the workload: every
     2nd row of the frame (every row for C1), 1-pass launches of increasing pass number
-    (1..spp) until the budget is spent (≈10 s), std::thread over rows on `threads` workers
-    (default: every CPU of the process's affinity mask, verdict r03)."""
+    (1..spp) until the budget is spent, std::thread over rows on `threads` workers."""
     from oracle import oracle as orc
-    avail = cpus_available()
-    threads = threads or avail
     nproc, model = host_cpu()
-    prims, nodes, leaves, depth, _ = orc.scene(args.scene, args.light)
+    mv = None
+    if args.scene == "mesh":   # the mesh workload: its buffers from the scene producer, oracle mesh walk
+        prims, nodes, leaves = scene.buffers()
+        depth = scene.depth()
+        mv = orc.MeshView(scene.mesh_buffers())
+    else:
+        prims, nodes, leaves, depth, _ = orc.scene(args.scene, args.light)
     if rough is not None:   # build_scene's override: material .y of every non-emissive record
         prims = np.array(prims, copy=True)
         prims[~(prims[:, 58] > 0), 57] = rough
@@ -342,24 +448,48 @@ def cpu_baseline(args, seconds: float, rough=None, threads=None):
     samples, t0, p = 0, time.perf_counter(), 1
     while True:
         orc.render(prims, nodes, leaves, depth, ipv, iv, W, H, p, 1, 0.0, args.bounces, args.ior, 0,
-                   row_step=row_step, row_offset=0, n_threads=threads, accum=acc)
+                   row_step=row_step, row_offset=0, n_threads=threads, accum=acc, meshes=mv)
         samples += rows * W
         p += 1
         dt = time.perf_counter() - t0
         if dt >= seconds or p > args.spp:
             break
-    return {"value": round(samples / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "threads_used": threads, "cores_available": avail, "cgroup_cpu_quota": cpu_quota(),
-            "host_logical_cpus": nproc, "cpu_model": model,
-            "threads_note": "std::thread workers over rows; cores_available = the process's CPU affinity "
-                            "(os.sched_getaffinity), cgroup_cpu_quota = cpu.max quota/period if one is set "
-                            "(a quota below the affinity count makes the workers share that many CPUs' time: "
-                            "at_quota_threads, when present, is the figure at the quota's core count)",
-            "sample": f"oracle/oracle.cpp, scene {args.scene} {W}x{H} "
+    scene_name = "the mesh workload (mcpt.meshes.big_mesh_scene)" if args.scene == "mesh" else f"scene {args.scene}"
+    return {"value": round(samples / dt / 1e6, 4), "threads": threads,
+            "sample": f"oracle/oracle.cpp, {scene_name} {W}x{H} "
                       f"{'every row' if row_step == 1 else f'every {row_step}nd row'} ({rows} rows), "
                       f"passes 1..{p - 1} ({samples} samples, {dt:.3g} s), B={args.bounces}, IOR {args.ior:g}"
                       + (f", roughness {rough:g}" if rough is not None else "")
-                      + ("" if row_step == 1 and p > args.spp else "; extrapolated rate, not the whole config")}
+                      + ("" if row_step == 1 and p > args.spp else "; extrapolated rate, not the whole config"),
+            "nproc": nproc, "model": model}
+
+
+def cpu_baseline(args, seconds: float, rough=None, scene=None):
+    """The CPU figure of the line: the oracle run with one worker per CPU of the process's
+    affinity mask and, when the cgroup's CPU quota grants fewer CPUs' time than that (the GPU
+    box: 256 CPUs visible, 16 granted), again with one worker per granted CPU; `value` is the
+    faster run and `cores` its thread count, the other run beside it (verdict / advisor r04)."""
+    avail, quota = cpus_available(), cpu_quota()
+    counts = [avail]
+    nq = cpu_threads()
+    if nq != avail:
+        counts.append(nq)
+    share = seconds / len(counts)
+    runs = [cpu_baseline_run(args, share, rough, threads=n, scene=scene) for n in counts]
+    best = max(runs, key=lambda r: r["value"])
+    others = [r for r in runs if r is not best]
+    return {"value": best["value"], "unit": "Msamples/s", "cores": best["threads"], "kind": "port",
+            "threads_used": best["threads"], "cores_available": avail, "cgroup_cpu_quota": quota,
+            "host_logical_cpus": best["nproc"], "cpu_model": best["model"], "sample": best["sample"],
+            "other_runs": [{"threads": r["threads"], "value": r["value"], "sample": r["sample"]} for r in others],
+            "threads_note": ("std::thread workers over rows. Run with one worker per CPU of the affinity mask "
+                             "(os.sched_getaffinity) and, when the cgroup quota (cpu.max quota/period) grants "
+                             "fewer CPUs' time, with one per granted CPU; value = the faster run, cores = its "
+                             "thread count, the other under other_runs"),
+            "algorithm_note": ("Same integrator and arithmetic as the GPU path, with one difference in work: the "
+                               "GPU traverses each pixel's camera ray once per 32-pass segment and reuses the primary hit "
+                               "(exact: raytracer.vert has no jitter and the walk draws no random number); the CPU "
+                               "port, like the reference's shader, re-traverses it every pass")}
 
 
 def check_rows(H: int, band_rows: int, world: int):
@@ -395,53 +525,71 @@ def self_check(args, scene, ipv, iv, frame: torch.Tensor, n_calls: int, S: int, 
 
 
 def roofline(workload: str, sha: str, avg_trace_ms: float, ref_bytes: float, bytes_per_sample: float, world: int,
-             launches: int = 1):
+             launches: int = 1, bound: str = "valu"):
     """`avg_trace_ms` is one timed call's kernel time, summed over its `launches` sub-launches; a
-    PMC record is used only if it sums the same number of launches."""
+    PMC record is used only if it sums the same number of launches.
+    bound "valu" (the LDS/L2-resident reference scenes): achieved = VALU lane-instructions / s
+    from the same-build PMC record, against the issue peak; the HBM side under `hbm`.
+    bound "hbm" (the mesh workload, whose records stream from HBM / the Infinity Cache):
+    achieved = the SURVEY §8d algorithmic bytes of one launch (counting build) / its time,
+    against 8 TB/s; `traffic` = the PMC fabric bytes of one launch, `traffic_ratio` = traffic /
+    algorithmic (> 1: re-reads); the VALU side under `valu`."""
     rec = pmc_record(workload, sha) if world == 1 else None
     if rec is not None and int(rec.get("launches_summed", 1)) != int(launches):
         rec = None
     t_s = avg_trace_ms / 1e3
-    roof = {"bound": "valu", "achieved": None, "peak": VALU_PEAK_T, "unit": "T lane-instr/s", "frac": None,
-            "lane_utilisation": None, "useful_frac": None, "traffic": None,
-            "hbm": {"achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None},
-            "kernel_ms": round(avg_trace_ms, 3), "launches_per_call": launches,
-            "pmc": {"workload": workload, "lib_sha256": sha, "matched": rec is not None,
-                    "source": rec.get("source") if rec else None,
-                    "note": None if rec else ("no rocprofv3 PMC record of this workload for this libmcpt.so "
-                                              "build (summing this call's launches) in profiles/pmc_records.json: "
-                                              "PMC fields left null"
-                                              if world == 1 else "PMC records are single-GPU measurements")}}
+    valu = {"achieved": None, "peak": VALU_PEAK_T, "unit": "T lane-instr/s", "frac": None,
+            "lane_utilisation": None, "useful_frac": None}
+    hbm = {"achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None}
+    traffic = None
     if rec is not None and t_s > 0:
         c = rec["counters_per_launch"]
         ach = c["SQ_INSTS_VALU"] * 64 / t_s / 1e12
-        roof["achieved"] = round(ach, 3)
-        roof["frac"] = round(ach / VALU_PEAK_T, 4)
+        valu.update(achieved=round(ach, 3), frac=round(ach / VALU_PEAK_T, 4), valu_instructions_per_launch=c["SQ_INSTS_VALU"])
         lu = rec.get("valu_lane_utilisation")
         if lu is not None:
-            roof["lane_utilisation"] = round(lu, 4)
-            roof["useful_frac"] = round(ach / VALU_PEAK_T * lu, 4)
-        roof["valu_instructions_per_launch"] = c["SQ_INSTS_VALU"]
+            valu.update(lane_utilisation=round(lu, 4), useful_frac=round(ach / VALU_PEAK_T * lu, 4))
         traffic = rec.get("hbm_bytes_per_launch")
-        roof["traffic"] = traffic
         if traffic is not None:
             gbs = traffic / t_s / 1e9
-            roof["hbm"].update(achieved=round(gbs, 2), frac=round(gbs / HBM_PEAK_GBS, 5))
-        if rec.get("wave_cycle_split"):
-            roof["wave_cycle_split"] = {k: round(v, 4) for k, v in rec["wave_cycle_split"].items()}
-    roof["reference_equivalent_bytes"] = {
-        "per_launch": ref_bytes, "per_sample": round(float(bytes_per_sample), 2),
-        "rate_GBs": round(ref_bytes / t_s / 1e9, 1) if t_s > 0 else None,
-        "note": ("SURVEY §8d texel-fetch model: the bytes the reference's shader would fetch for the "
-                 "same work (event counts of the counting build). Scene records are served from "
-                 "LDS/L1/L2 here, so this is NOT HBM traffic and is never divided by the HBM peak")}
+            hbm.update(achieved=round(gbs, 2), frac=round(gbs / HBM_PEAK_GBS, 5))
+    pmc = {"workload": workload, "lib_sha256": sha, "matched": rec is not None,
+           "source": rec.get("source") if rec else None,
+           "note": None if rec else ("no rocprofv3 PMC record of this workload for this libmcpt.so "
+                                     "build (summing this call's launches) in profiles/pmc_records.json: "
+                                     "PMC fields left null"
+                                     if world == 1 else "PMC records are single-GPU measurements")}
+    refb = {"per_launch": ref_bytes, "per_sample": round(float(bytes_per_sample), 2),
+            "rate_GBs": round(ref_bytes / t_s / 1e9, 1) if t_s > 0 else None}
+    if bound == "hbm":
+        ach = ref_bytes / t_s / 1e9 if t_s > 0 and ref_bytes > 0 else None
+        roof = {"bound": "hbm", "achieved": None if ach is None else round(ach, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": None if ach is None else round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "traffic_ratio": round(traffic / ref_bytes, 3) if traffic and ref_bytes > 0 else None,
+                "traffic_GBs": hbm["achieved"], "kernel_ms": round(avg_trace_ms, 3), "launches_per_call": launches,
+                "valu": valu, "pmc": pmc}
+        refb["note"] = ("SURVEY §8d texel-fetch model (incl. the mesh events), counted exactly by the counting "
+                        "build of the same kernel: the algorithmic bytes of `achieved`")
+    else:
+        roof = dict(bound="valu", **{k: valu[k] for k in ("achieved", "peak", "unit", "frac", "lane_utilisation",
+                                                           "useful_frac")})
+        if "valu_instructions_per_launch" in valu:
+            roof["valu_instructions_per_launch"] = valu["valu_instructions_per_launch"]
+        roof.update(traffic=traffic, hbm=hbm, kernel_ms=round(avg_trace_ms, 3), launches_per_call=launches, pmc=pmc)
+        refb["note"] = ("SURVEY §8d texel-fetch model: the bytes the reference's shader would fetch for the "
+                        "same work (event counts of the counting build). Scene records are served from "
+                        "LDS/L1/L2 here, so this is NOT HBM traffic and is never divided by the HBM peak")
+    if rec is not None and rec.get("wave_cycle_split"):
+        roof["wave_cycle_split"] = {k: round(v, 4) for k, v in rec["wave_cycle_split"].items()}
+    roof["reference_equivalent_bytes"] = refb
     return roof
 
 
-def run_point(args, sr, rough, S, world, barrier, stat_dev):
+def run_point(args, sr, rough, S, world, barrier, stat_dev, wd):
     """Upload the point's scene, AUTO trials, warm-up, K timed steps (render + gather), the
     counting launch and rank 0's self check.  Returns this rank's figures."""
     W, H, B = args.width, args.height, args.bounces
+    wd.enter("upload")
     scene = build_scene(args, rough)
     sr.upload_scene(scene)
     ipv, iv = mcpt.camera_canonical(W, H)
@@ -449,14 +597,17 @@ def run_point(args, sr, rough, S, world, barrier, stat_dev):
     # AUTO times its candidate schedules (per-lane / wave-coherent walk, two or four pass
     # segments per work item) on the first sizeable launches of a scene: run those before the
     # warm-up so that every warm-up and timed step uses the pick
+    wd.enter("auto")
     for _ in range(mcpt.AUTO_TRIALS):
         sr.render(ipv, iv, 1, S, 0.0, B, args.ior, mcpt.MONTECARLO)
     sr.r.clear_accum()
     frame = None
+    wd.enter("warmup")
     for k in range(args.warmup):
         sr.render(ipv, iv, k * S + 1, S, 0.0, B, args.ior, mcpt.MONTECARLO)
         frame = sr.gather()
     barrier()
+    wd.enter("timed")
     kernel_ms, gather_ev = [], []
     # the library keeps the HIP events of its last TIMING_RING render calls: the steps are
     # queued back to back and their kernel times read once per half ring (one wait per 32
@@ -477,6 +628,7 @@ def run_point(args, sr, rough, S, world, barrier, stat_dev):
     barrier()
     kernel_ms.extend(sr.r.kernel_ms_back(b) for b in reversed(range(args.steps % half)))
     elapsed = time.perf_counter() - t0
+    wd.enter("stats")
     sched = sr.r.schedule()   # what AUTO picked for this rank's timed launches
     launches = sr.r.last_launch_count()   # sub-launches of one timed call (segment-sum budget)
     t = torch.tensor([elapsed], dtype=torch.float64, device=stat_dev)
@@ -487,6 +639,7 @@ def run_point(args, sr, rough, S, world, barrier, stat_dev):
 
     # reference-equivalent bytes of one launch: the counting build over the first timed pass range
     ev_local = np.zeros(len(mcpt.EVENT_NAMES), np.uint64)
+    wd.enter("count")
     if not args.no_count:
         ev_local = sr.r.render_counted(ipv, iv, args.warmup * S + 1, S, 0.0, B, args.ior, mcpt.MONTECARLO)
     bytes_local = float((ev_local.astype(np.float64) * mcpt.Renderer.event_bytes()).sum())
@@ -503,10 +656,70 @@ def run_point(args, sr, rough, S, world, barrier, stat_dev):
     else:
         allstats = stats.cpu().numpy()[None]
     check = None
+    wd.enter("self_check")
     if args.rank == 0 and not args.no_check:
         check = self_check(args, scene, ipv, iv, frame, args.warmup + args.steps, S, args.local_rank)
     return dict(rough=rough, elapsed=elapsed, sched=sched, launches=launches, gather_ms=gather_ms, avg_trace_ms=avg_trace_ms,
-                avg_combine_ms=avg_combine_ms, allstats=allstats, check=check)
+                avg_combine_ms=avg_combine_ms, allstats=allstats, check=check, scene=scene)
+
+
+class Watchdog:
+    """A rank's phase stamps and its own deadline: past `deadline_s` the rank prints the phase it
+    is in (and since when) to stderr and exits 124 — also when a launcher other than ours
+    (torch.distributed.run) started it, which then stops the other ranks."""
+
+    def __init__(self, rank: int, deadline_s: float):
+        self.rank, self.deadline = rank, deadline_s
+        self.t0 = time.time()
+        self.phase, self.t_phase = "start", self.t0
+        stamp(rank, "start", self.t0)
+        threading.Thread(target=self._run, daemon=True).start()
+
+    def enter(self, phase: str) -> None:
+        self.phase, self.t_phase = phase, time.time()
+        stamp(self.rank, phase, self.t0)
+
+    def _run(self) -> None:
+        while True:
+            left = self.t0 + self.deadline - time.time()
+            if left <= 0:
+                break
+            time.sleep(min(left, 1.0))
+        if self.phase == "done":
+            return
+        print(f"bench rank {self.rank}: deadline {self.deadline:g} s reached in phase {self.phase} (entered "
+              f"{time.time() - self.t_phase:.1f} s ago, t={time.time() - self.t0:.1f} s); exiting",
+              file=sys.stderr, flush=True)
+        os._exit(124)
+
+
+def init_group(backend: str, local_rank: int, deadline_s: float) -> None:
+    """The process group, with a timeout bounded by the deadline (RCCL init and collectives
+    fail instead of hanging; gloo likewise)."""
+    import datetime
+    to = datetime.timedelta(seconds=max(10.0, min(300.0, deadline_s)))
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank), timeout=to)
+    else:
+        dist.init_process_group(backend, timeout=to)
+
+
+def drill(args, world: int, rank: int, wd: Watchdog) -> None:
+    """`--drill-stall`: the launcher's deadline and stall report on CPU.  The ranks walk PHASES
+    with a gloo barrier per phase and no GPU work; rank R sleeps before phase P."""
+    stall_rank, stall_phase, stall_s = args.drill_stall
+    for ph in PHASES[1:-1]:
+        if rank == stall_rank and ph == stall_phase:
+            time.sleep(stall_s)
+        wd.enter(ph)
+        if ph == "init":
+            init_group("gloo", 0, args.deadline)
+        elif world > 1 and ph not in ("cpu_baseline",):
+            dist.barrier()
+    wd.enter("done")
+    if rank == 0:
+        print(json.dumps({"metric": "drill", "n_gpus": world, "drill": True, "phases": list(PHASES)}), flush=True)
+    dist.destroy_process_group()
 
 
 def main():
@@ -518,6 +731,13 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
     backend = os.environ.get("MCPT_DIST_BACKEND", "nccl")   # "gloo": N>1 rehearsal sharing GPUs
+    wd = Watchdog(rank, args.deadline)
+    if args.drill_stall is not None:
+        if backend != "gloo":
+            print("bench: --drill-stall needs MCPT_DIST_BACKEND=gloo", file=sys.stderr, flush=True)
+            sys.exit(2)
+        drill(args, world, rank, wd)
+        return
     n_dev = torch.cuda.device_count()
     why = check_world(args.gpus, world, backend, n_dev, local_world)
     if why:
@@ -528,18 +748,17 @@ def main():
         local_rank = local_rank % n_dev   # ranks may share a GPU
     args.world, args.rank, args.local_rank = world, rank, local_rank
     torch.cuda.set_device(local_rank)
+    wd.enter("init")
     if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        else:
-            dist.init_process_group(backend)
+        init_group(backend, local_rank, args.deadline)
         if dist.get_world_size() != args.gpus:
             print(f"bench rank {rank}: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}",
                   file=sys.stderr, flush=True)
             sys.exit(3)
 
     W, H, B = args.width, args.height, args.bounces
-    # passes per step: weak (C2/C3) = one frame of samples per GPU; strong (C4/C5) = one frame in total
+    # passes per step: weak (C2/C3 default) = one frame of samples per GPU; strong (C4/C5/mesh,
+    # or --scaling strong) = one frame in total
     S = args.spp * world if args.scaling == "weak" else args.spp
     sr = ShardedRenderer(W, H, args.band_rows, world, rank, local_rank)
     stat_dev = sr.device if backend == "nccl" else torch.device("cpu")
@@ -549,7 +768,7 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    points = [run_point(args, sr, rough, S, world, barrier, stat_dev) for rough in args.rough_points]
+    points = [run_point(args, sr, rough, S, world, barrier, stat_dev, wd) for rough in args.rough_points]
 
     if rank == 0:
         sha = lib_sha256()
@@ -561,7 +780,8 @@ def main():
         for pt in points:
             a = pt["allstats"]
             pt["roof"] = roofline(workload_key(args, S, pt["rough"]), sha, pt["avg_trace_ms"], float(a[0, 0]),
-                                  float(a[:, 0].sum() / max(a[:, 3].sum(), 1.0)), world, pt["launches"])
+                                  float(a[:, 0].sum() / max(a[:, 3].sum(), 1.0)), world, pt["launches"],
+                                  bound="hbm" if args.scene == "mesh" else "valu")
         config = {
             "workload": workload_key(args, S, main_pt["rough"] if len(points) == 1 else None)
                         + ("_rough-sweep" if len(points) > 1 else ""),
@@ -626,19 +846,8 @@ def main():
                             "points": len(checks)}),
         }
         if not args.no_cpu_baseline and world == 1:
-            # one worker per CPU of the affinity mask (verdict r03); beside it, on shorter
-            # samples, the figure at the cgroup quota's core count when a quota caps the mask
-            # (the GPU box: 256 CPUs visible, 16 granted, where 16 workers run faster than 256)
-            # and the 16-thread figure of rounds 1-3
-            cb = cpu_baseline(args, args.cpu_seconds, main_pt["rough"])
-            nq = cpu_threads()
-            if nq < cb["threads_used"] and nq != 16:
-                cq = cpu_baseline(args, args.cpu_seconds / 2, main_pt["rough"], threads=nq)
-                cb["at_quota_threads"] = {k: cq[k] for k in ("value", "threads_used", "sample")}
-            if cb["threads_used"] != 16:
-                c16 = cpu_baseline(args, args.cpu_seconds / 2, main_pt["rough"], threads=16)
-                cb["at_16_threads"] = {k: c16[k] for k in ("value", "threads_used", "sample")}
-            out["cpu_baseline"] = cb
+            wd.enter("cpu_baseline")
+            out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds, main_pt["rough"], scene=main_pt["scene"])
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
@@ -646,6 +855,7 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    wd.enter("done")
     bad = [pt["check"] for pt in points if pt["check"] is not None and not pt["check"]["bit_equal"]]
     if bad:
         sys.exit(f"self check failed: {bad}")

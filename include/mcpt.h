@@ -146,11 +146,13 @@ int mcpt_render_counted(mcpt_ctx* ctx, const float* invPV, const float* invV, in
 int mcpt_event_bytes(int event);
 
 #define MCPT_DEBUG_SLOTS 64
-/* Diagnostics: read (and optionally zero) the context's MCPT_DEBUG_SLOTS device counter slots
- * (the first MCPT_EV_COUNT are the event counters).
- * Only the counting launches and diagnostic builds (-DMCPT_STAMPS: wave-cycle section
- * totals) write them.  Synchronizes the context's stream. */
-int mcpt_debug_counters(mcpt_ctx* ctx, unsigned long long* out, int reset);
+/* Diagnostics: read the first min(n_slots, MCPT_DEBUG_SLOTS) of the context's device counter
+ * slots into `out` (which holds n_slots values; the first MCPT_EV_COUNT are the event counters)
+ * and optionally zero them all.  Only the counting launches and diagnostic builds
+ * (-DMCPT_STAMPS: wave-cycle section totals; -DMCPT_LANESTATS) write them.  Synchronizes the
+ * context's stream.  (Version 2: the n_slots argument; version 1 copied MCPT_DEBUG_SLOTS
+ * values, 16 before round 4, whatever the caller's buffer held.) */
+int mcpt_debug_counters(mcpt_ctx* ctx, unsigned long long* out, int n_slots, int reset);
 
 /* Copy the local accumulator (n_local_rows × W × 3 f32) to the host and report the
  * number of passes accumulated (the caller divides: fs_frag, montecarlo.cpp:59-70).
@@ -183,14 +185,16 @@ int mcpt_copy_accum_device(mcpt_ctx* ctx, void* dst_dev_ptr, size_t bytes);
 int mcpt_gather_rows(mcpt_ctx* frame, mcpt_ctx* const* shards, int n_shards);
 
 /* Select the traversal strategy (mcpt_traversal) for later renders; default AUTO.  AUTO times
- * its schedule candidates (per-lane walk, wave-coherent walk, per-lane walk with two and with
- * four pass segments per work item, where the launch has that many segments; for BVH depth >= 8
- * also the stream schedule and per-lane walks with leaf batch 16 / walk exit 40 at four and
- * eight segments per item) on the first launches of >= 2^24 samples after a scene upload: two
- * rounds, forward then reverse order, each candidate's best time per sample kept, compared only
- * between launches of the same shape — at most 14 launches (mcpt.AUTO_TRIALS); later launches
- * of that shape use the fastest.  mcpt_get_walk_exit / mcpt_get_leaf_batch report the knobs of
- * the candidate the next launch uses.
+ * its schedule candidates on the first launches of >= 2^24 samples after a scene upload — the
+ * per-lane walk; the wave-coherent walk (BVH depth < 8 only); the per-lane walk with two and
+ * with four pass segments per work item (where the launch has that many segments); for BVH
+ * depth >= 8 also the per-lane walk with the deep knobs (leaf batch 16, walk exit 40, min-done 8)
+ * at four and at eight segments per item — at most five candidates, each timed twice (forward,
+ * then reverse order; each one's best time per sample kept), compared only between launches of
+ * the same shape: at most 10 trial launches (mcpt.AUTO_TRIALS).  It never times the stream
+ * schedule, which runs only when selected explicitly (MCPT_TRAVERSAL_STREAM).  Later launches of
+ * that shape use the fastest.  mcpt_get_walk_exit / mcpt_get_leaf_batch report the knobs of the
+ * candidate the next launch uses.
  * mcpt_get_traversal reports the strategy the next render uses (a trial candidate until AUTO
  * has settled: see mcpt_get_schedule's `settled`).  Every strategy gives the same bits. */
 int mcpt_set_traversal(mcpt_ctx* ctx, int mode);

@@ -20,8 +20,10 @@
 #include "mcpt_math.h"
 
 // The detail of the calling thread's last failed call (set_err), with its status.  "fresh"
-// until mcpt_error_string hands it out once, so a detail is never attached to a later error that
-// did not set one (HIP errors keep theirs: mcpt_error_string(MCPT_ERR_HIP) always returns it).
+// until mcpt_error_string hands it out once or a later call fails without a detail (every bare
+// error return goes through mcpt_err_bare, which drops it), so a detail is never attached to a
+// later error that did not set one (HIP errors keep theirs: mcpt_error_string(MCPT_ERR_HIP)
+// always returns it).
 static thread_local char g_last_error[256] = "";
 static thread_local char g_detail[320] = "";
 static thread_local int g_last_status = 0;
@@ -34,6 +36,11 @@ static int set_err(int status, const char* what, hipError_t e = hipSuccess) {
     std::snprintf(g_last_error, sizeof(g_last_error), "%s", what);
   g_last_status = status;
   g_fresh = true;
+  return status;
+}
+
+int mcpt_err_bare(int status) {
+  g_fresh = false;
   return status;
 }
 
@@ -64,8 +71,8 @@ struct mcpt_ctx {
   bool has_scene = false;
   // triangle meshes
   int4* d_minfo = nullptr;
-  float4* d_mnodes = nullptr;
-  int* d_mleaves = nullptr;
+  float4* d_mpairs = nullptr;      // mesh BVH child-pair records (SceneT::mpairs)
+  float4* d_mleaftris = nullptr;   // mesh leaf triangle records (SceneT::mleaftris)
   int4* d_mtris = nullptr;
   float4* d_mverts = nullptr;
   float4* d_mnorms = nullptr;
@@ -309,17 +316,17 @@ const char* mcpt_error_string(int status) {
   }
 }
 
-int mcpt_version(void) { return 1; }
+int mcpt_version(void) { return 2; }
 
 int mcpt_create(int device_ordinal, mcpt_ctx** out) {
-  if (!out) return MCPT_ERR_INVALID_ARG;
+  if (!out) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   *out = nullptr;
   int n = 0;
   HIP_OR_RETURN(hipGetDeviceCount(&n));
   if (device_ordinal < 0 || device_ordinal >= n) return set_err(MCPT_ERR_INVALID_ARG, "device ordinal out of range");
   HIP_OR_RETURN(hipSetDevice(device_ordinal));
   mcpt_ctx* c = new (std::nothrow) mcpt_ctx();
-  if (!c) return MCPT_ERR_INVALID_ARG;
+  if (!c) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   c->leaf_batch = env_int("MCPT_LEAF_BATCH", -1);   // tuning hook (same results for any value)
   c->stream_slots = env_int("MCPT_STREAM_SLOTS", 0);
   c->stream_refill = env_int("MCPT_STREAM_REFILL", -1);
@@ -339,9 +346,9 @@ int mcpt_create(int device_ordinal, mcpt_ctx** out) {
 }
 
 static void free_meshes(mcpt_ctx* c) {
-  (void)hipFree(c->d_minfo); (void)hipFree(c->d_mnodes); (void)hipFree(c->d_mleaves);
+  (void)hipFree(c->d_minfo); (void)hipFree(c->d_mpairs); (void)hipFree(c->d_mleaftris);
   (void)hipFree(c->d_mtris); (void)hipFree(c->d_mverts); (void)hipFree(c->d_mnorms);
-  c->d_minfo = nullptr; c->d_mnodes = nullptr; c->d_mleaves = nullptr;
+  c->d_minfo = nullptr; c->d_mpairs = nullptr; c->d_mleaftris = nullptr;
   c->d_mtris = nullptr; c->d_mverts = nullptr; c->d_mnorms = nullptr;
   c->n_meshes = 0;
 }
@@ -465,6 +472,30 @@ static void pack_nodes(const float* nodes, const int* leaves, int depth, float4*
   }
 }
 
+static float int_bits_f(int v) {
+  float f;
+  std::memcpy(&f, &v, sizeof f);
+  return f;
+}
+
+// A mesh BVH's child-pair records: internal node i -> 4 rows (the device's one 64-byte fetch per
+// visit): (c_left, has_left) (w_left, 0) (c_right, has_right) (w_right, 0), c and w computed as
+// pack_nodes does; 1/w is recomputed on the device (rcp_rn, correctly rounded: the bits of the
+// host's 1/w)
+static void pack_mesh_pairs(const float* nodes, const int* leaves, int depth, float4* out) {
+  const int n_leaf = 1 << depth, n_node = 2 * n_leaf - 1;
+  std::vector<float4> rec((size_t)n_node * 3);
+  pack_nodes(nodes, leaves, depth, rec.data());
+  for (int i = 0; i + 1 < n_leaf; ++i) {   // internal nodes 0 .. n_leaf - 2
+    const float4* l = &rec[(size_t)(2 * i + 1) * 3];
+    const float4* r = &rec[(size_t)(2 * i + 2) * 3];
+    out[(size_t)i * 4 + 0] = l[0];
+    out[(size_t)i * 4 + 1] = make_float4(l[1].x, l[1].y, l[1].z, 0.0f);
+    out[(size_t)i * 4 + 2] = r[0];
+    out[(size_t)i * 4 + 3] = make_float4(r[1].x, r[1].y, r[1].z, 0.0f);
+  }
+}
+
 int mcpt_upload_meshes(mcpt_ctx* c, int n_meshes, const int* info, int n_nodes, const float* nodes, int n_leaves,
                        const int* leaves, int n_tris, const int* tris, int n_verts, const float* verts,
                        const float* normals) {
@@ -483,7 +514,9 @@ int mcpt_upload_meshes(mcpt_ctx* c, int n_meshes, const int* info, int n_nodes, 
     return set_err(MCPT_ERR_INVALID_ARG, "mcpt_upload_meshes: bad arguments");
   // validate the layout: each mesh's BVH within the node / leaf arrays, leaf triangle ids
   // within the mesh's triangles, vertex ids within the vertex array
-  std::vector<float4> hn((size_t)n_nodes * 3);
+  // pair records indexed by the global node index (a mesh's leaf slots stay unused) and
+  // leaf triangle records indexed by the global leaf index
+  std::vector<float4> hn((size_t)n_nodes * 4, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
   for (int m = 0; m < n_meshes; ++m) {
     const int no = info[4 * m], lo = info[4 * m + 1], d = info[4 * m + 2], to = info[4 * m + 3];
     if (d < 0 || d > 24 || no < 0 || lo < 0 || to < 0) return set_err(MCPT_ERR_BAD_SCENE, "bad mesh info");
@@ -493,7 +526,7 @@ int mcpt_upload_meshes(mcpt_ctx* c, int n_meshes, const int* info, int n_nodes, 
     if (nt <= 0 || to + nt > n_tris) return set_err(MCPT_ERR_BAD_SCENE, "mesh triangles out of range");
     for (int k = 0; k < nl; ++k)
       if (leaves[lo + k] < -1 || leaves[lo + k] >= nt) return set_err(MCPT_ERR_BAD_SCENE, "mesh leaf id out of range");
-    pack_nodes(nodes + (size_t)no * 6, leaves + lo, d, &hn[(size_t)no * 3]);
+    pack_mesh_pairs(nodes + (size_t)no * 6, leaves + lo, d, &hn[(size_t)no * 4]);
   }
   for (int id : c->mesh_ids)
     if (id >= n_meshes) return set_err(MCPT_ERR_BAD_SCENE, "mesh instance refers to a missing mesh");
@@ -510,15 +543,34 @@ int mcpt_upload_meshes(mcpt_ctx* c, int n_meshes, const int* info, int n_nodes, 
     hv[i] = make_float4(verts[3 * i], verts[3 * i + 1], verts[3 * i + 2], 0.0f);
     hm[i] = make_float4(normals[3 * i], normals[3 * i + 1], normals[3 * i + 2], 0.0f);
   }
+  // leaf triangle records (one 64-byte fetch per leaf visit, no index -> vertex indirection):
+  // (A, t) (B - A, 0) (C - A, 0) (0): Triangle_intersect's vertex A and its two edges, computed
+  // with the binary32 subtractions the device did (same bits), and the mesh-local triangle id t
+  // (-1: an empty leaf) as int bits
+  std::vector<float4> hl((size_t)n_leaves * 4, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+  for (int k = 0; k < n_leaves; ++k) hl[(size_t)k * 4].w = int_bits_f(-1);
+  for (int m = 0; m < n_meshes; ++m) {
+    const int lo = info[4 * m + 1], d = info[4 * m + 2], to = info[4 * m + 3];
+    for (int k = 0; k < (1 << d); ++k) {
+      const int t = leaves[lo + k];
+      if (t < 0) continue;
+      const int4 vi = ht[to + t];
+      const float4 A = hv[vi.x], B = hv[vi.y], C = hv[vi.z];
+      float4* r = &hl[(size_t)(lo + k) * 4];
+      r[0] = make_float4(A.x, A.y, A.z, int_bits_f(t));
+      r[1] = make_float4(B.x - A.x, B.y - A.y, B.z - A.z, 0.0f);
+      r[2] = make_float4(C.x - A.x, C.y - A.y, C.z - A.z, 0.0f);
+    }
+  }
   HIP_OR_RETURN(hipMalloc(&c->d_minfo, hi.size() * sizeof(int4)));
-  HIP_OR_RETURN(hipMalloc(&c->d_mnodes, hn.size() * sizeof(float4)));
-  HIP_OR_RETURN(hipMalloc(&c->d_mleaves, (size_t)n_leaves * sizeof(int)));
+  HIP_OR_RETURN(hipMalloc(&c->d_mpairs, hn.size() * sizeof(float4)));
+  HIP_OR_RETURN(hipMalloc(&c->d_mleaftris, hl.size() * sizeof(float4)));
   HIP_OR_RETURN(hipMalloc(&c->d_mtris, ht.size() * sizeof(int4)));
   HIP_OR_RETURN(hipMalloc(&c->d_mverts, hv.size() * sizeof(float4)));
   HIP_OR_RETURN(hipMalloc(&c->d_mnorms, hm.size() * sizeof(float4)));
   HIP_OR_RETURN(hipMemcpy(c->d_minfo, hi.data(), hi.size() * sizeof(int4), hipMemcpyHostToDevice));
-  HIP_OR_RETURN(hipMemcpy(c->d_mnodes, hn.data(), hn.size() * sizeof(float4), hipMemcpyHostToDevice));
-  HIP_OR_RETURN(hipMemcpy(c->d_mleaves, leaves, (size_t)n_leaves * sizeof(int), hipMemcpyHostToDevice));
+  HIP_OR_RETURN(hipMemcpy(c->d_mpairs, hn.data(), hn.size() * sizeof(float4), hipMemcpyHostToDevice));
+  HIP_OR_RETURN(hipMemcpy(c->d_mleaftris, hl.data(), hl.size() * sizeof(float4), hipMemcpyHostToDevice));
   HIP_OR_RETURN(hipMemcpy(c->d_mtris, ht.data(), ht.size() * sizeof(int4), hipMemcpyHostToDevice));
   HIP_OR_RETURN(hipMemcpy(c->d_mverts, hv.data(), hv.size() * sizeof(float4), hipMemcpyHostToDevice));
   HIP_OR_RETURN(hipMemcpy(c->d_mnorms, hm.data(), hm.size() * sizeof(float4), hipMemcpyHostToDevice));
@@ -527,7 +579,7 @@ int mcpt_upload_meshes(mcpt_ctx* c, int n_meshes, const int* info, int n_nodes, 
 }
 
 int mcpt_set_flat_face(mcpt_ctx* c, int flat_face) {
-  if (!c) return MCPT_ERR_INVALID_ARG;
+  if (!c) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   c->flat_face = flat_face ? 1 : 0;
   return MCPT_OK;
 }
@@ -606,22 +658,22 @@ int mcpt_balanced_rows(int H, int world, int rank, int band_rows, int* rows_out,
 }
 
 int mcpt_local_row_ids(mcpt_ctx* c, int* rows_out) {
-  if (!c || !rows_out) return MCPT_ERR_INVALID_ARG;
-  if (!c->has_target) return MCPT_ERR_NO_TARGET;
+  if (!c || !rows_out) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
+  if (!c->has_target) return mcpt_err_bare(MCPT_ERR_NO_TARGET);
   std::copy(c->rows.begin(), c->rows.end(), rows_out);
   return MCPT_OK;
 }
 
 int mcpt_local_rows(mcpt_ctx* c, int* n) {
-  if (!c || !n) return MCPT_ERR_INVALID_ARG;
-  if (!c->has_target) return MCPT_ERR_NO_TARGET;
+  if (!c || !n) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
+  if (!c->has_target) return mcpt_err_bare(MCPT_ERR_NO_TARGET);
   *n = c->n_local_rows;
   return MCPT_OK;
 }
 
 int mcpt_clear_accum(mcpt_ctx* c) {
-  if (!c) return MCPT_ERR_INVALID_ARG;
-  if (!c->has_target) return MCPT_ERR_NO_TARGET;
+  if (!c) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
+  if (!c->has_target) return mcpt_err_bare(MCPT_ERR_NO_TARGET);
   HIP_OR_RETURN(hipSetDevice(c->device));
   if (c->accum_bytes) HIP_OR_RETURN(hipMemsetAsync(c->d_accum, 0, c->accum_bytes, c->stream));
   c->pass_count = 0;
@@ -839,7 +891,7 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
                           (((1LL << c->depth) + c->n_prims) * 4);
     p.lds_scene_bytes = (MCPT_LDS_SCENE && c->n_meshes == 0 && lds <= mcpt::kLdsSceneBytes) ? (int)lds : 0;
   }
-  p.minfo = c->d_minfo; p.mnodes = c->d_mnodes; p.mleaves = c->d_mleaves; p.mtris = c->d_mtris;
+  p.minfo = c->d_minfo; p.mpairs = c->d_mpairs; p.mleaftris = c->d_mleaftris; p.mtris = c->d_mtris;
   p.mverts = c->d_mverts; p.mnorms = c->d_mnorms; p.n_meshes = c->n_meshes; p.flat_face = c->flat_face;
   HIP_OR_RETURN(collect_tuning(c));
   // (the counting build is not timed: AUTO counts with the per-lane walk)
@@ -978,28 +1030,29 @@ int mcpt_render(mcpt_ctx* c, const float* invPV, const float* invV, int first_pa
 
 int mcpt_render_counted(mcpt_ctx* c, const float* invPV, const float* invV, int first_pass, int n_passes,
                         float date, int bounces, float refract_ind, int variant, unsigned long long* events) {
-  if (!events) return MCPT_ERR_INVALID_ARG;
+  if (!events) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   return launch(c, invPV, invV, first_pass, n_passes, date, bounces, refract_ind, variant, true, events);
 }
 
-int mcpt_debug_counters(mcpt_ctx* c, unsigned long long* out, int reset) {
-  if (!c || !out) return MCPT_ERR_INVALID_ARG;
+int mcpt_debug_counters(mcpt_ctx* c, unsigned long long* out, int n_slots, int reset) {
+  if (!c || n_slots < 0 || (!out && n_slots > 0)) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   HIP_OR_RETURN(hipSetDevice(c->device));
-  HIP_OR_RETURN(hipMemcpyAsync(out, c->d_events, sizeof(unsigned long long) * MCPT_DEBUG_SLOTS,
-                               hipMemcpyDeviceToHost, c->stream));
+  const int n = n_slots < MCPT_DEBUG_SLOTS ? n_slots : MCPT_DEBUG_SLOTS;   // never past the caller's buffer
+  if (n > 0)
+    HIP_OR_RETURN(hipMemcpyAsync(out, c->d_events, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost, c->stream));
   if (reset) HIP_OR_RETURN(hipMemsetAsync(c->d_events, 0, sizeof(unsigned long long) * MCPT_DEBUG_SLOTS, c->stream));
   HIP_OR_RETURN(hipStreamSynchronize(c->stream));
   return MCPT_OK;
 }
 
 int mcpt_event_bytes(int e) {
-  if (e < 0 || e >= mcpt::EV_COUNT) return MCPT_ERR_INVALID_ARG;
+  if (e < 0 || e >= mcpt::EV_COUNT) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   return mcpt::kEventBytes[e];
 }
 
 int mcpt_read_accum(mcpt_ctx* c, float* rgb_out, int* pass_count) {
-  if (!c) return MCPT_ERR_INVALID_ARG;
-  if (!c->has_target) return MCPT_ERR_NO_TARGET;
+  if (!c) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
+  if (!c->has_target) return mcpt_err_bare(MCPT_ERR_NO_TARGET);
   HIP_OR_RETURN(hipSetDevice(c->device));
   if (rgb_out && c->accum_bytes)
     HIP_OR_RETURN(hipMemcpyAsync(rgb_out, c->d_accum, c->accum_bytes, hipMemcpyDeviceToHost, c->stream));
@@ -1009,8 +1062,8 @@ int mcpt_read_accum(mcpt_ctx* c, float* rgb_out, int* pass_count) {
 }
 
 int mcpt_write_accum(mcpt_ctx* c, const float* rgb, int pass_count) {
-  if (!c || !rgb || pass_count < 0) return MCPT_ERR_INVALID_ARG;
-  if (!c->has_target) return MCPT_ERR_NO_TARGET;
+  if (!c || !rgb || pass_count < 0) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
+  if (!c->has_target) return mcpt_err_bare(MCPT_ERR_NO_TARGET);
   HIP_OR_RETURN(hipSetDevice(c->device));
   if (c->accum_bytes)
     HIP_OR_RETURN(hipMemcpyAsync(c->d_accum, rgb, c->accum_bytes, hipMemcpyHostToDevice, c->stream));
@@ -1040,8 +1093,8 @@ static unsigned long long rows_hash(const mcpt_ctx* c) {
 }
 
 int mcpt_checkpoint_save(mcpt_ctx* c, const char* path, int next_pass, const char* tag) {
-  if (!c || !path) return MCPT_ERR_INVALID_ARG;
-  if (!c->has_target) return MCPT_ERR_NO_TARGET;
+  if (!c || !path) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
+  if (!c->has_target) return mcpt_err_bare(MCPT_ERR_NO_TARGET);
   std::vector<float> acc((size_t)c->n_local_rows * c->W * 3);
   int n = 0;
   const int st = mcpt_read_accum(c, acc.data(), &n);
@@ -1053,8 +1106,8 @@ int mcpt_checkpoint_save(mcpt_ctx* c, const char* path, int next_pass, const cha
 }
 
 int mcpt_checkpoint_load(mcpt_ctx* c, const char* path, const char* tag, int* next_pass) {
-  if (!c || !path) return MCPT_ERR_INVALID_ARG;
-  if (!c->has_target) return MCPT_ERR_NO_TARGET;
+  if (!c || !path) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
+  if (!c->has_target) return mcpt_err_bare(MCPT_ERR_NO_TARGET);
   int w = 0, rows = 0, n = 0, nxt = 0, h = 0;
   unsigned long long hash = 0;
   std::vector<char> t(MCPT_CHECKPOINT_TAG_MAX);
@@ -1077,16 +1130,16 @@ int mcpt_checkpoint_load(mcpt_ctx* c, const char* path, const char* tag, int* ne
 }
 
 int mcpt_accum_device_ptr(mcpt_ctx* c, void** dev_ptr, size_t* bytes) {
-  if (!c || !dev_ptr) return MCPT_ERR_INVALID_ARG;
-  if (!c->has_target) return MCPT_ERR_NO_TARGET;
+  if (!c || !dev_ptr) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
+  if (!c->has_target) return mcpt_err_bare(MCPT_ERR_NO_TARGET);
   *dev_ptr = c->d_accum;
   if (bytes) *bytes = c->accum_bytes;
   return MCPT_OK;
 }
 
 int mcpt_copy_accum_device(mcpt_ctx* c, void* dst, size_t bytes) {
-  if (!c || (!dst && bytes)) return MCPT_ERR_INVALID_ARG;
-  if (!c->has_target) return MCPT_ERR_NO_TARGET;
+  if (!c || (!dst && bytes)) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
+  if (!c->has_target) return mcpt_err_bare(MCPT_ERR_NO_TARGET);
   if (bytes < c->accum_bytes) return set_err(MCPT_ERR_INVALID_ARG, "destination smaller than the accumulator");
   HIP_OR_RETURN(hipSetDevice(c->device));
   if (c->accum_bytes)
@@ -1176,7 +1229,7 @@ int mcpt_trace(mcpt_ctx* c, const float* origins, const float* dirs, int n, int 
   mcpt::TraceParams q;
   q.nodes = c->d_nodes; q.leaves = c->d_leaves; q.ptype = c->d_ptype; q.prims = c->d_prims; q.depth = c->depth;
   q.prim = prim < 0 ? -1 : prim;
-  q.minfo = c->d_minfo; q.mnodes = c->d_mnodes; q.mleaves = c->d_mleaves; q.mtris = c->d_mtris;
+  q.minfo = c->d_minfo; q.mpairs = c->d_mpairs; q.mleaftris = c->d_mleaftris; q.mtris = c->d_mtris;
   q.mverts = c->d_mverts; q.mnorms = c->d_mnorms; q.n_meshes = c->n_meshes; q.flat_face = c->flat_face;
   q.orig = (const float*)buf; q.dir = (const float*)(buf + n3);
   q.out_i = (int*)(buf + 2 * n3); q.out = (float*)(buf + 2 * n3 + ni); q.n = n;
@@ -1244,25 +1297,25 @@ int mcpt_set_stream_pool(mcpt_ctx* c, int slots, int refill) {
 }
 
 int mcpt_stream_iterations(mcpt_ctx* c, long long* iterations) {
-  if (!c || !iterations) return MCPT_ERR_INVALID_ARG;
+  if (!c || !iterations) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   *iterations = c->stream_iters;
   return MCPT_OK;
 }
 
 int mcpt_set_partial_budget(mcpt_ctx* c, size_t bytes) {
-  if (!c) return MCPT_ERR_INVALID_ARG;
+  if (!c) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   c->partial_budget = bytes;
   return MCPT_OK;
 }
 
 int mcpt_last_launch_count(mcpt_ctx* c, int* n_launches) {
-  if (!c || !n_launches) return MCPT_ERR_INVALID_ARG;
+  if (!c || !n_launches) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   *n_launches = c->timed ? c->n_sub : 0;
   return MCPT_OK;
 }
 
 int mcpt_last_pass_split(mcpt_ctx* c, int* split) {
-  if (!c || !split) return MCPT_ERR_INVALID_ARG;
+  if (!c || !split) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   *split = c->timed ? c->pass_split : 0;
   return MCPT_OK;
 }
@@ -1274,7 +1327,7 @@ int mcpt_set_leaf_batch(mcpt_ctx* c, int lanes) {
 }
 
 int mcpt_get_leaf_batch(mcpt_ctx* c, int* resolved) {
-  if (!c || !resolved) return MCPT_ERR_INVALID_ARG;
+  if (!c || !resolved) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   // the value the next launch of the last launch shape uses (an AUTO deep candidate sets its own)
   const int cand = resolve_candidate(c, c->meas_segs);
   *resolved = (cand_deep_knobs(cand) && c->leaf_batch < 0) ? kDeepLeafBatch : resolve_leaf_batch(c);
@@ -1282,20 +1335,20 @@ int mcpt_get_leaf_batch(mcpt_ctx* c, int* resolved) {
 }
 
 int mcpt_get_walk_exit(mcpt_ctx* c, int* resolved) {
-  if (!c || !resolved) return MCPT_ERR_INVALID_ARG;
+  if (!c || !resolved) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   const int cand = resolve_candidate(c, c->meas_segs);
   *resolved = (cand_deep_knobs(cand) && c->walk_exit < 0) ? kDeepWalkExit : resolve_walk_exit(c);
   return MCPT_OK;
 }
 
 int mcpt_get_traversal(mcpt_ctx* c, int* resolved) {
-  if (!c || !resolved) return MCPT_ERR_INVALID_ARG;
+  if (!c || !resolved) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   *resolved = resolve_traversal(c);
   return MCPT_OK;
 }
 
 int mcpt_get_schedule(mcpt_ctx* c, int* traversal, int* seg_per_item, int* settled) {
-  if (!c) return MCPT_ERR_INVALID_ARG;
+  if (!c) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   const int cand = resolve_candidate(c, c->meas_segs);
   if (traversal) *traversal = cand_traversal(cand);
   const int env_seg = env_int("MCPT_SEG_PER_ITEM", 0);
@@ -1305,7 +1358,7 @@ int mcpt_get_schedule(mcpt_ctx* c, int* traversal, int* seg_per_item, int* settl
 }
 
 int mcpt_set_stream(mcpt_ctx* c, void* s) {
-  if (!c) return MCPT_ERR_INVALID_ARG;
+  if (!c) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   HIP_OR_RETURN(hipSetDevice(c->device));
   HIP_OR_RETURN(hipStreamSynchronize(c->stream));
   c->stream = s ? (hipStream_t)s : c->own_stream;
@@ -1313,14 +1366,14 @@ int mcpt_set_stream(mcpt_ctx* c, void* s) {
 }
 
 int mcpt_synchronize(mcpt_ctx* c) {
-  if (!c) return MCPT_ERR_INVALID_ARG;
+  if (!c) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   HIP_OR_RETURN(hipSetDevice(c->device));
   HIP_OR_RETURN(hipStreamSynchronize(c->stream));
   return MCPT_OK;
 }
 
 int mcpt_last_render_ms(mcpt_ctx* c, float* ms) {
-  if (!c || !ms) return MCPT_ERR_INVALID_ARG;
+  if (!c || !ms) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   if (!c->timed) return set_err(MCPT_ERR_INVALID_ARG, "no render timed yet");
   HIP_OR_RETURN(hipSetDevice(c->device));
   HIP_OR_RETURN(hipEventSynchronize(ev_stop(c, c->n_sub - 1)));
@@ -1329,7 +1382,7 @@ int mcpt_last_render_ms(mcpt_ctx* c, float* ms) {
 }
 
 int mcpt_kernel_ms_back(mcpt_ctx* c, int back, float* trace_ms, float* combine_ms) {
-  if (!c || !trace_ms || !combine_ms) return MCPT_ERR_INVALID_ARG;
+  if (!c || !trace_ms || !combine_ms) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   if (back < 0 || back >= kTimingRing || back >= c->n_timed)
     return set_err(MCPT_ERR_INVALID_ARG, "mcpt_kernel_ms_back: no such call in the timing ring");
   HIP_OR_RETURN(hipSetDevice(c->device));
@@ -1338,7 +1391,7 @@ int mcpt_kernel_ms_back(mcpt_ctx* c, int back, float* trace_ms, float* combine_m
 }
 
 int mcpt_last_kernel_ms(mcpt_ctx* c, float* trace_ms, float* combine_ms) {
-  if (!c || !trace_ms || !combine_ms) return MCPT_ERR_INVALID_ARG;
+  if (!c || !trace_ms || !combine_ms) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   if (!c->timed) return set_err(MCPT_ERR_INVALID_ARG, "no render timed yet");
   HIP_OR_RETURN(hipSetDevice(c->device));
   HIP_OR_RETURN(sub_launch_ms(c, trace_ms, combine_ms));

@@ -96,9 +96,13 @@ struct SceneT {
   int depth;
   // meshes (mcpt_upload_meshes): per mesh (first node, first leaf, depth, first triangle)
   const int4* __restrict__ minfo;
-  const float4* __restrict__ mnodes;  // 3 per node, mesh space
-  const int* __restrict__ mleaves;    // mesh-local triangle ids or -1
-  const int4* __restrict__ mtris;     // global vertex ids (a, b, c, 0)
+  // mesh BVHs, mesh space: 4 rows per internal node at its global node index, both children's
+  // boxes in one 64-byte record, (c_left, has_left) (w_left, 0) (c_right, has_right) (w_right, 0)
+  const float4* __restrict__ mpairs;
+  // 4 rows per mesh leaf at its global leaf index: (A, t) (B - A, 0) (C - A, 0) (0) of the
+  // leaf's triangle, t = the mesh-local triangle id as int bits (-1: empty leaf)
+  const float4* __restrict__ mleaftris;
+  const int4* __restrict__ mtris;     // global vertex ids (a, b, c, 0) (intersection_info)
   const float4* __restrict__ mverts;  // (x, y, z, 0)
   const float4* __restrict__ mnorms;
   int flat_face;                      // uniform flat_face (raytracer_func.frag:26; never set: 0)
@@ -320,12 +324,15 @@ __device__ __forceinline__ void node_tests(const SR& s, const float4* __restrict
 // intersect_bvm raytracer_func.frag:273-311: the mesh BVH's box test, in mesh space (O, D),
 // with the entry point taken to world space through the mesh transform (rows t0..t2) and
 // compared with the world distance from Ol.  Same face loop as box_test.
-__device__ __forceinline__ bool box_test_mesh(float4 a0, float4 a1, float4 a2, f3 O, f3 D, f3 invD, f3 Ol,
+__device__ __forceinline__ bool box_test_mesh(float4 a0, float4 a1, f3 iw, f3 O, f3 D, f3 invD, f3 Ol,
                                               float4 t0, float4 t1, float4 t2, double cull2) {
-  f3 c = mk(a0.x, a0.y, a0.z), w = mk(a1.x, a1.y, a1.z), iw = mk(a2.x, a2.y, a2.z);
+  f3 c = mk(a0.x, a0.y, a0.z), w = mk(a1.x, a1.y, a1.z);
   f3 Oi = mulv(sub(O, c), iw);
   f3 Di = mulv(D, iw);
-  if (__builtin_fabsf(Oi.x) < 1.0f && __builtin_fabsf(Oi.y) < 1.0f && __builtin_fabsf(Oi.z) < 1.0f) return true;
+  // all |Oi| < 1 as one compare of the NaN-propagating maximum (exact, as in box_test)
+  if (__builtin_elementwise_maximum(__builtin_elementwise_maximum(__builtin_fabsf(Oi.x), __builtin_fabsf(Oi.y)),
+                                    __builtin_fabsf(Oi.z)) < 1.0f)
+    return true;
   f3 rD = mulv(invD, w);
   const bool dx = __builtin_fabsf(Di.x) > kEPS, dy = __builtin_fabsf(Di.y) > kEPS, dz = __builtin_fabsf(Di.z) > kEPS;
   float al = kFLTMAX;
@@ -366,16 +373,14 @@ __device__ __forceinline__ void accept_cand(const SR& s, int index, int shape, i
                      ld4<U>(s.prims, b + 5), h, ev, SR::kFastLen);
 }
 
-// Triangle_intersect raytracer_func.frag:354-396 (Möller–Trumbore, mesh space); a hit keeps
-// the mesh-local triangle index in Hit::dir (the reference's tri_index; its dir is 0)
+// Triangle_intersect raytracer_func.frag:354-396 (Möller–Trumbore, mesh space) on a leaf record
+// (vertex A, edges B - A and C - A: the same binary32 values the test computed from the vertices);
+// a hit keeps the mesh-local triangle index in Hit::tri (the reference's tri_index; its dir is 0)
 template <bool COUNT, class SR>
-__device__ __forceinline__ void tri_test(const SR& s, int tri_base, int t, int index, f3 O, f3 D, f3 Ol,
+__device__ __forceinline__ void tri_test(int t, float4 r0, float4 r1, float4 r2, int index, f3 O, f3 D, f3 Ol,
                                          float4 t0, float4 t1, float4 t2, Hit& h, Ev<COUNT>& ev) {
   ev.inc(EV_TRI);
-  const int4 vi = s.mtris[tri_base + t];
-  const float4 a4 = s.mverts[vi.x], b4 = s.mverts[vi.y], c4 = s.mverts[vi.z];
-  const f3 vA = mk(a4.x, a4.y, a4.z), vB = mk(b4.x, b4.y, b4.z), vC = mk(c4.x, c4.y, c4.z);
-  const f3 edge1 = sub(vB, vA), edge2 = sub(vC, vA);
+  const f3 vA = mk(r0.x, r0.y, r0.z), edge1 = mk(r1.x, r1.y, r1.z), edge2 = mk(r2.x, r2.y, r2.z);
   const f3 hv = cross3(D, edge2);
   const float det = dot3(edge1, hv);
   if (__builtin_fabsf(det) < kEPS) return;
@@ -398,6 +403,48 @@ __device__ __forceinline__ void tri_test(const SR& s, int tri_base, int t, int i
   }
 }
 
+// a mesh leaf visit: the leaf's triangle record in one round trip, then its test (t >= 0)
+template <bool COUNT, class SR>
+__device__ __forceinline__ void mesh_leaf(const SR& s, size_t leaf, int index, f3 O, f3 D, f3 Ol, float4 t0,
+                                          float4 t1, float4 t2, Hit& h, Ev<COUNT>& ev) {
+  const float4* q = s.mleaftris + leaf * 4;
+  const float4 r0 = q[0], r1 = q[1], r2 = q[2];
+  MCPT_ROWS_IN("v"(r0.x), "v"(r0.y), "v"(r0.z), "v"(r0.w), "v"(r1.x), "v"(r1.y), "v"(r1.z), "v"(r2.x),
+               "v"(r2.y), "v"(r2.z));
+  const int t = __float_as_int(r0.w);
+  if (t >= 0) tri_test<COUNT, SR>(t, r0, r1, r2, index, O, D, Ol, t0, t1, t2, h, ev);
+}
+
+// 1/w of a mesh child box, correctly rounded (= the host's 1.0f / w of pack_nodes): rcp_core on
+// all six lanes' values, the IEEE reciprocal where some operand leaves its exact range
+__device__ __forceinline__ void rcp6_rn(float4 wl, float4 wr, f3& il, f3& ir) {
+  il = mk(rcp_core(wl.x), rcp_core(wl.y), rcp_core(wl.z));
+  ir = mk(rcp_core(wr.x), rcp_core(wr.y), rcp_core(wr.z));
+  const bool ok = (int)rcp_core_ok(wl.x) & (int)rcp_core_ok(wl.y) & (int)rcp_core_ok(wl.z) &
+                  (int)rcp_core_ok(wr.x) & (int)rcp_core_ok(wr.y) & (int)rcp_core_ok(wr.z);
+  if (__builtin_expect(__ballot(!ok) != 0, 0)) {
+    if (!ok) {
+      il = mk(rcp_ieee(wl.x), rcp_ieee(wl.y), rcp_ieee(wl.z));
+      ir = mk(rcp_ieee(wr.x), rcp_ieee(wr.y), rcp_ieee(wr.z));
+    }
+  }
+}
+
+// a mesh node visit (intersect_bvm for both children, :273-311): the child-pair record in one
+// round trip (all four rows issued together: a visit waits for one fetch), 1/w recomputed
+template <bool COUNT, class SR>
+__device__ __forceinline__ void mesh_pair_tests(const SR& s, size_t node, f3 O, f3 D, f3 invD, f3 Ol, float4 t0,
+                                                float4 t1, float4 t2, double cull2, bool& hl, bool& hr) {
+  const float4* q = s.mpairs + node * 4;
+  const float4 a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
+  MCPT_ROWS_IN("v"(a0.x), "v"(a0.y), "v"(a0.z), "v"(a0.w), "v"(a1.x), "v"(a1.y), "v"(a1.z));
+  MCPT_ROWS_IN("v"(a2.x), "v"(a2.y), "v"(a2.z), "v"(a2.w), "v"(a3.x), "v"(a3.y), "v"(a3.z));
+  f3 il, ir;
+  rcp6_rn(a1, a3, il, ir);
+  hl = (COUNT || a0.w != 0.0f) && box_test_mesh(a0, a1, il, O, D, invD, Ol, t0, t1, t2, cull2);
+  hr = (COUNT || a2.w != 0.0f) && box_test_mesh(a2, a3, ir, O, D, invD, Ol, t0, t1, t2, cull2);
+}
+
 // Mesh_intersect raytracer_func.frag:642-678: the instance's own BVH, same DFS as
 // intersect_bvh (right child first, cull at push with intersect_bvm), stackless per lane
 template <bool COUNT, bool ANY, class SR>
@@ -407,7 +454,6 @@ __device__ __forceinline__ void mesh_test(const SR& s, int mesh, int index, f3 O
   const int4 mi = s.minfo[mesh];   // first node, first leaf, depth, first triangle
   const size_t b = (size_t)index * 8;
   const float4 t0 = s.prims[b + 3], t1 = s.prims[b + 4], t2 = s.prims[b + 5];   // read_mesh_transfo
-  const float4* nodes = s.mnodes + (size_t)mi.x * 3;
   const f3 invD = mk(rcp_rn(D.x), rcp_rn(D.y), rcp_rn(D.z));
   const int leaf0 = (1 << mi.z) - 1;
   int node = 0, level = 0;
@@ -416,19 +462,13 @@ __device__ __forceinline__ void mesh_test(const SR& s, int mesh, int index, f3 O
     bool pop = true;
     if (node >= leaf0) {
       ev.inc(EV_LEAF);
-      const int t = s.mleaves[mi.y + node - leaf0];
-      if (t >= 0) {
-        tri_test<COUNT>(s, mi.w, t, index, O, D, Ol, t0, t1, t2, h, ev);
-        if (ANY && h.hit()) return;   // hit_only (:664-665)
-      }
+      mesh_leaf<COUNT>(s, (size_t)mi.y + (node - leaf0), index, O, D, Ol, t0, t1, t2, h, ev);
+      if (ANY && h.hit()) return;   // hit_only (:664-665): only a triangle can have set it
     } else {
       ev.inc(EV_NODE);
       const size_t j = 2 * (size_t)node + 1;
-      const float4 l0 = nodes[j * 3], r0 = nodes[j * 3 + 3];   // (mesh kernels: see node_tests)
-      bool hl = (COUNT || l0.w != 0.0f) &&
-                box_test_mesh(l0, nodes[j * 3 + 1], nodes[j * 3 + 2], O, D, invD, Ol, t0, t1, t2, h.cull2);
-      bool hr = (COUNT || r0.w != 0.0f) &&
-                box_test_mesh(r0, nodes[j * 3 + 4], nodes[j * 3 + 5], O, D, invD, Ol, t0, t1, t2, h.cull2);
+      bool hl, hr;
+      mesh_pair_tests<COUNT>(s, (size_t)mi.x + node, O, D, invD, Ol, t0, t1, t2, h.cull2, hl, hr);
       pop = !(hl || hr);
       if (hr) {
         if (hl) pending |= 1u << (level + 1);
@@ -844,17 +884,12 @@ __device__ __forceinline__ bool walk_run_mesh(const SR& s, f3 O, f3 D, Hit& h, W
       bool mpop = true;
       if (w.mnode >= mleaf0) {
         ev.inc(EV_LEAF);
-        const int t = s.mleaves[mi.y + w.mnode - mleaf0];
-        if (t >= 0) tri_test<COUNT>(s, mi.w, t, w.mprim, w.Om, w.Dm, O, t0, t1, t2, h, ev);
+        mesh_leaf<COUNT>(s, (size_t)mi.y + (w.mnode - mleaf0), w.mprim, w.Om, w.Dm, O, t0, t1, t2, h, ev);
       } else {
         ev.inc(EV_NODE);
-        const float4* nodes = s.mnodes + (size_t)mi.x * 3;
         const size_t j = 2 * (size_t)w.mnode + 1;
-        const float4 l0 = nodes[j * 3], r0 = nodes[j * 3 + 3];   // (mesh kernels: see node_tests)
-        const bool hl = (COUNT || l0.w != 0.0f) &&
-                        box_test_mesh(l0, nodes[j * 3 + 1], nodes[j * 3 + 2], w.Om, w.Dm, w.invDm, O, t0, t1, t2, h.cull2);
-        const bool hr = (COUNT || r0.w != 0.0f) &&
-                        box_test_mesh(r0, nodes[j * 3 + 4], nodes[j * 3 + 5], w.Om, w.Dm, w.invDm, O, t0, t1, t2, h.cull2);
+        bool hl, hr;
+        mesh_pair_tests<COUNT>(s, (size_t)mi.x + w.mnode, w.Om, w.Dm, w.invDm, O, t0, t1, t2, h.cull2, hl, hr);
         mpop = !(hl || hr);
         if (hr) {
           if (hl) w.mpending |= 1u << (w.mlevel + 1);

@@ -29,6 +29,9 @@
 
 #include "../../include/mcpt.h"
 
+// mcpt_capi.hip: an error return without a detail (drops the thread's unread detail)
+int mcpt_err_bare(int status);
+
 namespace mcpt {
 namespace host {
 void transfo_translate(float x, float y, float z, float* out);
@@ -80,16 +83,16 @@ unsigned char unorm8(float c) {
 extern "C" {
 
 int mcpt_average(const float* accum, long long n_values, int pass_count, float* out) {
-  if (!accum || !out || n_values < 0 || pass_count <= 0) return MCPT_ERR_INVALID_ARG;
+  if (!accum || !out || n_values < 0 || pass_count <= 0) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   const float nb = (float)pass_count;
   for (long long i = 0; i < n_values; ++i) out[i] = accum[i] / nb;
   return MCPT_OK;
 }
 
 int mcpt_write_pfm(const char* path, const float* rgb, int W, int H) {
-  if (!path || !rgb || W <= 0 || H <= 0) return MCPT_ERR_INVALID_ARG;
+  if (!path || !rgb || W <= 0 || H <= 0) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   FILE* f = std::fopen(path, "wb");
-  if (!f) return MCPT_ERR_INVALID_ARG;
+  if (!f) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   std::fprintf(f, "PF\n%d %d\n-1.0\n", W, H);   // negative scale = little endian
   const size_t n = (size_t)W * H * 3;
   const bool ok = std::fwrite(rgb, sizeof(float), n, f) == n;
@@ -97,7 +100,7 @@ int mcpt_write_pfm(const char* path, const float* rgb, int W, int H) {
 }
 
 int mcpt_write_png(const char* path, const float* rgb, int W, int H) {
-  if (!path || !rgb || W <= 0 || H <= 0 || W > (1 << 24) || H > (1 << 24)) return MCPT_ERR_INVALID_ARG;
+  if (!path || !rgb || W <= 0 || H <= 0 || W > (1 << 24) || H > (1 << 24)) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   // raw scanlines, filter 0, top row first (the accumulator's row 0 is the bottom)
   const size_t row = (size_t)W * 3 + 1;
   std::vector<unsigned char> raw(row * H);
@@ -131,7 +134,7 @@ int mcpt_write_png(const char* path, const float* rgb, int W, int H) {
   chunk(out, "IDAT", z);
   chunk(out, "IEND", {});
   FILE* f = std::fopen(path, "wb");
-  if (!f) return MCPT_ERR_INVALID_ARG;
+  if (!f) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   const bool ok = std::fwrite(out.data(), 1, out.size(), f) == out.size();
   return (std::fclose(f) == 0 && ok) ? MCPT_OK : MCPT_ERR_INVALID_ARG;
 }
@@ -149,14 +152,14 @@ namespace host {
 // previous checkpoint or the new one, and two writers never share a temporary file.
 int checkpoint_write_ex(const char* path, const float* rgb, int W, int rows, int pass_count, int next_pass,
                         const char* tag, int H, unsigned long long rows_hash) {
-  if (!path || !rgb || W <= 0 || rows <= 0 || pass_count < 0 || H < 0) return MCPT_ERR_INVALID_ARG;
+  if (!path || !rgb || W <= 0 || rows <= 0 || pass_count < 0 || H < 0) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   const size_t tag_len = tag ? std::strlen(tag) : 0;
-  if (tag_len >= MCPT_CHECKPOINT_TAG_MAX) return MCPT_ERR_INVALID_ARG;
+  if (tag_len >= MCPT_CHECKPOINT_TAG_MAX) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   char suffix[64];
   std::snprintf(suffix, sizeof(suffix), ".tmp.%ld.%zx", (long)getpid(), std::hash<std::thread::id>()(std::this_thread::get_id()));
   const std::string tmp = std::string(path) + suffix;
   FILE* f = std::fopen(tmp.c_str(), "wb");
-  if (!f) return MCPT_ERR_INVALID_ARG;
+  if (!f) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   const int32_t hdr[6] = {W, rows, pass_count, next_pass, (int32_t)tag_len, H};
   const uint64_t hash = rows_hash;
   const size_t n = (size_t)W * rows * 3;
@@ -167,7 +170,7 @@ int checkpoint_write_ex(const char* path, const float* rgb, int W, int rows, int
   ok = (std::fclose(f) == 0) && ok;
   if (!ok || std::rename(tmp.c_str(), path) != 0) {
     std::remove(tmp.c_str());
-    return MCPT_ERR_INVALID_ARG;
+    return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   }
   // the rename itself reaches the device with the directory's metadata
   std::string dir(path);
@@ -183,9 +186,9 @@ int checkpoint_write_ex(const char* path, const float* rgb, int W, int rows, int
 
 int checkpoint_read_ex(const char* path, float* rgb_out, long long capacity, int* W, int* rows, int* pass_count,
                        int* next_pass, char* tag_out, int* H, unsigned long long* rows_hash) {
-  if (!path) return MCPT_ERR_INVALID_ARG;
+  if (!path) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   FILE* f = std::fopen(path, "rb");
-  if (!f) return MCPT_ERR_INVALID_ARG;
+  if (!f) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   char magic[8];
   int32_t hdr[6] = {0, 0, 0, 0, 0, 0};
   uint64_t hash = 0;
@@ -202,7 +205,7 @@ int checkpoint_read_ex(const char* path, float* rgb_out, long long capacity, int
     ok = capacity >= 0 && n <= (size_t)capacity && std::fread(rgb_out, sizeof(float), n, f) == n;
   }
   std::fclose(f);
-  if (!ok) return MCPT_ERR_INVALID_ARG;
+  if (!ok) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   tag[hdr[4]] = '\0';
   if (W) *W = hdr[0];
   if (rows) *rows = hdr[1];
@@ -228,22 +231,22 @@ int mcpt_checkpoint_read(const char* path, float* rgb_out, long long capacity, i
 }
 
 int mcpt_transfo_translate(float x, float y, float z, float* out16) {
-  if (!out16) return MCPT_ERR_INVALID_ARG;
+  if (!out16) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   mcpt::host::transfo_translate(x, y, z, out16);
   return MCPT_OK;
 }
 int mcpt_transfo_scale(float x, float y, float z, float* out16) {
-  if (!out16) return MCPT_ERR_INVALID_ARG;
+  if (!out16) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   mcpt::host::transfo_scale(x, y, z, out16);
   return MCPT_OK;
 }
 int mcpt_transfo_rotate(int axis, float degrees, float* out16) {
-  if (!out16 || axis < 0 || axis > 2) return MCPT_ERR_INVALID_ARG;
+  if (!out16 || axis < 0 || axis > 2) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   mcpt::host::transfo_rotate(axis, degrees, out16);
   return MCPT_OK;
 }
 int mcpt_mat4_mul(const float* a16, const float* b16, float* out16) {
-  if (!a16 || !b16 || !out16) return MCPT_ERR_INVALID_ARG;
+  if (!a16 || !b16 || !out16) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   mcpt::host::mat4_mul(a16, b16, out16);
   return MCPT_OK;
 }

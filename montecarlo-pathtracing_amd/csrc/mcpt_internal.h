@@ -3,6 +3,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// an error return without a detail (mcpt_capi.hip): drops the calling thread's unread detail of an
+// earlier failure, so mcpt_error_string never attaches it to this one
+int mcpt_err_bare(int status);
+
 namespace mcpt {
 
 // algorithmic-byte events; same order as the oracle's counters
@@ -70,10 +74,10 @@ struct RenderParams {
   int pass_split;               // 1: one segment per pass (n_segments = n_passes; small launches)
   int depth, n_prims;
   int lds_scene_bytes;          // > 0: stage the scene into LDS (<= kLdsSceneBytes, no meshes)
-  // triangle meshes (mcpt_upload_meshes); n_meshes == 0: none
+  // triangle meshes (mcpt_upload_meshes; layouts: SceneT); n_meshes == 0: none
   const int4* minfo;
-  const float4* mnodes;
-  const int* mleaves;
+  const float4* mpairs;
+  const float4* mleaftris;
   const int4* mtris;
   const float4* mverts;
   const float4* mnorms;
@@ -139,10 +143,10 @@ struct TraceParams {
   const int* ptype;
   const float4* prims;
   int depth;
-  // triangle meshes (mcpt_upload_meshes); n_meshes == 0: none
+  // triangle meshes (mcpt_upload_meshes; layouts: SceneT); n_meshes == 0: none
   const int4* minfo;
-  const float4* mnodes;
-  const int* mleaves;
+  const float4* mpairs;
+  const float4* mleaftris;
   const int4* mtris;
   const float4* mverts;
   const float4* mnorms;

@@ -108,7 +108,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
   }
   const int y = live ? p.rows[lr] : 0;   // this shard's local row -> image row (mcpt_set_target*)
 
-  SceneT<MESH, LDSS> s{p.nodes, p.leaves, p.ptype, p.prims, p.depth, p.minfo, p.mnodes, p.mleaves, p.mtris,
+  SceneT<MESH, LDSS> s{p.nodes, p.leaves, p.ptype, p.prims, p.depth, p.minfo, p.mpairs, p.mleaftris, p.mtris,
                        p.mverts, p.mnorms, p.flat_face};
   if constexpr (LDSS) {
     // staged layout: nodes (3 float4 each), prims (8 float4 each), leaves, type codes
@@ -530,7 +530,7 @@ template <bool ANY, bool MESH>
 __global__ __launch_bounds__(256) void trace_kernel(TraceParams q) {
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   if (i >= q.n) return;
-  SceneT<MESH> s{q.nodes, q.leaves, q.ptype, q.prims, q.depth, q.minfo, q.mnodes, q.mleaves, q.mtris, q.mverts,
+  SceneT<MESH> s{q.nodes, q.leaves, q.ptype, q.prims, q.depth, q.minfo, q.mpairs, q.mleaftris, q.mtris, q.mverts,
                  q.mnorms, q.flat_face};
   Ev<false> ev;
   const f3 O = mk(q.orig[3 * i], q.orig[3 * i + 1], q.orig[3 * i + 2]);

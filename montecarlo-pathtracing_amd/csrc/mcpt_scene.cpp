@@ -22,6 +22,9 @@
 
 #include "../../include/mcpt.h"
 
+// mcpt_capi.hip: an error return without a detail (drops the thread's unread detail)
+int mcpt_err_bare(int status);
+
 namespace mcpt {
 namespace host {
 
@@ -208,7 +211,7 @@ class PrimScene {
 
   int finalize() {   // BVH_GPU_Scene::finalize + BVH_KDtree::init/compute
     int n = count();
-    if (n <= 0) return MCPT_ERR_BAD_SCENE;
+    if (n <= 0) return mcpt_err_bare(MCPT_ERR_BAD_SCENE);
     nb_emissive = emissive_first();
     std::vector<Vec3> centre(n);
     std::vector<float> box((size_t)n * 6);
@@ -487,7 +490,7 @@ static int build_reference(PrimScene& sc, int id, float li) {
       break;
     }
     default:
-      return MCPT_ERR_INVALID_ARG;
+      return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   }
   return sc.finalize();
 }
@@ -559,17 +562,17 @@ static bool unpack(const float* trf16, const float* m7, Mat4& t, Material& m) {
 extern "C" {
 
 int mcpt_scene_create(mcpt_scene** out) {
-  if (!out) return MCPT_ERR_INVALID_ARG;
+  if (!out) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   *out = new (std::nothrow) mcpt_scene();
   return *out ? MCPT_OK : MCPT_ERR_INVALID_ARG;
 }
 int mcpt_scene_destroy(mcpt_scene* s) { delete s; return MCPT_OK; }
-int mcpt_scene_clear(mcpt_scene* s) { if (!s) return MCPT_ERR_INVALID_ARG; s->s.clear(); return MCPT_OK; }
+int mcpt_scene_clear(mcpt_scene* s) { if (!s) return mcpt_err_bare(MCPT_ERR_INVALID_ARG); s->s.clear(); return MCPT_OK; }
 
 #define MCPT_ADD(NAME, METHOD)                                                  \
   int NAME(mcpt_scene* s, const float* trf16, const float* m7) {                \
     Mat4 t; Material m;                                                         \
-    if (!s || !unpack(trf16, m7, t, m)) return MCPT_ERR_INVALID_ARG;            \
+    if (!s || !unpack(trf16, m7, t, m)) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);            \
     return s->s.METHOD(t, m) >= 0 ? MCPT_OK : MCPT_ERR_INVALID_ARG;             \
   }
 MCPT_ADD(mcpt_scene_add_sphere, sphere)
@@ -581,19 +584,19 @@ MCPT_ADD(mcpt_scene_add_oriented_quad, quad)
 
 int mcpt_scene_add_mesh(mcpt_scene* s, const float* vertices, const float* normals, int n_vertices,
                         const unsigned* tri_indices, int n_triangles, const float* bb6, int* mesh_id) {
-  if (!s) return MCPT_ERR_INVALID_ARG;
+  if (!s) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   int id = s->s.add_mesh(vertices, normals, n_vertices, tri_indices, n_triangles, bb6);
-  if (id < 0) return MCPT_ERR_INVALID_ARG;
+  if (id < 0) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   if (mesh_id) *mesh_id = id;
   return MCPT_OK;
 }
 int mcpt_scene_place_mesh(mcpt_scene* s, int mesh_id, const float* trf16, const float* m7) {
   Mat4 t; Material m;
-  if (!s || !unpack(trf16, m7, t, m)) return MCPT_ERR_INVALID_ARG;
+  if (!s || !unpack(trf16, m7, t, m)) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   return s->s.place_mesh(mesh_id, t, m) >= 0 ? MCPT_OK : MCPT_ERR_INVALID_ARG;
 }
 int mcpt_scene_mesh_sizes(mcpt_scene* s, int* n_meshes, int* n_nodes, int* n_leaves, int* n_tris, int* n_verts) {
-  if (!s || !n_meshes || !n_nodes || !n_leaves || !n_tris || !n_verts) return MCPT_ERR_INVALID_ARG;
+  if (!s || !n_meshes || !n_nodes || !n_leaves || !n_tris || !n_verts) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   *n_meshes = (int)s->s.meshes.size();
   *n_nodes = *n_leaves = *n_tris = *n_verts = 0;
   for (const auto& m : s->s.meshes) {
@@ -606,7 +609,7 @@ int mcpt_scene_mesh_sizes(mcpt_scene* s, int* n_meshes, int* n_nodes, int* n_lea
 }
 int mcpt_scene_get_mesh_buffers(mcpt_scene* s, int* info, float* nodes, int* leaves, int* tris, float* verts,
                                 float* normals) {
-  if (!s) return MCPT_ERR_INVALID_ARG;
+  if (!s) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   int no = 0, lo = 0, to = 0, vo = 0, k = 0;
   for (const auto& m : s->s.meshes) {
     if (info) { info[4 * k] = no; info[4 * k + 1] = lo; info[4 * k + 2] = m.depth; info[4 * k + 3] = to; }
@@ -624,41 +627,41 @@ int mcpt_scene_get_mesh_buffers(mcpt_scene* s, int* info, float* nodes, int* lea
 }
 
 int mcpt_scene_finalize(mcpt_scene* s) { return s ? s->s.finalize() : MCPT_ERR_INVALID_ARG; }
-int mcpt_scene_nb_prim(mcpt_scene* s, int* n) { if (!s || !n) return MCPT_ERR_INVALID_ARG; *n = s->s.count(); return MCPT_OK; }
+int mcpt_scene_nb_prim(mcpt_scene* s, int* n) { if (!s || !n) return mcpt_err_bare(MCPT_ERR_INVALID_ARG); *n = s->s.count(); return MCPT_OK; }
 int mcpt_scene_depth(mcpt_scene* s, int* d) {
-  if (!s || !d) return MCPT_ERR_INVALID_ARG;
-  if (!s->s.finalized) return MCPT_ERR_NOT_FINALIZED;
+  if (!s || !d) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
+  if (!s->s.finalized) return mcpt_err_bare(MCPT_ERR_NOT_FINALIZED);
   *d = s->s.depth; return MCPT_OK;
 }
 int mcpt_scene_nb_emissives(mcpt_scene* s, int* n) {
-  if (!s || !n) return MCPT_ERR_INVALID_ARG;
-  if (!s->s.finalized) return MCPT_ERR_NOT_FINALIZED;
+  if (!s || !n) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
+  if (!s->s.finalized) return mcpt_err_bare(MCPT_ERR_NOT_FINALIZED);
   *n = s->s.nb_emissive; return MCPT_OK;
 }
 int mcpt_scene_get_buffers(mcpt_scene* s, float* prims, float* nodes, int* leaves) {
-  if (!s) return MCPT_ERR_INVALID_ARG;
-  if (!s->s.finalized) return MCPT_ERR_NOT_FINALIZED;
+  if (!s) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
+  if (!s->s.finalized) return mcpt_err_bare(MCPT_ERR_NOT_FINALIZED);
   if (prims) std::memcpy(prims, s->s.records.data(), s->s.records.size() * 4);
   if (nodes) std::memcpy(nodes, s->s.nodes.data(), s->s.nodes.size() * 4);
   if (leaves) std::memcpy(leaves, s->s.leaves.data(), s->s.leaves.size() * 4);
   return MCPT_OK;
 }
 int mcpt_scene_set_material(mcpt_scene* s, int prim, const float* m7) {
-  if (!s || !m7 || prim < 0 || prim >= s->s.count()) return MCPT_ERR_INVALID_ARG;
-  if (!s->s.finalized) return MCPT_ERR_NOT_FINALIZED;
+  if (!s || !m7 || prim < 0 || prim >= s->s.count()) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
+  if (!s->s.finalized) return mcpt_err_bare(MCPT_ERR_NOT_FINALIZED);
   float* r = s->s.rec(prim);
   const bool was_emissive = r[58] > 0.0f, is_emissive = m7[6] > 0.0f;
-  if (was_emissive != is_emissive) return MCPT_ERR_INVALID_ARG;
+  if (was_emissive != is_emissive) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   std::memcpy(r + 52, m7, 16);
   r[56] = m7[4]; r[57] = m7[5]; r[58] = m7[6];
   return MCPT_OK;
 }
 int mcpt_scene_build_reference(mcpt_scene* s, int scene_id, float light_intensity) {
-  if (!s) return MCPT_ERR_INVALID_ARG;
+  if (!s) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   return mcpt::host::build_reference(s->s, scene_id, light_intensity);
 }
 int mcpt_camera_canonical(int W, int H, float* invPV16, float* invV16) {
-  if (W <= 0 || H <= 0 || !invPV16 || !invV16) return MCPT_ERR_INVALID_ARG;
+  if (W <= 0 || H <= 0 || !invPV16 || !invV16) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   mcpt::host::canonical_camera(W, H, invPV16, invV16);
   return MCPT_OK;
 }

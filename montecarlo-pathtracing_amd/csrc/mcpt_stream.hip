@@ -167,7 +167,7 @@ __global__ __launch_bounds__(TraceCfg<LDSN>::kBlock, TraceCfg<LDSN>::kMinWaves) 
   typedef TraceCfg<LDSN> C;
   constexpr int kChunkT = C::kChunk;
   const RenderParams& p = q.r;
-  SceneT<false, false> s{p.nodes, p.leaves, p.ptype, p.prims, p.depth, p.minfo, p.mnodes, p.mleaves,
+  SceneT<false, false> s{p.nodes, p.leaves, p.ptype, p.prims, p.depth, p.minfo, p.mpairs, p.mleaftris,
                          p.mtris, p.mverts, p.mnorms, p.flat_face};
   if constexpr (LDSN) {
     extern __shared__ float4 s_bvh[];
@@ -305,7 +305,7 @@ __global__ __launch_bounds__(TraceCfg<LDSN>::kBlock, TraceCfg<LDSN>::kMinWaves) 
 __device__ __forceinline__ bool stream_shade(const StreamParams& q, const Cols& Qi, uint32_t i, const SlotCols& Sl,
                                              int slot, Payload& out) {
   const RenderParams& p = q.r;
-  const SceneT<false, false> s{p.nodes, p.leaves, p.ptype, p.prims, p.depth, p.minfo, p.mnodes, p.mleaves,
+  const SceneT<false, false> s{p.nodes, p.leaves, p.ptype, p.prims, p.depth, p.minfo, p.mpairs, p.mleaftris,
                                p.mtris, p.mverts, p.mnorms, p.flat_face};
   Ev<false> ev;
   ev.init();

@@ -88,7 +88,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "mcpt_render": (i, [_vp, fp, fp, i, i, f, i, f, i]),
         "mcpt_render_counted": (i, [_vp, fp, fp, i, i, f, i, f, i, _c_u64_p]),
         "mcpt_event_bytes": (i, [i]),
-        "mcpt_debug_counters": (i, [_vp, _c_u64_p, i]),
+        "mcpt_debug_counters": (i, [_vp, _c_u64_p, i, i]),
         "mcpt_read_accum": (i, [_vp, fp, ip]),
         "mcpt_clear_accum": (i, [_vp]),
         "mcpt_accum_device_ptr": (i, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(ctypes.c_size_t)]),
@@ -525,7 +525,7 @@ class Renderer:
     def debug_counters(self, reset: bool = True) -> np.ndarray:
         """The context's MCPT_DEBUG_SLOTS device counter slots (diagnostic builds write there)."""
         out = np.zeros(DEBUG_SLOTS, np.uint64)
-        _check(lib().mcpt_debug_counters(self._h, out.ctypes.data_as(_c_u64_p), int(reset)),
+        _check(lib().mcpt_debug_counters(self._h, out.ctypes.data_as(_c_u64_p), out.size, int(reset)),
                "mcpt_debug_counters")
         return out
 

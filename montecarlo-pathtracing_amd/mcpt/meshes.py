@@ -15,7 +15,7 @@ from __future__ import annotations
 
 import numpy as np
 
-__all__ = ["cube", "uv_sphere", "torus"]
+__all__ = ["cube", "uv_sphere", "torus", "big_mesh_scene"]
 
 
 def cube():
@@ -36,17 +36,21 @@ def uv_sphere(n_lon: int = 24, n_lat: int = 12):
     ph = np.linspace(0.0, 2.0 * np.pi, n_lon + 1)
     T, Pp = np.meshgrid(th, ph, indexing="ij")
     pos = np.stack([np.sin(T) * np.cos(Pp), np.sin(T) * np.sin(Pp), np.cos(T)], -1).reshape(-1, 3)
-    tris = []
+    # per (latitude band i, longitude j): the quad's upper triangle (a, c, b) unless i is the
+    # first band, then its lower triangle (b, c, d) unless i is the last band, bands in order
     w = n_lon + 1
-    for i in range(n_lat):
-        for j in range(n_lon):
-            a, b, c, d = i * w + j, i * w + j + 1, (i + 1) * w + j, (i + 1) * w + j + 1
-            if i > 0:
-                tris.append((a, c, b))
-            if i < n_lat - 1:
-                tris.append((b, c, d))
+    i, j = np.meshgrid(np.arange(n_lat, dtype=np.int64), np.arange(n_lon, dtype=np.int64), indexing="ij")
+    a, b = i * w + j, i * w + j + 1
+    c, d = a + w, b + w
+    up = np.stack([a, c, b], -1)
+    lo = np.stack([b, c, d], -1)
+    both = np.stack([up, lo], 2)                       # (n_lat, n_lon, 2, 3), in emission order
+    keep = np.ones((n_lat, n_lon, 2), bool)
+    keep[0, :, 0] = False                              # no upper triangle at the north pole
+    keep[n_lat - 1, :, 1] = False                      # no lower triangle at the south pole
+    tris = both[keep].astype(np.uint32)
     pos = pos.astype(np.float32)
-    return pos, pos.copy(), np.array(tris, np.uint32), np.array([-1, -1, -1, 1, 1, 1], np.float32)
+    return pos, pos.copy(), tris.reshape(-1, 3), np.array([-1, -1, -1, 1, 1, 1], np.float32)
 
 
 def torus(n_major: int = 32, n_minor: int = 16, r: float = 0.35):
@@ -66,3 +70,26 @@ def torus(n_major: int = 32, n_minor: int = 16, r: float = 0.35):
     bb = np.array([-1 - r, -1 - r, -r, 1 + r, 1 + r, r], np.float32)
     return (pos.reshape(-1, 3).astype(np.float32), nrm.reshape(-1, 3).astype(np.float32),
             np.array(tris, np.uint32), bb)
+
+
+def big_mesh_scene(n_tris: int = 1_000_000, mcpt_mod=None):
+    """The HBM-sized mesh workload (bench.py --config mesh, tools/big_mesh_bench.py): a
+    500x500 ground cube, two instances of one UV sphere of about `n_tris` triangles (mesh BVH
+    depth 20 at 1 M: 2^21 - 1 mesh nodes), a small transparent sphere and a light quad.
+    Returns (finalized Scene, triangles per instance)."""
+    import mcpt as m
+    m = mcpt_mod or m
+    # uv_sphere(n_lon, n_lat) has 2 n_lon (n_lat - 1) triangles; n_lon = 2 n_lat
+    n_lat = max(3, int(round((n_tris / 4.0) ** 0.5)))
+    v, n, t, bb = uv_sphere(2 * n_lat, n_lat)
+    T, M = m.Transfo, m.material
+    s = m.Scene()
+    s.add_cube(T.mul(T.translate(0, 0, -51), T.scale(500, 500, 1)), M([0.9, 0.9, 0.9, 1], 0.3, 0.95))
+    mid = s.add_mesh(v, n, t, bb)
+    s.place_mesh(mid, T.mul(T.translate(60, -20, 0), T.scale(45)), M([0.1, 0.9, 0.9, 0.4], 0.7, 0.9))
+    s.place_mesh(mid, T.mul(T.translate(-70, 40, 10), T.scale(35)), M([0.9, 0.3, 0.1, 1], 0.5, 0.8))
+    s.add_sphere(T.mul(T.translate(0, 0, 20), T.scale(20)), M([0.9, 0, 0.9, 0.2], 0.6, 0.7))
+    s.add_oriented_quad(T.mul(T.translate(0, 0, 160), T.rotateX(180), T.scale(70, 70, 1)),
+                        m.light([0.9, 0.9, 0.9, 1], 24))
+    s.finalize()
+    return s, len(t)

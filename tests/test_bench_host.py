@@ -145,18 +145,95 @@ def test_host_cpu_statement():
     assert q is None or q > 0
 
 
-def test_cpu_baseline_uses_available_cores():
-    """The CPU baseline runs one worker per CPU of the process's affinity mask (verdict r03:
-    not OMP_NUM_THREADS) and states it with the cgroup quota; a bounded C1 sample keeps this a
-    quick CPU test."""
+def test_cpu_baseline_reports_the_faster_run(monkeypatch):
+    """The CPU baseline runs one worker per CPU of the affinity mask and, when the cgroup quota
+    grants fewer CPUs' time, one per granted CPU; `value` is the faster run, `cores` its thread
+    count, the other run beside it (verdict r04 #4, advisor r04).  A bounded C1 sample keeps this
+    a quick CPU test."""
     args = bench.parse(["--config", "c1"])
     cb = bench.cpu_baseline(args, 0.2)
     avail = len(os.sched_getaffinity(0))
-    assert cb["threads_used"] == cb["cores"] == cb["cores_available"] == avail
-    assert cb["cgroup_cpu_quota"] == bench.cpu_quota()
-    assert cb["value"] > 0 and cb["kind"] == "port"
-    c1 = bench.cpu_baseline(args, 0.2, threads=1)
-    assert c1["threads_used"] == 1
+    assert cb["cores_available"] == avail and cb["cgroup_cpu_quota"] == bench.cpu_quota()
+    assert cb["threads_used"] == cb["cores"] and cb["value"] > 0 and cb["kind"] == "port"
+    assert "primary hit" in cb["algorithm_note"]
+    # a quota below the mask: two runs, the faster one is the value
+    fake = {2: 5.0, 1: 7.0}
+    monkeypatch.setattr(bench, "cpus_available", lambda: 2)
+    monkeypatch.setattr(bench, "cpu_quota", lambda: 1.0)
+    monkeypatch.setattr(bench, "cpu_baseline_run",
+                        lambda a, s, rough=None, threads=None, scene=None:
+                        {"value": fake[threads], "threads": threads, "sample": f"t{threads}", "nproc": 2, "model": "x"})
+    cb = bench.cpu_baseline(args, 1.0)
+    assert cb["value"] == 7.0 and cb["cores"] == 1 and cb["threads_used"] == 1
+    assert cb["other_runs"] == [{"threads": 2, "value": 5.0, "sample": "t2"}]
+    fake[2] = 9.0
+    cb = bench.cpu_baseline(args, 1.0)
+    assert cb["value"] == 9.0 and cb["cores"] == 2 and cb["other_runs"][0]["threads"] == 1
+
+
+def test_stall_report_names_least_advanced_rank():
+    import time
+    now = time.time()
+    last = {0: ("stats", now), 1: ("timed", now - 5), 2: ("stats", now)}
+    rep = bench.stall_report(last, {1, 2}, 3)
+    assert "Stalled: rank(s) 1 in phase timed (next: stats)" in rep
+    assert "rank 0 exited, last phase stats" in rep and "rank 1 running" in rep
+    rep = bench.stall_report({0: ("auto", now)}, {0, 1}, 2)      # rank 1 never stamped
+    assert "Stalled: rank(s) 1 in phase (no stamp yet)" in rep
+    assert bench.parse_stamp("bench-phase rank=3 phase=gather t=1.5") == (3, "gather")
+    assert bench.parse_stamp("other line") is None
+
+
+def _drill_env():
+    env = dict(os.environ, MCPT_DIST_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    return env
+
+
+def test_drill_stalled_rank_is_named_within_the_deadline():
+    """Verdict r04 #2: `bench.py --gpus 2` with one rank stalling before a phase exits non-zero
+    inside its deadline and names that rank and phase (gloo, CPU only: --drill-stall walks the
+    phases with collectives and no GPU work)."""
+    import subprocess
+    import time
+    t0 = time.time()
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--deadline", "15",
+                        "--drill-stall", "1:stats"], env=_drill_env(), capture_output=True, text=True, timeout=120)
+    dt = time.time() - t0
+    assert p.returncode != 0 and "{" not in p.stdout         # no result line
+    assert dt < 15 + 15 + 20, dt
+    assert "Stalled: rank(s) 1 in phase timed (next: stats)" in p.stderr, p.stderr[-2000:]
+    assert "bench-phase rank=0 phase=stats" in p.stderr
+
+
+def test_drill_success_relays_the_line():
+    import subprocess
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--deadline", "60",
+                        "--drill-stall", "1:cpu_baseline:0.2"], env=_drill_env(), capture_output=True, text=True,
+                       timeout=120)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads(p.stdout.strip().splitlines()[-1])
+    assert d["drill"] is True and d["n_gpus"] == 2
+    assert p.stderr.count("phase=done") == 2
+
+
+def test_drill_rank_deadline_under_torchrun():
+    """Launched by torch.distributed.run (the driver's N-GPU command), a rank past --deadline
+    names its phase and exits 124 by itself."""
+    import subprocess
+    import time
+    t0 = time.time()
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(bench.free_port()),
+                        os.path.join(REPO, "bench.py"), "--gpus", "2", "--deadline", "10", "--drill-stall",
+                        "0:count"], env=_drill_env(), capture_output=True, text=True, timeout=150)
+    assert p.returncode != 0
+    assert time.time() - t0 < 90
+    # whichever rank's watchdog fires first names its phase: rank 0 sleeps before `count` (its
+    # phase: stats), rank 1 waits for it in the `count` barrier
+    import re
+    assert re.search(r"bench rank (0: deadline 10 s reached in phase stats|1: deadline 10 s reached in phase count)",
+                     p.stderr), p.stderr[-2000:]
 
 
 def test_cpu_threads_capped_by_quota(monkeypatch):

@@ -8,10 +8,13 @@ polynomials (raytracer_func.frag:322-338, tp/montecarlo.frag:63-88, 134).  Diagn
 with those instructions (mcpt_math.h MCPT_DRIVER_MATH: 1 roots, 2 transcendentals, 4 division, 7
 all) render the C2 frame (scene 6, 1080p, 256 spp, B 8) and the C3 frame (1,024 spp, IOR 1.5,
 roughness 0.5) with the same seeds as the shipped build; per-pixel max / mean |delta| of the
-averaged RGB and the share of pixels over the north star's 1e-3 bar go to
-profiles/r04_parity_gpu_math.json, for the whole frame and for the 64x48 crop of
+averaged RGB and the share of pixels over the north star's 1e-3 bar are written (as
+profiles/r04_parity_gpu_math.json records them) to $MCPT_PROFILE_OUT/r04_parity_gpu_math.json when
+that is set, else under the test's tmp_path, for the whole frame and for the 64x48 crop of
 tests/test_oracle_variants.py.  The shipped build's crop is checked bit for bit against the
-oracle first, so the baseline is the contract.  A measurement, not a pass/fail of the bar.
+oracle first, so the baseline is the contract.  A measurement of the bar, not a pass/fail of
+it; the test asserts that the deviation stays within the bounds recorded in round 4 (mean
+|delta| 2e-6..6e-6, at most 0.039 % of the pixels over 1e-3, max 0.098), with margin.
 """
 import json
 import os
@@ -26,8 +29,9 @@ pytestmark = pytest.mark.gpu
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 VARIANTS = os.path.join(REPO, "montecarlo-pathtracing_amd", "mcpt", "variants")
 SCRIPT = os.path.join(REPO, "tools", "driver_math_render.py")
-# (on a gpurun box only gpurun_out/ comes back: MCPT_PROFILE_OUT redirects the file there)
-OUT = os.path.join(os.environ.get("MCPT_PROFILE_OUT", os.path.join(REPO, "profiles")), "r04_parity_gpu_math.json")
+# the record is written only where asked (MCPT_PROFILE_OUT, e.g. gpurun_out/...), never over the
+# committed profiles/r04_parity_gpu_math.json
+OUT_NAME = "r04_parity_gpu_math.json"
 BUILDS = {"roots": 1, "transcendentals": 2, "division": 4, "all": 7}
 CROP = (928, 520, 64, 48)   # tests/test_oracle_variants.py: x0, y0 (row 0 = bottom), w, h
 BAR = 1e-3
@@ -81,9 +85,14 @@ def test_driver_math_deviation(oracle_mod, tmp_path):
     result["bar_holds_on_every_pixel"] = {
         name: all(e[c]["frame"]["frac_pixels_over_1e-3"] == 0.0 for c in ("C2", "C3"))
         for name, e in result["builds"].items()}
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    with open(OUT, "w") as f:
+    out_dir = os.environ.get("MCPT_PROFILE_OUT") or str(tmp_path)
+    os.makedirs(out_dir, exist_ok=True)
+    with open(os.path.join(out_dir, OUT_NAME), "w") as f:
         json.dump(result, f, indent=1)
-    for e in result["builds"].values():
+    for name, e in result["builds"].items():
         for c in ("C2", "C3"):
-            assert np.isfinite(e[c]["frame"]["mean_abs"])
+            fr = e[c]["frame"]
+            assert np.isfinite(fr["mean_abs"]) and fr["mean_abs"] < 1e-4, (name, c, fr)
+            assert fr["frac_pixels_over_1e-3"] < 0.005, (name, c, fr)     # recorded <= 0.00039
+            assert fr["max_abs"] < 1.0, (name, c, fr)                     # recorded <= 0.098
+            assert fr["pixels_identical_frac"] < 1.0, (name, c, fr)       # the diagnostic build did differ

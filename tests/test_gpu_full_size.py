@@ -105,3 +105,31 @@ def test_c2_shards_cover_frame(mcpt_mod, renderer):
         seen[rows] = True
         assert np.array_equal(bits(part), bits(full[rows]))
     assert seen.all()
+
+
+@pytest.fixture(scope="module")
+def big_mesh(mcpt_mod):
+    from mcpt import meshes
+    return meshes.big_mesh_scene(1_000_000)[0]
+
+
+@pytest.mark.parametrize("traversal", [0, 1])
+def test_mesh_1m_rows(mcpt_mod, oracle_mod, renderer, big_mesh, traversal):
+    """The HBM-sized mesh workload (bench.py --config mesh: two instances of a 1 M-triangle UV
+    sphere, mesh BVH depth 20), 1080p, B 8, against the oracle's own mesh DFS on a row subset."""
+    sc = big_mesh
+    W, H, S, B = 1920, 1080, 2, 8
+    renderer.set_traversal(traversal)
+    try:
+        img = render(mcpt_mod, renderer, sc, W, H, 1, S, B)
+    finally:
+        renderer.set_traversal(0)
+    rows = np.arange(7, H, 149)
+    prims, nodes, leaves = sc.buffers()
+    ipv, iv = oracle_mod.camera(W, H)
+    mv = oracle_mod.MeshView(sc.mesh_buffers())
+    for y in rows:
+        ref, _ = oracle_mod.render(prims, nodes, leaves, sc.depth(), ipv, iv, W, H, 1, S, 0.0, B, 1.0, 0,
+                                   row_step=H, row_offset=int(y), meshes=mv)
+        assert np.array_equal(bits(img[y]), bits(ref[int(y)])), f"1 M-triangle mesh scene row {y}"
+    assert np.isfinite(img).all()

@@ -24,23 +24,6 @@ import mcpt  # noqa: E402
 from mcpt import meshes  # noqa: E402
 
 
-def big_mesh_scene(n_tris: int):
-    # uv_sphere(n_lon, n_lat) has 2 n_lon (n_lat - 1) triangles; n_lon = 2 n_lat
-    n_lat = max(3, int(round((n_tris / 4.0) ** 0.5)))
-    v, n, t, bb = meshes.uv_sphere(2 * n_lat, n_lat)
-    T, M = mcpt.Transfo, mcpt.material
-    s = mcpt.Scene()
-    s.add_cube(T.mul(T.translate(0, 0, -51), T.scale(500, 500, 1)), M([0.9, 0.9, 0.9, 1], 0.3, 0.95))
-    mid = s.add_mesh(v, n, t, bb)
-    s.place_mesh(mid, T.mul(T.translate(60, -20, 0), T.scale(45)), M([0.1, 0.9, 0.9, 0.4], 0.7, 0.9))
-    s.place_mesh(mid, T.mul(T.translate(-70, 40, 10), T.scale(35)), M([0.9, 0.3, 0.1, 1], 0.5, 0.8))
-    s.add_sphere(T.mul(T.translate(0, 0, 20), T.scale(20)), M([0.9, 0, 0.9, 0.2], 0.6, 0.7))
-    s.add_oriented_quad(T.mul(T.translate(0, 0, 160), T.rotateX(180), T.scale(70, 70, 1)),
-                        mcpt.light([0.9, 0.9, 0.9, 1], 24))
-    s.finalize()
-    return s, len(t)
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sizes", type=int, nargs="+", default=[10_000, 100_000, 1_000_000])
@@ -55,7 +38,7 @@ def main():
     ipv, iv = mcpt.camera_canonical(W, H)
     eb = mcpt.Renderer.event_bytes()
     for n in a.sizes:
-        sc, n_tris = big_mesh_scene(n)
+        sc, n_tris = meshes.big_mesh_scene(n)
         r.upload_scene(sc)
         mb = sc.mesh_buffers()
         mesh_mb = sum(x.nbytes for x in mb.values()) / 1e6
