@@ -207,7 +207,7 @@ int mcpt_get_schedule(mcpt_ctx* ctx, int* traversal, int* seg_per_item, int* set
 
 /* Per-lane walks (MCPT_TRAVERSAL_LANE): the wave suspends its BVH walk loop once at most
  * `lanes` lanes are still walking, shades the finished lanes and resumes the rest with
- * their next rays (0 = never suspend; -1 = default: 40 with mesh instances, 16 for BVH
+ * their next rays (0 = never suspend; -1 = default: 24 with mesh instances, 16 for BVH
  * depth >= 8, else 0).  Same
  * results for every value; a scheduling knob.  mcpt_get_walk_exit reports the value used. */
 int mcpt_set_walk_exit(mcpt_ctx* ctx, int lanes);

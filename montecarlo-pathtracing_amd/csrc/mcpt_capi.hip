@@ -181,9 +181,11 @@ static int env_int(const char* name, int dflt) {
 static int resolve_walk_exit(const mcpt_ctx* c) {
   if (c->walk_exit >= 0) return c->walk_exit;
   // mesh scenes: a lane's walk includes its instances' mesh DFSs (walk_run_mesh), long and
-  // very unequal across lanes: leaving the loop once 24 lanes are done more than doubles
-  // throughput (1 M-triangle meshes 173 -> 381 Msamples/s, tools/big_mesh_bench.py)
-  if (c->n_meshes > 0) return 40;
+  // very unequal across lanes: leaving the loop once 24 lanes are done more than doubled
+  // throughput in round 1 (1 M-triangle meshes 173 -> 381 Msamples/s, walk exit 40); with the
+  // one-fetch mesh records of round 5, exit 24 (40 lanes done) measures best (24 / 32 / 40 / 48:
+  // 840 / 784 / 760 / 691 Msamples/s, profiles/r05_ab_mesh_walk_exit.jsonl)
+  if (c->n_meshes > 0) return 24;
   return c->depth >= 8 ? 16 : 0;
 }
 static int resolve_leaf_batch(const mcpt_ctx* c) {
@@ -489,10 +491,11 @@ static void pack_mesh_pairs(const float* nodes, const int* leaves, int depth, fl
   for (int i = 0; i + 1 < n_leaf; ++i) {   // internal nodes 0 .. n_leaf - 2
     const float4* l = &rec[(size_t)(2 * i + 1) * 3];
     const float4* r = &rec[(size_t)(2 * i + 2) * 3];
-    out[(size_t)i * 4 + 0] = l[0];
-    out[(size_t)i * 4 + 1] = make_float4(l[1].x, l[1].y, l[1].z, 0.0f);
-    out[(size_t)i * 4 + 2] = r[0];
-    out[(size_t)i * 4 + 3] = make_float4(r[1].x, r[1].y, r[1].z, 0.0f);
+    float4* o = out + (size_t)mcpt::mesh_pair_slot((unsigned)i) * 4;
+    o[0] = l[0];
+    o[1] = make_float4(l[1].x, l[1].y, l[1].z, 0.0f);
+    o[2] = r[0];
+    o[3] = make_float4(r[1].x, r[1].y, r[1].z, 0.0f);
   }
 }
 
@@ -514,9 +517,19 @@ int mcpt_upload_meshes(mcpt_ctx* c, int n_meshes, const int* info, int n_nodes, 
     return set_err(MCPT_ERR_INVALID_ARG, "mcpt_upload_meshes: bad arguments");
   // validate the layout: each mesh's BVH within the node / leaf arrays, leaf triangle ids
   // within the mesh's triangles, vertex ids within the vertex array
-  // pair records indexed by the global node index (a mesh's leaf slots stay unused) and
-  // leaf triangle records indexed by the global leaf index
-  std::vector<float4> hn((size_t)n_nodes * 4, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+  // pair records: each mesh's in its own run of slots (mesh_pair_slot), the run starting at an
+  // even slot so that two-slot lines are 128-byte aligned; leaf triangle records indexed by the
+  // global leaf index
+  std::vector<unsigned> pair_base(n_meshes);
+  size_t n_slots = 0;
+  for (int m = 0; m < n_meshes; ++m) {
+    const int d = info[4 * m + 2];
+    if (d < 0 || d > 24) return set_err(MCPT_ERR_BAD_SCENE, "bad mesh info");
+    pair_base[m] = (unsigned)n_slots;
+    n_slots = (n_slots + mcpt::mesh_pair_slots(d) + 1) & ~(size_t)1;
+  }
+  if (n_slots * 4 >= (size_t(1) << 31)) return set_err(MCPT_ERR_BAD_SCENE, "mesh BVHs too large");
+  std::vector<float4> hn(std::max<size_t>(n_slots, 2) * 4, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
   for (int m = 0; m < n_meshes; ++m) {
     const int no = info[4 * m], lo = info[4 * m + 1], d = info[4 * m + 2], to = info[4 * m + 3];
     if (d < 0 || d > 24 || no < 0 || lo < 0 || to < 0) return set_err(MCPT_ERR_BAD_SCENE, "bad mesh info");
@@ -526,12 +539,13 @@ int mcpt_upload_meshes(mcpt_ctx* c, int n_meshes, const int* info, int n_nodes, 
     if (nt <= 0 || to + nt > n_tris) return set_err(MCPT_ERR_BAD_SCENE, "mesh triangles out of range");
     for (int k = 0; k < nl; ++k)
       if (leaves[lo + k] < -1 || leaves[lo + k] >= nt) return set_err(MCPT_ERR_BAD_SCENE, "mesh leaf id out of range");
-    pack_mesh_pairs(nodes + (size_t)no * 6, leaves + lo, d, &hn[(size_t)no * 4]);
+    pack_mesh_pairs(nodes + (size_t)no * 6, leaves + lo, d, &hn[(size_t)pair_base[m] * 4]);
   }
   for (int id : c->mesh_ids)
     if (id >= n_meshes) return set_err(MCPT_ERR_BAD_SCENE, "mesh instance refers to a missing mesh");
   std::vector<int4> hi(n_meshes), ht(n_tris);
-  for (int m = 0; m < n_meshes; ++m) hi[m] = make_int4(info[4 * m], info[4 * m + 1], info[4 * m + 2], info[4 * m + 3]);
+  // device mesh info: (first pair slot, first leaf, depth, first triangle)
+  for (int m = 0; m < n_meshes; ++m) hi[m] = make_int4((int)pair_base[m], info[4 * m + 1], info[4 * m + 2], info[4 * m + 3]);
   for (int t = 0; t < n_tris; ++t) {
     const int* v = tris + (size_t)t * 3;
     for (int k = 0; k < 3; ++k)

@@ -94,10 +94,11 @@ struct SceneT {
   const int* __restrict__ ptype;      // type code | mesh id << 4
   const float4* __restrict__ prims;   // 8 per prim: inv r0..r2, trf r0..r2, colour, material
   int depth;
-  // meshes (mcpt_upload_meshes): per mesh (first node, first leaf, depth, first triangle)
+  // meshes (mcpt_upload_meshes): per mesh (first pair slot, first leaf, depth, first triangle)
   const int4* __restrict__ minfo;
-  // mesh BVHs, mesh space: 4 rows per internal node at its global node index, both children's
-  // boxes in one 64-byte record, (c_left, has_left) (w_left, 0) (c_right, has_right) (w_right, 0)
+  // mesh BVHs, mesh space: one 64-byte slot of 4 rows per internal node (slot: mesh_pair_slot,
+  // from the mesh's first slot), both children's boxes, (c_left, has_left) (w_left, 0)
+  // (c_right, has_right) (w_right, 0)
   const float4* __restrict__ mpairs;
   // 4 rows per mesh leaf at its global leaf index: (A, t) (B - A, 0) (C - A, 0) (0) of the
   // leaf's triangle, t = the mesh-local triangle id as int bits (-1: empty leaf)
@@ -411,6 +412,8 @@ __device__ __forceinline__ void mesh_leaf(const SR& s, size_t leaf, int index, f
   const float4 r0 = q[0], r1 = q[1], r2 = q[2];
   MCPT_ROWS_IN("v"(r0.x), "v"(r0.y), "v"(r0.z), "v"(r0.w), "v"(r1.x), "v"(r1.y), "v"(r1.z), "v"(r2.x),
                "v"(r2.y), "v"(r2.z));
+  MCPT_ROWS_IN("v"(t0.x), "v"(t0.y), "v"(t0.z), "v"(t0.w), "v"(t1.x), "v"(t1.y), "v"(t1.z), "v"(t1.w),
+               "v"(t2.x), "v"(t2.y), "v"(t2.z), "v"(t2.w));
   const int t = __float_as_int(r0.w);
   if (t >= 0) tri_test<COUNT, SR>(t, r0, r1, r2, index, O, D, Ol, t0, t1, t2, h, ev);
 }
@@ -439,6 +442,8 @@ __device__ __forceinline__ void mesh_pair_tests(const SR& s, size_t node, f3 O, 
   const float4 a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
   MCPT_ROWS_IN("v"(a0.x), "v"(a0.y), "v"(a0.z), "v"(a0.w), "v"(a1.x), "v"(a1.y), "v"(a1.z));
   MCPT_ROWS_IN("v"(a2.x), "v"(a2.y), "v"(a2.z), "v"(a2.w), "v"(a3.x), "v"(a3.y), "v"(a3.z));
+  MCPT_ROWS_IN("v"(t0.x), "v"(t0.y), "v"(t0.z), "v"(t0.w), "v"(t1.x), "v"(t1.y), "v"(t1.z), "v"(t1.w),
+               "v"(t2.x), "v"(t2.y), "v"(t2.z), "v"(t2.w));
   f3 il, ir;
   rcp6_rn(a1, a3, il, ir);
   hl = (COUNT || a0.w != 0.0f) && box_test_mesh(a0, a1, il, O, D, invD, Ol, t0, t1, t2, cull2);
@@ -468,7 +473,8 @@ __device__ __forceinline__ void mesh_test(const SR& s, int mesh, int index, f3 O
       ev.inc(EV_NODE);
       const size_t j = 2 * (size_t)node + 1;
       bool hl, hr;
-      mesh_pair_tests<COUNT>(s, (size_t)mi.x + node, O, D, invD, Ol, t0, t1, t2, h.cull2, hl, hr);
+      mesh_pair_tests<COUNT>(s, (size_t)mi.x + mesh_pair_slot(node), O, D, invD, Ol, t0, t1, t2,
+                             h.cull2, hl, hr);
       pop = !(hl || hr);
       if (hr) {
         if (hl) pending |= 1u << (level + 1);
@@ -509,7 +515,9 @@ __device__ __forceinline__ float quot(float num, float den, float y, bool ok) {
 #define MCPT_ONE_ACCEPT 1
 #endif
 // intersect_prim raytracer_func.frag:681-705 + Sphere/Cube/Cylinder/Cone/OrientedQuad :398-640
-template <bool COUNT, bool UNI, bool ANY = false, class SR>
+// NOMESH: the caller handles CODE_MESH leaves itself (walk_run_mesh), so the nested mesh DFS is not
+// compiled in here
+template <bool COUNT, bool UNI, bool ANY = false, bool NOMESH = false, class SR>
 __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit& h, Ev<COUNT>& ev) {
   ev.inc(EV_PRIM);
   constexpr bool U = UNI && !SR::kLds;
@@ -643,7 +651,7 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
     }
     if (tl < kFLTMAX) accept(CODE_CONE, cl, add(O, muls(D, tl)));
   } else if (t == CODE_MESH) {
-    if constexpr (SR::kMesh) mesh_test<COUNT, ANY>(s, pt >> 4, i, O, D, Ow, h, ev);
+    if constexpr (SR::kMesh && !NOMESH) mesh_test<COUNT, ANY>(s, pt >> 4, i, O, D, Ow, h, ev);
   }
   if constexpr (kOne) {
     if (has1) accept_cand<COUNT, UNI>(s, i, shape1, dir1, P1, Ow, h, ev);
@@ -870,6 +878,9 @@ __device__ __forceinline__ bool walk_run(const SR& s, f3 O, f3 D, Hit& h, Walk& 
 // mesh-space ray (intersect_prim :681-705) and continues in the mesh until its pending mask
 // is empty, then pops the scene stack.  Each lane's sequence of box / primitive / triangle
 // tests is the reference's, in the reference's order (same bits, same event counts).
+#ifndef MCPT_MESH_TRF_RELOAD
+#define MCPT_MESH_TRF_RELOAD 1
+#endif
 template <bool COUNT, bool SUSPEND, class SR>
 __device__ __forceinline__ bool walk_run_mesh(const SR& s, f3 O, f3 D, Hit& h, Walk& w, Ev<COUNT>& ev, int exit) {
   const int leaf0 = (1 << s.depth) - 1;
@@ -879,7 +890,16 @@ __device__ __forceinline__ bool walk_run_mesh(const SR& s, f3 O, f3 D, Hit& h, W
     if (w.mprim >= 0) {
       // one step of the instance's mesh walk (mesh_test's loop body)
       const int4 mi = w.mi;
-      const float4 t0 = w.t0, t1 = w.t1, t2 = w.t2;
+      float4 t0, t1, t2;
+      if constexpr (MCPT_MESH_TRF_RELOAD) {
+        // the instance's transform rows are read again at every mesh step (L1/L2 hits, issued
+        // with the step's record) rather than held: 12 VGPRs fewer across the shading rounds
+        // that suspended walks wait through
+        const float4* tp = s.prims + (size_t)w.mprim * 8 + 3;
+        t0 = tp[0]; t1 = tp[1]; t2 = tp[2];
+      } else {
+        t0 = w.t0; t1 = w.t1; t2 = w.t2;
+      }
       const int mleaf0 = (1 << mi.z) - 1;
       bool mpop = true;
       if (w.mnode >= mleaf0) {
@@ -889,7 +909,8 @@ __device__ __forceinline__ bool walk_run_mesh(const SR& s, f3 O, f3 D, Hit& h, W
         ev.inc(EV_NODE);
         const size_t j = 2 * (size_t)w.mnode + 1;
         bool hl, hr;
-        mesh_pair_tests<COUNT>(s, (size_t)mi.x + w.mnode, w.Om, w.Dm, w.invDm, O, t0, t1, t2, h.cull2, hl, hr);
+        mesh_pair_tests<COUNT>(s, (size_t)mi.x + mesh_pair_slot(w.mnode), w.Om, w.Dm, w.invDm, O,
+                               t0, t1, t2, h.cull2, hl, hr);
         mpop = !(hl || hr);
         if (hr) {
           if (hl) w.mpending |= 1u << (w.mlevel + 1);
@@ -925,11 +946,13 @@ __device__ __forceinline__ bool walk_run_mesh(const SR& s, f3 O, f3 D, Hit& h, W
           w.Dm = wnormalize3<SR::kFastNorm>(xdir(r0, r1, r2, D));
           w.invDm = mk(rcp_rn(w.Dm.x), rcp_rn(w.Dm.y), rcp_rn(w.Dm.z));
           w.mprim = p; w.mi = s.minfo[pt >> 4];
-          w.t0 = s.prims[b + 3]; w.t1 = s.prims[b + 4]; w.t2 = s.prims[b + 5];
+          if constexpr (!MCPT_MESH_TRF_RELOAD) {
+            w.t0 = s.prims[b + 3]; w.t1 = s.prims[b + 4]; w.t2 = s.prims[b + 5];
+          }
           w.mnode = 0; w.mlevel = 0; w.mpending = 0;
           pop = false;
         } else {
-          prim_test<COUNT, false, false>(s, p, O, D, h, ev);
+          prim_test<COUNT, false, false, true>(s, p, O, D, h, ev);
         }
       }
     } else {

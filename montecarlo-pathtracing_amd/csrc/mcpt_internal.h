@@ -55,6 +55,16 @@ constexpr int kTileW = MCPT_TILE_W, kTileH = MCPT_TILE_H;
 constexpr int kTileThreads = kTileW * kTileH;
 static_assert(kTileW % 8 == 0 && kTileH % 8 == 0 && kTileThreads <= 1024, "tiles are made of 8x8 waves");
 
+// Slot of a mesh BVH internal node's child-pair record (64 B) from its mesh's first slot
+// (mcpt_upload_meshes; SceneT::mpairs): node i -> slot i + 1, so the records of two siblings
+// (2i+1, 2i+2: the left child's pending pop follows the right child's subtree) share one
+// 128-byte line.  Measured interleaved on the mesh workload (tools/ab_interleave.py,
+// profiles/r05_ab_mesh_layouts.jsonl): heap order (slot i) within noise of it, two-level
+// treelets (a node and its right child, the reference's first descent, in one line) 2-8 %
+// slower.
+__host__ __device__ inline unsigned mesh_pair_slot(unsigned i) { return i + 1u; }
+__host__ __device__ inline unsigned mesh_pair_slots(int depth) { return 1u << depth; }   // slots one mesh spans
+
 struct RenderParams {
   const float4* nodes;
   const int* leaves;

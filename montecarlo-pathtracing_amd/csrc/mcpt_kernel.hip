@@ -63,11 +63,13 @@ namespace mcpt {
 // SUSPEND: the deep-BVH walk (suspendable walks, batched leaf visits: RenderParams::walk_exit,
 // leaf_batch; walk_run)
 template <bool COUNT, bool WAVE, bool MESH, bool LDSS, bool SUSPEND>
-// per-lane walks of mesh scenes (walk_run_mesh keeps the mesh walk state, ray in mesh space
-// and instance transform in registers): 4 waves/SIMD, 128 VGPRs (tools/big_mesh_bench.py:
-// 7 waves with that state spills and runs at a third of the speed)
+// per-lane walks of mesh scenes (walk_run_mesh keeps the mesh walk state and the ray in mesh
+// space in registers; the instance transform is re-read per step): 5 waves/SIMD, 96 VGPRs and
+// 48 B of scratch, against 113 VGPRs without spills at 4 waves: the mesh workload +5..8 %
+// (round 5, profiles/r05_ab_mesh_*.jsonl; 7 waves with that state spill and run at a third of
+// the speed, round 1)
 #ifndef MCPT_MIN_WAVES_MESH
-#define MCPT_MIN_WAVES_MESH 4
+#define MCPT_MIN_WAVES_MESH 5
 #endif
 // per-lane walks over scenes read through L1/L2 (not LDS-staged: scenes 3, 5, 7, 8): 6 waves/SIMD
 // while their state spilled at 7 (profiles/r01_ab35_occupancy_v12.jsonl); with the packed hit
@@ -246,8 +248,11 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
         traverse<COUNT, WAVE>(s, O, D, h, ev);
       } else {
         if (!walking) { walk_begin<COUNT>(s, D, h, walk, ev, p.cull2_max); walking = true; }
-        if constexpr (MESH) walking = !walk_run_mesh<COUNT, SUSPEND>(s, O, D, h, walk, ev, p.walk_exit);
-        else walking = !walk_run<COUNT, SUSPEND>(s, O, D, h, walk, ev, p.walk_exit, p.leaf_batch, p.walk_min_done);
+        if constexpr (MESH) {
+          walking = !walk_run_mesh<COUNT, SUSPEND>(s, O, D, h, walk, ev, p.walk_exit);
+        } else {
+          walking = !walk_run<COUNT, SUSPEND>(s, O, D, h, walk, ev, p.walk_exit, p.leaf_batch, p.walk_min_done);
+        }
         ready = !walking;
       }
     }

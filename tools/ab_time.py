@@ -20,7 +20,7 @@ import torch  # noqa: E402,F401
 
 import mcpt  # noqa: E402
 
-BOUNCES = {1: 3, 2: 8, 3: 8, 4: 8, 5: 8, 6: 8, 7: 8, 8: 12}
+BOUNCES = {0: 8, 1: 3, 2: 8, 3: 8, 4: 8, 5: 8, 6: 8, 7: 8, 8: 12}   # scene 0: the mesh workload
 
 
 def main():
@@ -33,12 +33,17 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--tag", default=os.path.basename(mcpt.lib_path()))
     ap.add_argument("--walk-exit", type=int, nargs="+", default=[-1])
+    ap.add_argument("--mesh-tris", type=int, default=1_000_000, help="scene 0: mcpt.meshes.big_mesh_scene(N)")
     a = ap.parse_args()
     r = mcpt.Renderer(0)
     r.set_target(a.width, a.height)
     ipv, iv = mcpt.camera_canonical(a.width, a.height)
     for sid in a.scenes:
-        r.upload_scene(mcpt.Scene.reference(sid))
+        if sid == 0:
+            from mcpt import meshes
+            r.upload_scene(meshes.big_mesh_scene(a.mesh_tris)[0])
+        else:
+            r.upload_scene(mcpt.Scene.reference(sid))
         for mode, wx in [(m, w) for m in a.modes for w in (a.walk_exit if m == 1 else [-1])]:
             r.set_traversal(mode)
             if hasattr(r, "set_walk_exit"):
