@@ -89,6 +89,28 @@ def main():
         # fp32 flop upper bound (every lane active): FMA = 2, MUL / ADD = 1
         rec["f32_flop_per_launch_upper"] = 64.0 * (2 * c["SQ_INSTS_VALU_FMA_F32"] + c["SQ_INSTS_VALU_MUL_F32"] +
                                                    c["SQ_INSTS_VALU_ADD_F32"])
+    if c.get("TCP_TCC_READ_REQ_sum"):
+        # the gathers' memory hierarchy (tools/pmc.sh PMC_MEM=1 passes): L1 -> L2 read requests per
+        # VMEM read instruction, their mean latency (cycles), the L2 hit rate, fabric read requests
+        # by size and the share of them that went to DRAM (the rest: Infinity Cache hits)
+        m = {"l1_to_l2_reads": c["TCP_TCC_READ_REQ_sum"],
+             "l1_to_l2_latency_cycles": c.get("TCP_TCC_READ_REQ_LATENCY_sum", 0.0) / c["TCP_TCC_READ_REQ_sum"]}
+        if c.get("SQ_INSTS_VMEM_RD"):
+            m["l1_to_l2_reads_per_vmem_rd"] = c["TCP_TCC_READ_REQ_sum"] / c["SQ_INSTS_VMEM_RD"]
+        if c.get("TCP_TOTAL_CACHE_ACCESSES_sum"):
+            m["l1_accesses"] = c["TCP_TOTAL_CACHE_ACCESSES_sum"]
+        if c.get("TCC_HIT_sum") is not None and c.get("TCC_MISS_sum") is not None:
+            m["l2_hit_rate"] = c["TCC_HIT_sum"] / max(c["TCC_HIT_sum"] + c["TCC_MISS_sum"], 1.0)
+        if c.get("TCC_EA0_RDREQ_sum"):
+            m["fabric_reads"] = c["TCC_EA0_RDREQ_sum"]
+            m["fabric_reads_dram_frac"] = c.get("TCC_EA0_RDREQ_DRAM_sum", 0.0) / c["TCC_EA0_RDREQ_sum"]
+        if c.get("TCC_EA0_RDREQ_128B_sum") is not None:
+            m["fabric_reads_128B"] = c["TCC_EA0_RDREQ_128B_sum"]
+            m["fabric_reads_64B"] = c.get("TCC_EA0_RDREQ_64B_sum")
+            m["fabric_read_bytes_by_size"] = 128.0 * c["TCC_EA0_RDREQ_128B_sum"] + 64.0 * c.get("TCC_EA0_RDREQ_64B_sum", 0.0)
+        if c.get("TA_TA_BUSY_sum") and c.get("GRBM_GUI_ACTIVE"):
+            m["ta_busy_frac"] = c["TA_TA_BUSY_sum"] / (256 * c["GRBM_GUI_ACTIVE"] / 8.0)
+        rec["memory"] = m
     try:
         with open(out) as f:
             recs = json.load(f)["records"]
