@@ -903,7 +903,7 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   {
     const long long lds = ((3LL * ((2LL << c->depth) - 1) + (long long)mcpt::kPrimF4 * c->n_prims) * 16) +
                           (((1LL << c->depth) + c->n_prims) * 4);
-    p.lds_scene_bytes = (MCPT_LDS_SCENE && c->n_meshes == 0 && lds <= mcpt::kLdsSceneBytes) ? (int)lds : 0;
+    p.lds_scene_bytes = (MCPT_LDS_SCENE && lds <= mcpt::kLdsSceneBytes) ? (int)lds : 0;
   }
   p.minfo = c->d_minfo; p.mpairs = c->d_mpairs; p.mleaftris = c->d_mleaftris; p.mtris = c->d_mtris;
   p.mverts = c->d_mverts; p.mnorms = c->d_mnorms; p.n_meshes = c->n_meshes; p.flat_face = c->flat_face;

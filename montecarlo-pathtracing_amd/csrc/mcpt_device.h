@@ -325,15 +325,18 @@ __device__ __forceinline__ void node_tests(const SR& s, const float4* __restrict
 // intersect_bvm raytracer_func.frag:273-311: the mesh BVH's box test, in mesh space (O, D),
 // with the entry point taken to world space through the mesh transform (rows t0..t2) and
 // compared with the world distance from Ol.  Same face loop as box_test.
+// FLAT (default): no exec-mask branches, as box_test's FLAT form; the mesh workload +0.8..4 %
+// (profiles/r05_ab_mesh_flat_lds.jsonl)
+template <bool FLAT = true>
 __device__ __forceinline__ bool box_test_mesh(float4 a0, float4 a1, f3 iw, f3 O, f3 D, f3 invD, f3 Ol,
                                               float4 t0, float4 t1, float4 t2, double cull2) {
   f3 c = mk(a0.x, a0.y, a0.z), w = mk(a1.x, a1.y, a1.z);
   f3 Oi = mulv(sub(O, c), iw);
   f3 Di = mulv(D, iw);
   // all |Oi| < 1 as one compare of the NaN-propagating maximum (exact, as in box_test)
-  if (__builtin_elementwise_maximum(__builtin_elementwise_maximum(__builtin_fabsf(Oi.x), __builtin_fabsf(Oi.y)),
-                                    __builtin_fabsf(Oi.z)) < 1.0f)
-    return true;
+  const bool inside = __builtin_elementwise_maximum(__builtin_elementwise_maximum(__builtin_fabsf(Oi.x),
+                                                    __builtin_fabsf(Oi.y)), __builtin_fabsf(Oi.z)) < 1.0f;
+  if (!FLAT && inside) return true;
   f3 rD = mulv(invD, w);
   const bool dx = __builtin_fabsf(Di.x) > kEPS, dy = __builtin_fabsf(Di.y) > kEPS, dz = __builtin_fabsf(Di.z) > kEPS;
   float al = kFLTMAX;
@@ -343,6 +346,12 @@ __device__ __forceinline__ bool box_test_mesh(float4 a0, float4 a1, f3 iw, f3 O,
   al = box_face(al, 1.0f, Oi.y, dy, rD.y, Oi.z, Di.z, Oi.x, Di.x);
   al = box_face(al, -1.0f, Oi.z, dz, rD.z, Oi.x, Di.x, Oi.y, Di.y);
   al = box_face(al, 1.0f, Oi.z, dz, rD.z, Oi.x, Di.x, Oi.y, Di.y);
+  if constexpr (FLAT) {   // no exec-mask branches: the entry point's cull computed and selected
+    f3 Pl = add(Oi, muls(Di, al));
+    f3 Pg = xpoint(t0, t1, t2, add(mulv(Pl, w), c));
+    f3 v = sub(Ol, Pg);
+    return inside | ((al < kFLTMAX) & ((double)dot3(v, v) < cull2));
+  }
   if (al < kFLTMAX) {
     f3 Pl = add(Oi, muls(Di, al));
     f3 Pg = xpoint(t0, t1, t2, add(mulv(Pl, w), c));

@@ -617,15 +617,16 @@ hipError_t mcpt_launch_render(const mcpt::RenderParams& p, bool count, hipStream
   if (items <= 0) return hipSuccess;
   dim3 block(mcpt::kTileThreads), grid((unsigned)items);
   const bool wave = p.wave_traversal != 0, mesh = p.n_meshes > 0;
-  const bool lds = !mesh && p.lds_scene_bytes > 0;
+  const bool lds = p.lds_scene_bytes > 0;
   // deep-BVH walk kernel: suspendable walks and/or batched leaf visits (walk_run)
   const bool susp = !count && !wave && (p.walk_exit > 0 || p.leaf_batch > 0);
   const size_t shm = lds ? (size_t)p.lds_scene_bytes : 0;
 #define MCPT_RENDER(C, W, M, L, S) \
   hipLaunchKernelGGL((mcpt::render_kernel<C, W, M, L, S>), grid, block, shm, stream, p)
-#define MCPT_RENDER_CW(C, W, S)                       \
-  if (mesh) MCPT_RENDER(C, W, true, false, S);        \
-  else if (lds) MCPT_RENDER(C, W, false, true, S);    \
+#define MCPT_RENDER_CW(C, W, S)                              \
+  if (mesh && lds) MCPT_RENDER(C, W, true, true, S);         \
+  else if (mesh) MCPT_RENDER(C, W, true, false, S);          \
+  else if (lds) MCPT_RENDER(C, W, false, true, S);           \
   else MCPT_RENDER(C, W, false, false, S)
   if (count) {
     if (wave) { MCPT_RENDER_CW(true, true, false); } else { MCPT_RENDER_CW(true, false, false); }
