@@ -7,12 +7,16 @@
    tp/montecarlo.frag) and DESIGN.md §3, not from oracle.cpp.  fma is emulated exactly
    (double product + TwoSum + midpoint fix-up), so the vectors are bit-exact.
 2. img_s{scene}_v{variant}.npy — small accumulator images rendered by the C++ oracle
-   (regression pins for the oracle and direct fixtures for the GPU tests).
+   (regression pins for the oracle and direct fixtures for the GPU tests) on scene buffers and
+   cameras from scene_restate.py.
 3. paths.npz (`python gen_golden.py paths`) — 688 whole samples of the integrator
    ((pixel, pass) at 1080p on all eight reference scenes, 6 and 5 also at IOR 1.5, and a scene
    with the pure refraction branch; 96 of them run montecarlo_mat / montecarlo_mat_tr) from the
    same independent numpy restatement extended to the camera
-   ray, the BVH DFS, intersection_info and random_path, with the branch sequence each took.
+   ray, the BVH DFS, intersection_info and random_path, with the branch sequence each took; the
+   scene buffers, BVHs and cameras come from scene_restate.py, a numpy restatement of the host
+   producer (Transfo, PrimData, prim_bb, sortEmissiveFirst, libstdc++ nth_element, BVH_KDtree,
+   camera), so nothing of the fixture comes from oracle.cpp (round 5).
 
 The reference itself cannot run here (no GL 4.3 / Eigen / GLFW / assimp):
 parity with the executed GLSL is unpinned; these fixtures pin the restatement.
@@ -27,6 +31,8 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, REPO)
+sys.path.insert(0, HERE)
+import scene_restate  # noqa: E402  (numpy restatement of the host producer and camera)
 
 f32 = np.float32
 u32 = np.uint32
@@ -741,10 +747,11 @@ def image_name(c):
     return f"img_s{s}_v{v}_{W}x{H}_p{p}_n{n}_B{B}_ior{ior}_li{li}.npy"
 
 
-def pure_refraction_scene(orc):
+def pure_refraction_scene():
     """A scene for the refraction branch no reference scene reaches (alpha < 1, shininess 0:
     montecarlo.frag:139-146): glass sphere and cylinder over a diffuse floor, a reflective
-    cube, an emissive quad — built with the oracle's producer (scene.h add_* + finalize)."""
+    cube, an emissive quad — built with the numpy restatement of the producer (scene.h add_* +
+    finalize, scene_restate.py)."""
     def T(tx, ty, tz, sx, sy, sz):   # translate · scale, column-major
         m = np.eye(4, dtype=np.float32)
         m[0, 0], m[1, 1], m[2, 2] = sx, sy, sz
@@ -755,7 +762,7 @@ def pure_refraction_scene(orc):
            (3, T(70, 30, 0, 30, 30, 50), [0.9, 0.6, 0.6, 0.6, 0.0, 0.8, 0.0]),
            (2, T(0, 0, -60, 400, 400, 5), [0.8, 0.8, 0.8, 1.0, 0.0, 0.5, 0.0]),
            (2, T(30, -90, -20, 25, 25, 25), [0.5, 0.5, 0.9, 1.0, 0.6, 0.4, 0.0])]
-    return orc.custom_scene([(t, np.asarray(m, np.float32), np.asarray(a, np.float32)) for t, m, a in ops])
+    return scene_restate.custom([(t, np.asarray(m, np.float32), np.asarray(a, np.float32)) for t, m, a in ops])
 
 
 PATH_CASES = [  # (scene id or 0 = pure_refraction_scene, light, ior, bounces, samples)
@@ -776,16 +783,18 @@ VARIANT_CASES = [(1, 1.2, 1.0, 8, 16, 1), (6, 1.2, 1.0, 8, 16, 1), (8, 1.2, 1.0,
                  (1, 1.2, 1.0, 8, 16, 2), (6, 1.2, 1.0, 8, 16, 2), (8, 1.2, 1.0, 12, 16, 2)]
 
 
-def make_path_kat(orc, rng, cases=PATH_CASES, rng2=None, cases2=(), rng3=None, cases3=()):
+def make_path_kat(rng, cases=PATH_CASES, rng2=None, cases2=(), rng3=None, cases3=()):
     """Whole samples of the integrator (pixel, pass) at 1920×1080 with the numpy restatement
-    above: the oracle must reproduce every one bit for bit (tests/test_oracle_paths.py)."""
+    above, on scene buffers and a camera from the numpy restatement of the host producer
+    (scene_restate.py, round 5: no longer the oracle's): the oracle must reproduce every one bit
+    for bit (tests/test_oracle_paths.py)."""
     W, H = 1920, 1080
-    ipv, iv = orc.camera(W, H)
+    ipv, iv = scene_restate.camera(W, H)
     out = {k: [] for k in ("scene", "light", "ior", "bounces", "x", "y", "npass", "rgb", "trace", "variant")}
-    custom = pure_refraction_scene(orc)
+    custom = pure_refraction_scene()
     for scene_id, li, ior, B, n, variant, rng in ([c + (0, rng) for c in cases] + [c + (0, rng2) for c in cases2] +
                                                   [c + (rng3,) for c in cases3]):
-        prims, nodes, leaves, depth, _ = custom if scene_id == 0 else orc.scene(scene_id, li)
+        prims, nodes, leaves, depth, _ = custom if scene_id == 0 else scene_restate.build(scene_id, li)
         for k in range(n):
             # pixels near the image centre (objects) or anywhere; every 8th sample is drawn
             # until its path ends on an emissive primitive (at most 400 draws), so the
@@ -807,16 +816,16 @@ def make_path_kat(orc, rng, cases=PATH_CASES, rng2=None, cases2=(), rng3=None, c
     kat["path_light"] = np.array(out["light"], np.float32)
     kat["path_ior"] = np.array(out["ior"], np.float32)
     kat["path_trace"] = np.array(out["trace"], "U32")
-    kat["custom_prims"], kat["custom_nodes"], kat["custom_leaves"] = custom[0], custom[1], custom[2]
+    kat["custom_prims"], kat["custom_nodes"], kat["custom_leaves"] = custom[0], custom[1].reshape(-1), custom[2]
     kat["custom_depth"] = np.array(custom[3], np.int32)
     kat["path_W"], kat["path_H"] = np.array(W, np.int32), np.array(H, np.int32)
     return kat
 
 
 def main():
-    from oracle import oracle as orc
+    from oracle import oracle as orc   # renders the img_*.npy regression images only
     if len(sys.argv) > 1 and sys.argv[1] == "paths":   # paths.npz only (round-2 addition)
-        kat = make_path_kat(orc, np.random.default_rng(20250216), PATH_CASES,
+        kat = make_path_kat(np.random.default_rng(20250216), PATH_CASES,
                             np.random.default_rng(20251016), PATH_CASES_2,
                             np.random.default_rng(20251017), VARIANT_CASES)
         np.savez_compressed(os.path.join(HERE, "paths.npz"), **kat)
@@ -826,7 +835,7 @@ def main():
         return
     rng = np.random.default_rng(20241008)
     kat = make_kat(rng)
-    prims = [orc.scene(s)[0] for s in (1, 2, 3, 6, 8)]
+    prims = [scene_restate.build(s)[0] for s in (1, 2, 3, 6, 8)]
     prims = [p[: 24] for p in prims]
     kat.update(make_prim_kat(rng, prims))
     rng2 = np.random.default_rng(20241009)          # round-1 additions: cone + sampler
@@ -835,8 +844,8 @@ def main():
     np.savez_compressed(os.path.join(HERE, "kat.npz"), **kat)
     for c in IMAGES:
         s, v, W, H, p, n, B, ior, li = c
-        pr, nodes, leaves, d, _ = orc.scene(s, li)
-        ipv, iv = orc.camera(W, H)
+        pr, nodes, leaves, d, _ = scene_restate.build(s, li)
+        ipv, iv = scene_restate.camera(W, H)
         acc, _ = orc.render(pr, nodes, leaves, d, ipv, iv, W, H, p, n, 0.0, B, ior, v)
         np.save(os.path.join(HERE, image_name(c)), acc)
     print("wrote kat.npz and", len(IMAGES), "images")

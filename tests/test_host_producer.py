@@ -120,3 +120,79 @@ def test_camera_matches_oracle_and_geometry(mcpt_mod, oracle_mod):
     a, b = mcpt_mod.camera_canonical(1920, 1080)
     eye = b.reshape(4, 4).T @ np.array([0, 0, 0, 1.0])
     assert np.allclose(eye[:3], [0, -347.39, 61.25], atol=0.05)
+
+
+# the numpy restatement of the host producer written from the reference's C++ text
+# (tests/golden/scene_restate.py; round 5): the source of tests/golden/paths.npz' scene buffers
+# and cameras.  Product, oracle and restatement: three producers, bit for bit.
+@pytest.mark.parametrize("sid", sorted(SCENES))
+def test_reference_scene_buffers_match_numpy_restatement(mcpt_mod, oracle_mod, sid):
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import scene_restate as R
+    for li in (1.2, 0.443):
+        p, n, l, d, e = R.build(sid, li)
+        s = mcpt_mod.Scene.reference(sid, li)
+        sp, sn, sl = s.buffers()
+        assert (d, e) == (s.depth(), s.nb_emissives())
+        assert np.array_equal(bits(p), bits(sp)) and np.array_equal(bits(n), bits(sn)) and np.array_equal(l, sl)
+        op, on, ol, od, oe = oracle_mod.scene(sid, li)
+        assert (d, e) == (od, oe)
+        assert np.array_equal(bits(p), bits(op)) and np.array_equal(bits(n), bits(on)) and np.array_equal(l, ol)
+
+
+def test_camera_matches_numpy_restatement(mcpt_mod, oracle_mod):
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import scene_restate as R
+    for W, H in ((1920, 1080), (3840, 2160), (256, 256), (32, 24), (1000, 1280), (64, 40)):
+        a, b = R.camera(W, H)
+        pa, pb = mcpt_mod.camera_canonical(W, H)
+        oa, ob = oracle_mod.camera(W, H)
+        assert np.array_equal(bits(a), bits(pa)) and np.array_equal(bits(b), bits(pb)), (W, H)
+        assert np.array_equal(bits(a), bits(oa)) and np.array_equal(bits(b), bits(ob)), (W, H)
+
+
+def test_nth_element_restatement_matches_libstdcxx(oracle_mod):
+    """The restated std::nth_element (libstdc++ introselect, incl. the heap-select fallback)
+    against the C++ library's own on adversarial and random inputs, through the oracle's
+    mesh BVH builder (the same BVH_KDtree code path, with its nth_element calls)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import scene_restate as R
+    rng = np.random.default_rng(5)
+    for n in (2, 3, 4, 5, 7, 16, 33, 100, 257, 1000):
+        for kind in ("random", "sorted", "reversed", "equal", "organ"):
+            if kind == "random":
+                keys = rng.integers(0, 50, n).astype(np.float32)
+            elif kind == "sorted":
+                keys = np.arange(n, dtype=np.float32)
+            elif kind == "reversed":
+                keys = np.arange(n, dtype=np.float32)[::-1].copy()
+            elif kind == "equal":
+                keys = np.zeros(n, np.float32)
+            else:
+                keys = np.concatenate([np.arange(n // 2), np.arange(n - n // 2)[::-1]]).astype(np.float32)
+            for nth in sorted({0, n // 2, n - 1}):
+                v = list(range(n))
+                R.nth_element(v, 0, nth, n, lambda a, b: keys[a] < keys[b])
+                ref = sorted(keys)
+                assert keys[v[nth]] == ref[nth]
+                assert all(keys[v[i]] <= keys[v[nth]] for i in range(nth)) and \
+                    all(keys[v[i]] >= keys[v[nth]] for i in range(nth + 1, n))
+    # exact element placement against libstdc++: the oracle's mesh BVH (BVH_KDtree over the
+    # triangles' centres) and the restatement's kd_tree on the same centres and boxes
+    v = rng.uniform(-1, 1, (300, 3)).astype(np.float32)
+    t = rng.integers(0, 300, (701, 3)).astype(np.int32)
+    depth, nodes, leaves = oracle_mod.mesh_bvh(v, t)
+    cen, bbs = [], []
+    for tri in t:
+        p = v[tri]
+        lo, hi = p.min(0), p.max(0)
+        cen.append(np.array([np.float32(np.float32(lo[k] + hi[k]) / np.float32(2.0)) for k in range(3)], np.float32))
+        bbs.append(np.concatenate([lo, hi]))
+    d2, n2, l2 = R.kd_tree(cen, bbs)
+    assert d2 == depth and np.array_equal(l2, leaves)
