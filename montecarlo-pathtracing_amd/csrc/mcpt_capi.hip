@@ -729,7 +729,8 @@ constexpr int kStreamBatch = 8;   // iterations issued between two reads of the 
 constexpr double kStreamCompactBelow = 0.6;
 
 static bool stream_applies(const mcpt_ctx* c, int variant, int bounces, bool count) {
-  return !count && variant == 0 && bounces > 0 && c->n_meshes == 0;
+  (void)c;
+  return !count && variant == 0 && bounces > 0;
 }
 
 // path-slot pools of a launch: each runs its own iterations on its own stream, so one pool's
@@ -776,7 +777,7 @@ static int stream_run(mcpt_ctx* c, const mcpt::RenderParams& p) {
   // BVH nodes in the trace kernel's LDS where they fit (MCPT_STREAM_LDS_NODES=1): off by default,
   // no faster on scenes 3/7/8 (random lanes' node reads conflict in the LDS banks, 11 conflict
   // cycles per LDS instruction; gpurun_out r03e/r03f)
-  const bool lds_nodes = env_int("MCPT_STREAM_LDS_NODES", 0) != 0 && mcpt_stream_lds_nodes_fit(p.depth);
+  const bool lds_nodes = env_int("MCPT_STREAM_LDS_NODES", 0) != 0 && p.n_meshes == 0 && mcpt_stream_lds_nodes_fit(p.depth);
   mcpt::StreamParams q[kStreamPools];
   unsigned* unit_ctr = c->d_sctr + mcpt::SC_UNIT;   // pool 0's slot: shared
   {
@@ -897,13 +898,10 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   corner_rays(invPV, invV, p);
   p.W = c->W; p.H = c->H; p.rows = c->d_rows;
   p.n_local_rows = c->n_local_rows; p.depth = c->depth; p.n_prims = c->n_prims;
-#ifndef MCPT_LDS_SCENE
-#define MCPT_LDS_SCENE 1
-#endif
   {
     const long long lds = ((3LL * ((2LL << c->depth) - 1) + (long long)mcpt::kPrimF4 * c->n_prims) * 16) +
                           (((1LL << c->depth) + c->n_prims) * 4);
-    p.lds_scene_bytes = (MCPT_LDS_SCENE && lds <= mcpt::kLdsSceneBytes) ? (int)lds : 0;
+    p.lds_scene_bytes = lds <= mcpt::kLdsSceneBytes ? (int)lds : 0;
   }
   p.minfo = c->d_minfo; p.mpairs = c->d_mpairs; p.mleaftris = c->d_mleaftris; p.mtris = c->d_mtris;
   p.mverts = c->d_mverts; p.mnorms = c->d_mnorms; p.n_meshes = c->n_meshes; p.flat_face = c->flat_face;

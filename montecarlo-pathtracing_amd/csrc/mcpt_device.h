@@ -446,9 +446,11 @@ __device__ __forceinline__ void rcp6_rn(float4 wl, float4 wr, f3& il, f3& ir) {
 // round trip (all four rows issued together: a visit waits for one fetch), 1/w recomputed
 template <bool COUNT, class SR>
 __device__ __forceinline__ void mesh_pair_tests(const SR& s, size_t node, f3 O, f3 D, f3 invD, f3 Ol, float4 t0,
-                                                float4 t1, float4 t2, double cull2, bool& hl, bool& hr) {
+                                                float4 t1, float4 t2, double cull2, bool& hl, bool& hr,
+                                                const int* prefetch = nullptr, int* prefetched = nullptr) {
   const float4* q = s.mpairs + node * 4;
   const float4 a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
+  if (prefetch) *prefetched = *prefetch;   // issued after the rows: their wait does not include it
   MCPT_ROWS_IN("v"(a0.x), "v"(a0.y), "v"(a0.z), "v"(a0.w), "v"(a1.x), "v"(a1.y), "v"(a1.z));
   MCPT_ROWS_IN("v"(a2.x), "v"(a2.y), "v"(a2.z), "v"(a2.w), "v"(a3.x), "v"(a3.y), "v"(a3.z));
   MCPT_ROWS_IN("v"(t0.x), "v"(t0.y), "v"(t0.z), "v"(t0.w), "v"(t1.x), "v"(t1.y), "v"(t1.z), "v"(t1.w),
@@ -502,17 +504,12 @@ __device__ __forceinline__ void mesh_test(const SR& s, int mesh, int index, f3 O
   }
 }
 
-// 1: the L1/L2-read kernels (scene 8, C4 shape: +2.1 %; profiles/r04_ab_deep_walk.jsonl), 2: all,
-// 0: none (the LDS-scene C2 kernel: -0.6 % with it)
 // num / den from den's reciprocal y = rcp_core(den) by div_core (mcpt_math.h; exhaustively
 // checked), the IEEE division for the lanes whose operands leave div_core's exact range (ok false;
-// a wave-uniform branch, taken only when some lane is out of range).  Same bits as num / den.
-// MCPT_SHORT_DIV=0: the IEEE division everywhere.
-#ifndef MCPT_SHORT_DIV
-#define MCPT_SHORT_DIV 1
-#endif
+// a wave-uniform branch, taken only when some lane is out of range).  Same bits as num / den;
+// C2 +1.6 % over the IEEE division everywhere (profiles/r04_ab_short_div.jsonl).
 __device__ __forceinline__ float quot(float num, float den, float y, bool ok) {
-  if constexpr (!MCPT_SHORT_DIV || kDriverDiv) return fdiv(num, den);
+  if constexpr (kDriverDiv) return fdiv(num, den);
   float q = div_core(num, den, y);
   if (__builtin_expect(__ballot(!ok) != 0, 0)) {
     if (!ok) q = div_ieee(num, den);
@@ -520,9 +517,6 @@ __device__ __forceinline__ float quot(float num, float den, float y, bool ok) {
   return q;
 }
 
-#ifndef MCPT_ONE_ACCEPT
-#define MCPT_ONE_ACCEPT 1
-#endif
 // intersect_prim raytracer_func.frag:681-705 + Sphere/Cube/Cylinder/Cone/OrientedQuad :398-640
 // NOMESH: the caller handles CODE_MESH leaves itself (walk_run_mesh), so the nested mesh DFS is not
 // compiled in here
@@ -547,12 +541,14 @@ __device__ __forceinline__ void prim_test(const SR& s, int i, f3 Ow, f3 Dw, Hit&
   } else {
     r0 = ld4<U>(s.prims, b); r1 = ld4<U>(s.prims, b + 1); r2 = ld4<U>(s.prims, b + 2);
   }
-  // MCPT_ONE_ACCEPT: the type branches only record their candidate (the sphere's near and far
+  // kOne (the L1/L2-read kernels: scene 8, C4 shape +2.1 %, profiles/r04_ab_deep_walk.jsonl; the
+  // LDS-scene C2 kernel -0.6 % with it, so not there): the type branches only record their
+  // candidate (the sphere's near and far
   // roots: two) and one accept site after the switch tests it against the hit record, so a leaf
   // block whose lanes hold several primitive types runs the candidate code (transform rows,
   // world point, length, compare, record update) once instead of once per type.  Each lane's
   // candidates reach the hit record in the same order (same bits).
-  constexpr bool kOne = MCPT_ONE_ACCEPT == 2 || (MCPT_ONE_ACCEPT == 1 && !SR::kLds);
+  constexpr bool kOne = !SR::kLds;
   bool has1 = false, has2 = false;
   int shape1 = 0, dir1 = 0;
   f3 P1 = mk(0.0f, 0.0f, 0.0f), P2 = P1;
@@ -733,10 +729,10 @@ struct Walk {
   // mesh kernels (walk_run_mesh): the instance whose mesh BVH this lane is walking (-1: none),
   // its mesh id, the mesh walk's node / level / pending mask, and the ray in mesh space
   int mprim, mnode, mlevel;
+  int mpf;                 // mesh kernels: the last prefetch's dummy value (MCPT_MESH_PREFETCH)
   uint32_t mpending;
   f3 Om, Dm, invDm;
-  int4 mi;                 // the mesh's (first node, first leaf, depth, first triangle)
-  float4 t0, t1, t2;       // the instance's mesh transform rows
+  int4 mi;                 // the mesh's (first pair slot, first leaf, depth, first triangle)
 };
 
 template <bool COUNT, class SR>
@@ -887,8 +883,8 @@ __device__ __forceinline__ bool walk_run(const SR& s, f3 O, f3 D, Hit& h, Walk& 
 // mesh-space ray (intersect_prim :681-705) and continues in the mesh until its pending mask
 // is empty, then pops the scene stack.  Each lane's sequence of box / primitive / triangle
 // tests is the reference's, in the reference's order (same bits, same event counts).
-#ifndef MCPT_MESH_TRF_RELOAD
-#define MCPT_MESH_TRF_RELOAD 1
+#ifndef MCPT_MESH_PREFETCH
+#define MCPT_MESH_PREFETCH 1
 #endif
 template <bool COUNT, bool SUSPEND, class SR>
 __device__ __forceinline__ bool walk_run_mesh(const SR& s, f3 O, f3 D, Hit& h, Walk& w, Ev<COUNT>& ev, int exit) {
@@ -899,16 +895,11 @@ __device__ __forceinline__ bool walk_run_mesh(const SR& s, f3 O, f3 D, Hit& h, W
     if (w.mprim >= 0) {
       // one step of the instance's mesh walk (mesh_test's loop body)
       const int4 mi = w.mi;
-      float4 t0, t1, t2;
-      if constexpr (MCPT_MESH_TRF_RELOAD) {
-        // the instance's transform rows are read again at every mesh step (L1/L2 hits, issued
-        // with the step's record) rather than held: 12 VGPRs fewer across the shading rounds
-        // that suspended walks wait through
-        const float4* tp = s.prims + (size_t)w.mprim * 8 + 3;
-        t0 = tp[0]; t1 = tp[1]; t2 = tp[2];
-      } else {
-        t0 = w.t0; t1 = w.t1; t2 = w.t2;
-      }
+      // the instance's transform rows are read again at every mesh step (LDS for small scenes,
+      // else L1/L2 hits issued with the step's record) rather than held in the walk state: the
+      // mesh workload +6 % (profiles/r05_ab_mesh_trf_reload_waves.jsonl: main vs trf0)
+      const float4* tp = s.prims + (size_t)w.mprim * 8 + 3;
+      const float4 t0 = tp[0], t1 = tp[1], t2 = tp[2];
       const int mleaf0 = (1 << mi.z) - 1;
       bool mpop = true;
       if (w.mnode >= mleaf0) {
@@ -918,8 +909,21 @@ __device__ __forceinline__ bool walk_run_mesh(const SR& s, f3 O, f3 D, Hit& h, W
         ev.inc(EV_NODE);
         const size_t j = 2 * (size_t)w.mnode + 1;
         bool hl, hr;
-        mesh_pair_tests<COUNT>(s, (size_t)mi.x + mesh_pair_slot(w.mnode), w.Om, w.Dm, w.invDm, O,
-                               t0, t1, t2, h.cull2, hl, hr);
+        if constexpr (MCPT_MESH_PREFETCH) {
+          // the children's records (both in one 128-byte line: their pair records, or the leaf
+          // triangle records of the last level) are requested with this node's, so that the
+          // step that descends finds its record in L1/L2; the dummy value is consumed one step
+          // later, when the load has long returned
+          asm volatile("" ::"v"(w.mpf));
+          const size_t line = (w.mlevel + 1 < mi.z) ? ((size_t)mi.x + mesh_pair_slot((unsigned)j)) * 4
+                                                    : 0;
+          const float4* q = (w.mlevel + 1 < mi.z) ? s.mpairs + line : s.mleaftris + ((size_t)mi.y + (j - mleaf0)) * 4;
+          mesh_pair_tests<COUNT>(s, (size_t)mi.x + mesh_pair_slot(w.mnode), w.Om, w.Dm, w.invDm, O,
+                                 t0, t1, t2, h.cull2, hl, hr, (const int*)q, &w.mpf);
+        } else {
+          mesh_pair_tests<COUNT>(s, (size_t)mi.x + mesh_pair_slot(w.mnode), w.Om, w.Dm, w.invDm, O,
+                                 t0, t1, t2, h.cull2, hl, hr);
+        }
         mpop = !(hl || hr);
         if (hr) {
           if (hl) w.mpending |= 1u << (w.mlevel + 1);
@@ -955,9 +959,6 @@ __device__ __forceinline__ bool walk_run_mesh(const SR& s, f3 O, f3 D, Hit& h, W
           w.Dm = wnormalize3<SR::kFastNorm>(xdir(r0, r1, r2, D));
           w.invDm = mk(rcp_rn(w.Dm.x), rcp_rn(w.Dm.y), rcp_rn(w.Dm.z));
           w.mprim = p; w.mi = s.minfo[pt >> 4];
-          if constexpr (!MCPT_MESH_TRF_RELOAD) {
-            w.t0 = s.prims[b + 3]; w.t1 = s.prims[b + 4]; w.t2 = s.prims[b + 5];
-          }
           w.mnode = 0; w.mlevel = 0; w.mpending = 0;
           pop = false;
         } else {
@@ -1115,7 +1116,7 @@ __device__ __forceinline__ void geom_info(const SR& s, const Hit& h, f3& N, f3& 
 
 // sample_hemisphere + random_ray tp/montecarlo.frag:49-89
 //
-// MCPT_RR_SHORT drops range checks the sampler's operands never fail (same bits):
+// Range checks the sampler's operands never fail are dropped (same bits):
 //  * log(1 - u): 1 - u in [2^-23, 1] (mc_log_unit);
 //  * 1/sqrt(1 + tanTheta2): one range test for the pair (rsqrt_rn = RN(1/RN(sqrt)));
 //  * sqrt(max(0, 1 - c^2)): the operand is 0 or >= 2^-24 (1 - RN(c^2) with RN(c^2) <= 1 is
@@ -1123,30 +1124,22 @@ __device__ __forceinline__ void geom_info(const SR& s, const Hit& h, f3& N, f3& 
 //  * the local sample's normalize: |(cos b sin t, sin b sin t, cos t)|^2 is 1 within a few
 //    ulp for every finite angle pair (NaN stays NaN either way), where rcp_core(sqrt_core)
 //    is exact.
-// Bits 1 / 2 / 4 / 8 select the four in that order.  All four: scene 6 +1.4..+1.9 %, scene 3
-// +2.5 %, scenes 1 / 8 +0.4..+0.8 % (profiles/r02_ab19_rr_short.jsonl); the C2 kernel then keeps
-// 12 B of scratch, stored once in the prologue and reloaded only on the segment flush.
-#ifndef MCPT_RR_SHORT
-#define MCPT_RR_SHORT 15
-#endif
+// Scene 6 +1.4..+1.9 %, scene 3 +2.5 %, scenes 1 / 8 +0.4..+0.8 % over the checked sequences
+// (profiles/r02_ab19_rr_short.jsonl).
 __device__ __forceinline__ f3 random_ray(Rng& rng, f3 D, float roughness) {
   f3 W = normalize3(mk(D.x, D.y + 5.0f, D.z + 3.0f));
   f3 U = normalize3(cross3(D, W));
   f3 V = normalize3(cross3(D, U));
   float alpha = roughness * roughness;
   float beta = (2.0f * kPI) * rnd(rng);
-  float tanTheta2 = ((-alpha) * alpha) * ((MCPT_RR_SHORT & 1) ? mc_log_unit(1.0f - rnd(rng)) : mc_log(1.0f - rnd(rng)));
-  float cosTheta = (MCPT_RR_SHORT & 2) ? rsqrt_rn(1.0f + tanTheta2) : rcp_rn(sqrt_rn(1.0f + tanTheta2));
+  float tanTheta2 = ((-alpha) * alpha) * mc_log_unit(1.0f - rnd(rng));
+  float cosTheta = rsqrt_rn(1.0f + tanTheta2);
   const float s2 = gmax(0.0f, 1.0f - cosTheta * cosTheta);
-  float sinTheta = (MCPT_RR_SHORT & 4) ? sqrt_core(s2) : sqrt_rn(s2);
+  float sinTheta = sqrt_core(s2);
   float sb, cb;
   mc_sincos(beta, sb, cb);
-#if MCPT_RR_SHORT & 8
   const f3 sl = mk(cb * sinTheta, sb * sinTheta, cosTheta);
   f3 sm = muls(sl, rcp_core(sqrt_core(dot3(sl, sl))));
-#else
-  f3 sm = normalize3(mk(cb * sinTheta, sb * sinTheta, cosTheta));
-#endif
   f3 m = mk(__builtin_fmaf(D.x, sm.z, __builtin_fmaf(V.x, sm.y, U.x * sm.x)),
             __builtin_fmaf(D.y, sm.z, __builtin_fmaf(V.y, sm.y, U.y * sm.x)),
             __builtin_fmaf(D.z, sm.z, __builtin_fmaf(V.z, sm.y, U.z * sm.x)));

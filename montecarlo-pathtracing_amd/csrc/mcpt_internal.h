@@ -40,18 +40,10 @@ constexpr int kPassChunk = 32;
 constexpr int kLdsSceneBytes = 3584;
 constexpr int kPrimF4 = 8;
 // work-item tile (pixels): a work item is a kTileW x kTileH pixel tile for one pass chunk, one
-// lane per pixel, made of 8x8-pixel waves side by side (kTileW/8 x kTileH/8 of them).
-//   16x16 (MCPT_TILE_W=16 MCPT_TILE_H=16): four waves in a square;
-//   32x8 (default): four waves in one 8-row strip, so in a row-band shard (8-row bands,
-//   mcpt_set_target) all waves of a workgroup lie in one band of the image.
-//   8x8: one wave per workgroup.
-#ifndef MCPT_TILE_W
-#define MCPT_TILE_W 32
-#endif
-#ifndef MCPT_TILE_H
-#define MCPT_TILE_H 8
-#endif
-constexpr int kTileW = MCPT_TILE_W, kTileH = MCPT_TILE_H;
+// lane per pixel, made of 8x8-pixel waves side by side: 32x8 = four waves in one 8-row strip, so
+// in a row-band shard (8-row bands) all waves of a workgroup lie in one band of the image (16x16
+// tiles: the slowest 8-GPU shard 2.4-4.1 % slower, profiles/r01_ab33_tile_shape.jsonl)
+constexpr int kTileW = 32, kTileH = 8;
 constexpr int kTileThreads = kTileW * kTileH;
 static_assert(kTileW % 8 == 0 && kTileH % 8 == 0 && kTileThreads <= 1024, "tiles are made of 8x8 waves");
 
@@ -119,6 +111,7 @@ enum QueueField {
   QF_PASS, QF_UNIT,                           // current pass; unit = segment * n_local_px + px
   QF_SLOT,                                    // the slot running the unit (-1: a dead entry)
   QF_HX, QF_HY, QF_HZ, QF_HCODE,              // the traversal's hit record (pl, code)
+  QF_HTRI,                                    // ... and a mesh hit's triangle (mesh scenes)
   QF_COUNT
 };
 enum SlotField {
@@ -187,5 +180,6 @@ hipError_t mcpt_launch_combine(const mcpt::RenderParams& p, hipStream_t stream);
 // trace kernel over queue[parity] + the shade kernel appending to queue[parity ^ 1]
 hipError_t mcpt_launch_stream_init(const mcpt::StreamParams& q, hipStream_t stream);
 hipError_t mcpt_launch_stream_iter(const mcpt::StreamParams& q, int n_cu, bool lds_nodes, hipStream_t stream);
+// (q.r.n_meshes > 0: the mesh instantiations, walk_run_mesh in the trace kernel)
 // the trace kernel can hold a BVH of this depth in LDS (nodes + leaf ids)
 bool mcpt_stream_lds_nodes_fit(int depth);

@@ -31,19 +31,9 @@
 #include <stdint.h>
 #include "mcpt_device.h"
 
-// minimum waves per SIMD the register allocator must allow (occupancy vs spills)
-#ifndef MCPT_MIN_WAVES
-#define MCPT_MIN_WAVES 7
-#endif
-// sky fold (render_kernel): a bounce ray that misses the scene starts the lane's next pass in
-// the same round
-#ifndef MCPT_FOLD_SKY
-#define MCPT_FOLD_SKY 1
-#endif
-// end fold: emissive hits and hits at bounce B-1 (black) end the pass before the shading block
-#ifndef MCPT_FOLD_END
-#define MCPT_FOLD_END 1
-#endif
+// minimum waves per SIMD the register allocator must allow (occupancy vs spills):
+// the LDS-scene and wave-coherent kernels (72 VGPRs, no spills: 7 waves)
+constexpr int kMinWaves = 7;
 
 
 namespace mcpt {
@@ -62,24 +52,20 @@ namespace mcpt {
 // node loads are LDS reads instead of L1/L2 gathers.
 // SUSPEND: the deep-BVH walk (suspendable walks, batched leaf visits: RenderParams::walk_exit,
 // leaf_batch; walk_run)
-template <bool COUNT, bool WAVE, bool MESH, bool LDSS, bool SUSPEND>
 // per-lane walks of mesh scenes (walk_run_mesh keeps the mesh walk state and the ray in mesh
 // space in registers; the instance transform is re-read per step): 5 waves/SIMD, 96 VGPRs and
 // 48 B of scratch, against 113 VGPRs without spills at 4 waves: the mesh workload +5..8 %
-// (round 5, profiles/r05_ab_mesh_*.jsonl; 7 waves with that state spill and run at a third of
-// the speed, round 1)
-#ifndef MCPT_MIN_WAVES_MESH
-#define MCPT_MIN_WAVES_MESH 5
-#endif
+// (round 5, profiles/r05_ab_mesh_layouts.jsonl, r05_ab_mesh_trf_reload_waves.jsonl; 7 waves
+// with that state spill and run at a third of the speed, round 1)
+constexpr int kMinWavesMesh = 5;
 // per-lane walks over scenes read through L1/L2 (not LDS-staged: scenes 3, 5, 7, 8): 6 waves/SIMD
 // while their state spilled at 7 (profiles/r01_ab35_occupancy_v12.jsonl); with the packed hit
 // record they fit 72 VGPRs and 7 waves hide more of the dependent node loads (scene 8 +4 %,
-// scene 3 +5 %: profiles/r02_ab4_spill_free.jsonl)
-#ifndef MCPT_MIN_WAVES_L2
-#define MCPT_MIN_WAVES_L2 7
-#endif
-__global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
-                                           : (!WAVE && !LDSS ? MCPT_MIN_WAVES_L2 : MCPT_MIN_WAVES)) void render_kernel(
+// scene 3 +5 %: profiles/r02_ab4_spill_free.jsonl; 6 / 8 waves re-measured in round 4: -1.9 / -6.1 %)
+constexpr int kMinWavesL2 = 7;
+template <bool COUNT, bool WAVE, bool MESH, bool LDSS, bool SUSPEND>
+__global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? kMinWavesMesh
+                                           : (!WAVE && !LDSS ? kMinWavesL2 : kMinWaves)) void render_kernel(
     RenderParams p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -221,7 +207,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
     }
   };
   Walk walk;
-  walk.invD = mk(0.0f, 0.0f, 0.0f); walk.node = 0; walk.level = 0; walk.pending = 0;
+  walk.invD = mk(0.0f, 0.0f, 0.0f); walk.node = 0; walk.level = 0; walk.pending = 0; walk.mpf = 0;
   bool walking = false;   // a suspended per-lane walk is waiting to be continued
 #ifdef MCPT_LANESTATS
   ls_add(LS_WAVES, 1u);
@@ -261,7 +247,6 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
     st_t += st_b - st_a;
     st_s -= st_b;
 #endif
-#if MCPT_FOLD_SKY
     // Sky fold: a bounce ray that left the scene ends its pass here, before the shading
     // block, and the lane starts its next pass at once with the cached primary hit, so
     // that one shading block serves both (the pass's camera-ray round, in which this
@@ -269,7 +254,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
     // per-lane sequence of values: the sky term, the segment sum in pass order, then the
     // next pass from its seed.
     //
-    // End fold (MCPT_FOLD_END): the other two path ends known before shading fold the same
+    // End fold: the other two path ends known before shading fold the same
     // way.  An emissive hit (material .z > 0.5) ends the pass with total + its emission
     // term (montecarlo.frag's `else` branch: no RNG draw, no new ray), and a non-emissive
     // hit at bounce B-1 ends it black whatever the branch (reflect / diffuse reach bounce
@@ -282,7 +267,6 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
         const float a = gmax(0.0f, D.z);
         fres = add(total, mulv(att, gmix3(mk(0.5f, 0.5f, 0.9f), mk(1.0f, 1.0f, 0.8f), a)));
       } else {
-#if MCPT_FOLD_END
         const float4 m4 = s.prims[(size_t)h.index() * 8 + 7];
         if (!(m4.z <= 0.5f)) {   // the shading block's emissive `else`, NaN included
           const float4 c4 = s.prims[(size_t)h.index() * 8 + 6];
@@ -290,9 +274,6 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
         } else if (bounce < B - 1) {
           fold_end = false;
         }
-#else
-        fold_end = false;
-#endif
       }
     }
     if (fold_end) {
@@ -313,7 +294,6 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? MCPT_MIN_WAVES_MESH
         ready = false;   // unit finished: the lane claims another at the end of the round
       }
     }
-#endif
     if (ready && run) {
       if (p.variant != 0) {
         // tp/montecarlo_mat.frag:5-20 / montecarlo_mat_tr.frag:5-20

@@ -27,22 +27,15 @@ namespace mcpt {
 // ------------------------------------------------------------------------------------
 constexpr uint32_t kPhaseInner = 1, kPhasePrimary = 2;
 constexpr int kStreamBlock = 256, kStreamWaves = kStreamBlock / 64;   // stream kernels' workgroups
-#ifndef MCPT_MIN_WAVES_STREAM
-#define MCPT_MIN_WAVES_STREAM 8
-#endif
+constexpr int kMinWavesStream = 8;
+// the mesh trace kernel (walk_run_mesh: the mesh walk state and mesh-space ray): as the mesh
+// megakernel, 5 waves/SIMD
+constexpr int kMinWavesStreamMesh = 5;
 // the shade kernel streams payloads from HBM: occupancy over registers
-#ifndef MCPT_MIN_WAVES_SHADE
-#define MCPT_MIN_WAVES_SHADE 5
-#endif
+constexpr int kMinWavesShade = 5;
 // queue entries a trace wave claims (one atomic) and stages in LDS at once
-#ifndef MCPT_STREAM_CHUNK
-#define MCPT_STREAM_CHUNK 128
-#endif
-constexpr int kStreamChunk = MCPT_STREAM_CHUNK;
-// trace waves stage each claimed chunk in order of the rays' direction octants
-#ifndef MCPT_STREAM_SORT
-#define MCPT_STREAM_SORT 1
-#endif
+constexpr int kStreamChunk = 128;
+// trace waves stage each claimed chunk in order of the rays' direction octants (+2-4 %)
 static_assert(kStreamChunk % 64 == 0, "chunks are staged 64 entries per step");
 
 // Field columns through a buffer resource: the column offset f * n * 4 is a wave-uniform
@@ -51,12 +44,9 @@ static_assert(kStreamChunk % 64 == 0, "chunks are staged 64 entries per step");
 // strength-reduced ~40 columns into live 64-bit addresses and spilled them).  Buffers stay
 // below 2 GiB (host check).  0x00020000: the gfx9 raw-buffer descriptor word 3.
 // Queue payloads are streamed once per iteration: their loads and stores carry the
-// non-temporal hint (MCPT_STREAM_NT, aux bit 1: nt on gfx950) so that they do not evict the
+// non-temporal hint (aux bit 1: nt on gfx950) so that they do not evict the
 // BVH records the walks read through L2.
-#ifndef MCPT_STREAM_NT
-#define MCPT_STREAM_NT 1
-#endif
-constexpr int kQueueAux = MCPT_STREAM_NT ? 2 : 0;
+constexpr int kQueueAux = 2;
 template <int AUX>
 struct ColsT {
   __amdgpu_buffer_rsrc_t rs;
@@ -154,7 +144,7 @@ __global__ __launch_bounds__(256) void stream_init_kernel(StreamParams q) {
 // workgroup; one 1024-thread workgroup per CU, 4 waves/SIMD), so the walk's dependent node
 // loads are LDS reads; primitive records stay in global memory.
 template <bool LDSN> struct TraceCfg {
-  static constexpr int kBlock = 256, kWaves = 4, kChunk = kStreamChunk, kMinWaves = MCPT_MIN_WAVES_STREAM;
+  static constexpr int kBlock = 256, kWaves = 4, kChunk = kStreamChunk, kMinWaves = kMinWavesStream;
 };
 template <> struct TraceCfg<true> {
   static constexpr int kBlock = 1024, kWaves = 16, kChunk = 64, kMinWaves = 4;
@@ -162,13 +152,16 @@ template <> struct TraceCfg<true> {
 // LDS of the LDSN trace kernel besides its scene copy: the waves' staged rays
 constexpr int kTraceLdsStaging = TraceCfg<true>::kWaves * TraceCfg<true>::kChunk * 32;
 
-template <bool LDSN>
-__global__ __launch_bounds__(TraceCfg<LDSN>::kBlock, TraceCfg<LDSN>::kMinWaves) void stream_trace_kernel(StreamParams q) {
+// MESH: scenes with triangle-mesh instances, the walk of walk_run_mesh (suspended at <= refill
+// walking lanes like walk_run), the hit's triangle kept in the entry
+template <bool LDSN, bool MESH>
+__global__ __launch_bounds__(TraceCfg<LDSN>::kBlock, MESH ? kMinWavesStreamMesh : TraceCfg<LDSN>::kMinWaves)
+void stream_trace_kernel(StreamParams q) {
   typedef TraceCfg<LDSN> C;
   constexpr int kChunkT = C::kChunk;
   const RenderParams& p = q.r;
-  SceneT<false, false> s{p.nodes, p.leaves, p.ptype, p.prims, p.depth, p.minfo, p.mpairs, p.mleaftris,
-                         p.mtris, p.mverts, p.mnorms, p.flat_face};
+  SceneT<MESH, false> s{p.nodes, p.leaves, p.ptype, p.prims, p.depth, p.minfo, p.mpairs, p.mleaftris,
+                        p.mtris, p.mverts, p.mnorms, p.flat_face};
   if constexpr (LDSN) {
     extern __shared__ float4 s_bvh[];
     const int n_nodes = (2 << p.depth) - 1, n_leaves = 1 << p.depth;
@@ -211,7 +204,7 @@ __global__ __launch_bounds__(TraceCfg<LDSN>::kBlock, TraceCfg<LDSN>::kMinWaves) 
         live = 0;
         cc = 0;
         // the chunk's live entries (neighbouring pixels' rays), staged in order of the
-        // direction octant (MCPT_STREAM_SORT): lanes that take consecutive staged rays then
+        // direction octant: lanes that take consecutive staged rays then
         // walk rays of one octant from nearby origins, which visit the same nodes and take the
         // same branches
         constexpr int G = kChunkT / 64;
@@ -227,11 +220,11 @@ __global__ __launch_bounds__(TraceCfg<LDSN>::kBlock, TraceCfg<LDSN>::kMinWaves) 
           if (slot >= 0) {
             eo[g].x = Q.ld(QF_OX, idx); eo[g].y = Q.ld(QF_OY, idx); eo[g].z = Q.ld(QF_OZ, idx);
             ed[g].x = Q.ld(QF_DX, idx); ed[g].y = Q.ld(QF_DY, idx); ed[g].z = Q.ld(QF_DZ, idx);
-            key[g] = MCPT_STREAM_SORT ? ((ed[g].x < 0.0f) | ((ed[g].y < 0.0f) << 1) | ((ed[g].z < 0.0f) << 2)) : 0;
+            key[g] = (ed[g].x < 0.0f) | ((ed[g].y < 0.0f) << 1) | ((ed[g].z < 0.0f) << 2);
           }
         }
 #pragma unroll
-        for (int o = 0; o < (MCPT_STREAM_SORT ? 8 : 1); ++o) {
+        for (int o = 0; o < 8; ++o) {
 #pragma unroll
           for (int g = 0; g < G; ++g) {
             const bool mine = key[g] == o;
@@ -262,18 +255,22 @@ __global__ __launch_bounds__(TraceCfg<LDSN>::kBlock, TraceCfg<LDSN>::kMinWaves) 
   auto put_hit = [&](int r, const Hit& h) {
     Q.set3(QF_HX, (uint32_t)r, h.pl);
     Q.setu(QF_HCODE, (uint32_t)r, (uint32_t)h.code);
+    if constexpr (MESH) Q.setu(QF_HTRI, (uint32_t)r, (uint32_t)h.tri);
   };
   int r = -1;                // queue index of this lane's ray
   f3 O = mk(0.0f, 0.0f, 0.0f), D = O;
   Hit h;
   h.pl = O; h.dist = kFLTMAX; h.clear(); h.tri = 0; h.cull2 = 0.0;
   Walk w;
-  w.invD = O; w.node = 0; w.level = 0; w.pending = 0;
+  w.invD = O; w.node = 0; w.level = 0; w.pending = 0; w.mpf = 0;
   for (;;) {
     take(r, O, D, h, w);
     if (__ballot(r >= 0) == 0) break;   // nothing staged and nothing left to claim
     if (r >= 0) {
-      if (walk_run<false, true>(s, O, D, h, w, ev, q.refill, p.leaf_batch)) {
+      bool ended;
+      if constexpr (MESH) ended = walk_run_mesh<false, true>(s, O, D, h, w, ev, q.refill);
+      else ended = walk_run<false, true>(s, O, D, h, w, ev, q.refill, p.leaf_batch);
+      if (ended) {
         put_hit(r, h);
         r = -1;
       }
@@ -302,11 +299,12 @@ __global__ __launch_bounds__(TraceCfg<LDSN>::kBlock, TraceCfg<LDSN>::kMinWaves) 
 // ray is the cached primary hit (shaded at once, no traversal); a unit that ends writes its
 // sum and the slot takes the next unit.  Returns true with the next payload in `out` when the
 // slot's next ray must be traversed, false when the slot has no unit left.
+template <bool MESH>
 __device__ __forceinline__ bool stream_shade(const StreamParams& q, const Cols& Qi, uint32_t i, const SlotCols& Sl,
                                              int slot, Payload& out) {
   const RenderParams& p = q.r;
-  const SceneT<false, false> s{p.nodes, p.leaves, p.ptype, p.prims, p.depth, p.minfo, p.mpairs, p.mleaftris,
-                               p.mtris, p.mverts, p.mnorms, p.flat_face};
+  const SceneT<MESH, false> s{p.nodes, p.leaves, p.ptype, p.prims, p.depth, p.minfo, p.mpairs, p.mleaftris,
+                              p.mtris, p.mverts, p.mnorms, p.flat_face};
   Ev<false> ev;
   ev.init();
   const uint32_t sidx = (uint32_t)slot;
@@ -319,7 +317,8 @@ __device__ __forceinline__ bool stream_shade(const StreamParams& q, const Cols& 
   const int B = p.bounces;
   const f3 Ocam = mk(p.ox, p.oy, p.oz);
   Hit h;
-  h.pl = Qi.ld3(QF_HX, i); h.code = (int)Qi.ldu(QF_HCODE, i); h.dist = 0.0f; h.tri = 0; h.cull2 = 0.0;
+  h.pl = Qi.ld3(QF_HX, i); h.code = (int)Qi.ldu(QF_HCODE, i); h.dist = 0.0f; h.cull2 = 0.0;
+  h.tri = MESH ? (int)Qi.ldu(QF_HTRI, i) : 0;
   f3 O = Qi.ld3(QF_OX, i), D = Qi.ld3(QF_DX, i), att, total, N = mk(0.0f, 0.0f, 0.0f), P = N;
   Rng rng;
   bool first = false;
@@ -460,7 +459,8 @@ __device__ __forceinline__ bool stream_shade(const StreamParams& q, const Cols& 
   }
 }
 
-__global__ __launch_bounds__(kStreamBlock, MCPT_MIN_WAVES_SHADE) void stream_shade_kernel(StreamParams q) {
+template <bool MESH>
+__global__ __launch_bounds__(kStreamBlock, kMinWavesShade) void stream_shade_kernel(StreamParams q) {
   const int par = q.parity;
   const unsigned n = q.ctr[SC_CNT + par];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -475,7 +475,7 @@ __global__ __launch_bounds__(kStreamBlock, MCPT_MIN_WAVES_SHADE) void stream_sha
     const unsigned i = base + threadIdx.x;
     const int slot = i < n ? (int)Qi.ldu(QF_SLOT, i) : -1;
     Payload pl;
-    const bool cont = slot >= 0 && stream_shade(q, Qi, i, Sl, slot, pl);
+    const bool cont = slot >= 0 && stream_shade<MESH>(q, Qi, i, Sl, slot, pl);
     if (!q.compact) {   // in place: entry i of the next queue (dead entries marked)
       if (cont) put_payload(Qo, i, pl, slot);
       else if (i < n) Qo.setu(QF_SLOT, i, 0xFFFFFFFFu);
@@ -513,21 +513,26 @@ bool mcpt_stream_lds_nodes_fit(int depth) {
 
 hipError_t mcpt_launch_stream_iter(const mcpt::StreamParams& q, int n_cu, bool lds_nodes, hipStream_t stream) {
   hipError_t e;
-  if (lds_nodes) {
+  const bool mesh = q.r.n_meshes > 0;
+  if (mesh) {
+    hipLaunchKernelGGL((mcpt::stream_trace_kernel<false, true>), dim3((unsigned)n_cu * 8), dim3(mcpt::kStreamBlock), 0,
+                       stream, q);
+  } else if (lds_nodes) {
     const size_t shm = (size_t)mcpt_stream_lds_nodes_bytes(q.r.depth);
     // above the default 64 KiB of dynamic LDS (set on the calling thread's current device)
-    e = hipFuncSetAttribute((const void*)mcpt::stream_trace_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024 - mcpt::kTraceLdsStaging);
+    e = hipFuncSetAttribute((const void*)mcpt::stream_trace_kernel<true, false>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - mcpt::kTraceLdsStaging);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(mcpt::stream_trace_kernel<true>, dim3((unsigned)n_cu), dim3(mcpt::TraceCfg<true>::kBlock), shm,
-                       stream, q);
+    hipLaunchKernelGGL((mcpt::stream_trace_kernel<true, false>), dim3((unsigned)n_cu),
+                       dim3(mcpt::TraceCfg<true>::kBlock), shm, stream, q);
   } else {
-    hipLaunchKernelGGL(mcpt::stream_trace_kernel<false>, dim3((unsigned)n_cu * 8), dim3(mcpt::kStreamBlock), 0, stream,
-                       q);
+    hipLaunchKernelGGL((mcpt::stream_trace_kernel<false, false>), dim3((unsigned)n_cu * 8), dim3(mcpt::kStreamBlock), 0,
+                       stream, q);
   }
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   const unsigned persistent_blocks = (unsigned)n_cu * 8;
-  hipLaunchKernelGGL(mcpt::stream_shade_kernel, dim3(persistent_blocks), dim3(mcpt::kStreamBlock), 0, stream, q);
+  if (mesh) hipLaunchKernelGGL(mcpt::stream_shade_kernel<true>, dim3(persistent_blocks), dim3(mcpt::kStreamBlock), 0, stream, q);
+  else hipLaunchKernelGGL(mcpt::stream_shade_kernel<false>, dim3(persistent_blocks), dim3(mcpt::kStreamBlock), 0, stream, q);
   return hipGetLastError();
 }

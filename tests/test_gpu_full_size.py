@@ -113,7 +113,7 @@ def big_mesh(mcpt_mod):
     return meshes.big_mesh_scene(1_000_000)[0]
 
 
-@pytest.mark.parametrize("traversal", [0, 1])
+@pytest.mark.parametrize("traversal", [0, 1, 3])
 def test_mesh_1m_rows(mcpt_mod, oracle_mod, renderer, big_mesh, traversal):
     """The HBM-sized mesh workload (bench.py --config mesh: two instances of a 1 M-triangle UV
     sphere, mesh BVH depth 20), 1080p, B 8, against the oracle's own mesh DFS on a row subset."""

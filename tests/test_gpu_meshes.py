@@ -20,7 +20,7 @@ def renderer(mcpt_mod):
 
 
 @pytest.mark.parametrize("flat,walk_exit", [(False, -1), (True, -1), (False, 12), (False, 0), (False, 63)])
-@pytest.mark.parametrize("traversal", [1, 2])
+@pytest.mark.parametrize("traversal", [1, 2, 3])
 def test_mesh_scene_render(mcpt_mod, oracle_mod, renderer, traversal, flat, walk_exit):
     sc = mesh_scene(mcpt_mod)
     prims, nodes, leaves = sc.buffers()

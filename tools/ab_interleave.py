@@ -83,6 +83,7 @@ def main():
     ap.add_argument("--reps", type=int, default=6)
     ap.add_argument("--traversal", type=int, default=1)
     ap.add_argument("--walk-exit", type=int, nargs="+", default=[-1])
+    ap.add_argument("--leaf-batch", type=int, nargs="+", default=[-1])
     ap.add_argument("--mesh-tris", type=int, default=1_000_000)
     a = ap.parse_args()
     W, H, S, B = a.width, a.height, a.spp, BOUNCES[a.scene]
@@ -101,9 +102,10 @@ def main():
     ctxs = [Ctx(lib_path(n), bufs, mb, W, H) for n in a.libs]
     for c in ctxs:
         c._ok(c.L.mcpt_set_traversal(c.h, a.traversal))
-    for wx in a.walk_exit:
+    for wx, lb in [(x, b) for x in a.walk_exit for b in a.leaf_batch]:
         for c in ctxs:
             c._ok(c.L.mcpt_set_walk_exit(c.h, wx))
+            c._ok(c.L.mcpt_set_leaf_batch(c.h, lb))
             c.render(ipv, iv, 1, S, B)   # warm-up
             c.kernel_ms()
         ms = [[] for _ in ctxs]
@@ -114,7 +116,7 @@ def main():
                 ms[k].append(ctxs[k].kernel_ms())
         for n, m in zip(a.libs, ms):
             m = np.array(m)
-            print(json.dumps({"lib": n, "scene": a.scene, "walk_exit": wx, "spp": S, "reps": a.reps,
+            print(json.dumps({"lib": n, "scene": a.scene, "walk_exit": wx, "leaf_batch": lb, "spp": S, "reps": a.reps,
                               "kernel_ms_median": round(float(np.median(m)), 3), "kernel_ms_mean": round(float(m.mean()), 3),
                               "kernel_ms_min": round(float(m.min()), 3),
                               "msamples_s_median": round(W * H * S / float(np.median(m)) / 1e3, 1)}), flush=True)

@@ -20,7 +20,8 @@ import mcpt  # noqa: E402
 NAMES = ["node_it", "node_ln", "ne_wv", "ne_ln", "out_wv", "out_ln", "val_wv", "val_ln",
          "leaf_it", "leaf_ln", "prim_ln", "sph_wv", "sph_ln", "cube_wv", "cube_ln", "cyl_wv",
          "cyl_ln", "quad_wv", "quad_ln", "walk_it", "walk_ln", "walk_calls", "rounds", "round_ln",
-         "shade_wv", "shade_ln", "rr2_wv", "rr2_ln", "waves", "fit_it", "two_it"]
+         "shade_wv", "shade_ln", "rr2_wv", "rr2_ln", "waves", "fit_it", "two_it",
+         "snode_it", "snode_ln", "sleaf_it", "sleaf_ln", "exit_ln"]
 
 
 def util(ln, wv):
@@ -32,7 +33,11 @@ def run(sid, B, spp, seg, leaf_batch, walk_exit, W=1920, H=1080):
     os.environ["MCPT_LEAF_BATCH"] = str(leaf_batch)   # read when a context is created
     r = mcpt.Renderer(0)
     r.set_traversal(1)
-    r.upload_scene(mcpt.Scene.reference(sid))
+    if sid == 0:   # the mesh workload (walk_run_mesh: node / leaf = mesh-node / mesh-leaf steps)
+        from mcpt import meshes
+        r.upload_scene(meshes.big_mesh_scene(1_000_000)[0])
+    else:
+        r.upload_scene(mcpt.Scene.reference(sid))
     r.set_target(W, H)
     if walk_exit is not None:
         r.set_walk_exit(walk_exit)
@@ -51,7 +56,10 @@ def run(sid, B, spp, seg, leaf_batch, walk_exit, W=1920, H=1080):
                     "cull_stage": util(d["val_ln"], d["val_wv"]), "leaf_block": util(d["leaf_ln"], d["leaf_it"]),
                     "sphere": util(d["sph_ln"], d["sph_wv"]), "cube": util(d["cube_ln"], d["cube_wv"]),
                     "cylinder": util(d["cyl_ln"], d["cyl_wv"]), "quad": util(d["quad_ln"], d["quad_wv"]),
-                    "shade": util(d["shade_ln"], d["shade_wv"]), "reflect_rr": util(d["rr2_ln"], d["rr2_wv"])},
+                    "shade": util(d["shade_ln"], d["shade_wv"]), "reflect_rr": util(d["rr2_ln"], d["rr2_wv"]),
+                    "scene_node": util(d["snode_ln"], d["snode_it"]), "scene_leaf": util(d["sleaf_ln"], d["sleaf_it"])},
+           "walk_lanes_at_exit": round(d["exit_ln"] / max(d["walk_calls"], 1), 2),
+           "walk_it_share": {k: round(d[k] / max(d["walk_it"], 1), 3) for k in ("node_it", "leaf_it", "snode_it", "sleaf_it")},
            "node_it_share": {"face_jobs_fit_one_round": round(d["fit_it"] / max(d["node_it"], 1), 3),
                              "some_lane_two_face_jobs": round(d["two_it"] / max(d["node_it"], 1), 3),
                              "face_jobs_per_walking_lane": round(d["out_ln"] / max(d["walk_ln"] * d["node_it"] / max(d["walk_it"], 1), 1), 3)},
@@ -64,6 +72,10 @@ def run(sid, B, spp, seg, leaf_batch, walk_exit, W=1920, H=1080):
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "mesh":   # the mesh workload (walk_run_mesh), walk exits
+        for wx in (24, 40):
+            run(0, 8, 64, 1, -1, wx)
+        sys.exit(0)
     run(8, 12, 256, 8, 16, 40)      # C4 shape: deep knobs, eight segments per item
     run(8, 12, 256, 1, 16, 40)
     run(8, 12, 256, 8, 8, 16)       # the depth >= 8 defaults
