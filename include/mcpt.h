@@ -111,7 +111,8 @@ int mcpt_set_flat_face(mcpt_ctx* ctx, int flat_face);
  * Row-band sharding for multi-GPU: this context renders global rows y whose band
  * (y / band_rows) satisfies band % world == rank; its accumulator holds only those
  * "local" rows, in increasing y.  Single GPU: band_rows = any > 0, world = 1, rank = 0.
- * Allocates and zeroes the accumulator; pass count reset to 0. */
+ * Allocates and zeroes the accumulator; pass count reset to 0.  MCPT_ERR_INVALID_ARG when this
+ * context's local rows × W reach 2^31 pixels (the kernels index a shard with 32-bit ints). */
 int mcpt_set_target(mcpt_ctx* ctx, int W, int H, int band_rows, int world, int rank);
 int mcpt_local_rows(mcpt_ctx* ctx, int* n_local_rows);
 /* Explicit shard: this context renders the n_rows global rows rows[0..n_rows) (distinct, in

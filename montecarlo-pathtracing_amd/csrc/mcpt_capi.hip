@@ -602,6 +602,9 @@ int mcpt_set_flat_face(mcpt_ctx* c, int flat_face) {
 // local-row order.  mcpt_set_target (interleaved bands) and mcpt_balanced_rows are row lists.
 static int set_target_rows(mcpt_ctx* c, int W, int H, const int* rows, int n_rows, int band_rows, int world,
                            int rank) {
+  // the kernels index a shard's pixels with 32-bit ints (render_kernel's local pixel index)
+  if ((long long)n_rows * W >= (1LL << 31))
+    return set_err(MCPT_ERR_INVALID_ARG, "mcpt_set_target: a shard of 2^31 pixels or more");
   HIP_OR_RETURN(hipSetDevice(c->device));
   HIP_OR_RETURN(hipStreamSynchronize(c->stream));
   size_t bytes = (size_t)n_rows * W * 3 * sizeof(float);
@@ -941,6 +944,9 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   {
     float r0 = (refract_ind - 1.0f) / (refract_ind + 1.0f);   // schlick tp/montecarlo.frag:93-94
     p.schlick_r0 = r0 * r0;
+    p.schlick_1mr0 = 1.0f - p.schlick_r0;
+    p.ior_sq = refract_ind * refract_ind;
+    p.inv_ior_sq = p.inv_ior * p.inv_ior;
     const float fmax = mcpt::kFLTMAX, nx = std::nextafter(fmax, INFINITY);   // cull_bound_sq(FLT_MAX)
     const double m = ((double)fmax + (double)nx) * 0.5;
     p.cull2_max = m * m;

@@ -729,7 +729,7 @@ struct Walk {
   // mesh kernels (walk_run_mesh): the instance whose mesh BVH this lane is walking (-1: none),
   // its mesh id, the mesh walk's node / level / pending mask, and the ray in mesh space
   int mprim, mnode, mlevel;
-  int mpf;                 // mesh kernels: the last prefetch's dummy value (MCPT_MESH_PREFETCH)
+  int mpf;                 // mesh kernels: the last prefetch's dummy value (walk_run_mesh)
   uint32_t mpending;
   f3 Om, Dm, invDm;
   int4 mi;                 // the mesh's (first pair slot, first leaf, depth, first triangle)
@@ -883,9 +883,6 @@ __device__ __forceinline__ bool walk_run(const SR& s, f3 O, f3 D, Hit& h, Walk& 
 // mesh-space ray (intersect_prim :681-705) and continues in the mesh until its pending mask
 // is empty, then pops the scene stack.  Each lane's sequence of box / primitive / triangle
 // tests is the reference's, in the reference's order (same bits, same event counts).
-#ifndef MCPT_MESH_PREFETCH
-#define MCPT_MESH_PREFETCH 1
-#endif
 template <bool COUNT, bool SUSPEND, class SR>
 __device__ __forceinline__ bool walk_run_mesh(const SR& s, f3 O, f3 D, Hit& h, Walk& w, Ev<COUNT>& ev, int exit) {
   const int leaf0 = (1 << s.depth) - 1;
@@ -909,20 +906,18 @@ __device__ __forceinline__ bool walk_run_mesh(const SR& s, f3 O, f3 D, Hit& h, W
         ev.inc(EV_NODE);
         const size_t j = 2 * (size_t)w.mnode + 1;
         bool hl, hr;
-        if constexpr (MCPT_MESH_PREFETCH) {
+        {
           // the children's records (both in one 128-byte line: their pair records, or the leaf
           // triangle records of the last level) are requested with this node's, so that the
           // step that descends finds its record in L1/L2; the dummy value is consumed one step
-          // later, when the load has long returned
+          // later, when the load has long returned.  +0.9..1.4 % on the mesh workload; the
+          // grandchildren's two lines as well: -5..8 % (profiles/r05_ab_mesh_prefetch.jsonl)
           asm volatile("" ::"v"(w.mpf));
           const size_t line = (w.mlevel + 1 < mi.z) ? ((size_t)mi.x + mesh_pair_slot((unsigned)j)) * 4
                                                     : 0;
           const float4* q = (w.mlevel + 1 < mi.z) ? s.mpairs + line : s.mleaftris + ((size_t)mi.y + (j - mleaf0)) * 4;
           mesh_pair_tests<COUNT>(s, (size_t)mi.x + mesh_pair_slot(w.mnode), w.Om, w.Dm, w.invDm, O,
                                  t0, t1, t2, h.cull2, hl, hr, (const int*)q, &w.mpf);
-        } else {
-          mesh_pair_tests<COUNT>(s, (size_t)mi.x + mesh_pair_slot(w.mnode), w.Om, w.Dm, w.invDm, O,
-                                 t0, t1, t2, h.cull2, hl, hr);
         }
         mpop = !(hl || hr);
         if (hr) {
@@ -1147,10 +1142,12 @@ __device__ __forceinline__ f3 random_ray(Rng& rng, f3 D, float roughness) {
 }
 
 // r0 = ((ior-1)/(ior+1))^2 (:93-94), computed once on the host (RenderParams::schlick_r0)
-__device__ __forceinline__ float schlick(float r0, f3 I, f3 N) {   // :91-98
+// one_m_r0 = 1 - r0 (binary32; RenderParams::schlick_1mr0)
+__device__ __forceinline__ float schlick(float r0, float one_m_r0, f3 I, f3 N) {   // :91-98
   float x = 1.0f - dot3(N, I);
-  return gclamp(r0 + ((((1.0f - r0) * x) * x * x) * x) * x, 0.0f, 1.0f);
+  return gclamp(r0 + ((((one_m_r0) * x) * x * x) * x) * x, 0.0f, 1.0f);
 }
+__device__ __forceinline__ float schlick(float r0, f3 I, f3 N) { return schlick(r0, 1.0f - r0, I, N); }
 
 __device__ __forceinline__ int floordiv(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
 

@@ -75,7 +75,7 @@ struct RenderParams {
   int seg_per_item;             // consecutive segments one work item runs (>= 1)
   int pass_split;               // 1: one segment per pass (n_segments = n_passes; small launches)
   int depth, n_prims;
-  int lds_scene_bytes;          // > 0: stage the scene into LDS (<= kLdsSceneBytes, no meshes)
+  int lds_scene_bytes;          // > 0: stage the scene into LDS (<= kLdsSceneBytes)
   // triangle meshes (mcpt_upload_meshes; layouts: SceneT); n_meshes == 0: none
   const int4* minfo;
   const float4* mpairs;
@@ -92,8 +92,12 @@ struct RenderParams {
   float date, ior;
   // wave-uniform constants computed on the host (same binary32/binary64 operations as the
   // kernel would do) so that they live in SGPRs, not in spilled VGPRs: 1/ior (grefract of the
-  // inner exit), Schlick's ((ior-1)/(ior+1))^2, and cull_bound_sq(FLT_MAX) (walk start)
+  // inner exit), Schlick's ((ior-1)/(ior+1))^2, and cull_bound_sq(FLT_MAX) (walk start).
+  // ior², (1/ior)² and 1 - r0 too: computed in the kernel, the compiler hoisted them out of the
+  // render loop into VGPRs and spilled them (12 B of scratch written per lane and work item:
+  // ~0.4 GB of HBM writes per C4 launch, round 5)
   float inv_ior, schlick_r0;
+  float ior_sq, inv_ior_sq, schlick_1mr0;
   double cull2_max;
 };
 

@@ -131,10 +131,32 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? kMinWavesMesh
   // (primary hit), 9-11 N / 15-17 P saved across the inner traversal, 12-14 this segment's
   // sum (from 0 in pass order); s_hit0 = primary hit shape << 28 | index (-1: miss).
   // 19 KB per workgroup, + the staged scene (LDSS, <= kLdsSceneBytes): 7 workgroups/CU.
-  __shared__ float s_pix[18][kTileThreads];
+  // Kernels without a staged scene also keep the pixel's (u, v) there (rows 18-19), the mesh
+  // kernels its local index too (row 20): held in VGPRs across the render loop they were
+  // spilled registers, written to scratch once per lane and work item (C4: 1.16 -> 0.43 GB of
+  // HBM writes per launch, round 5, profiles/r05_ab_c4_spills.jsonl).  The LDS-scene kernel
+  // at 7 waves/SIMD has no room for them (7 x (22 + 3) KB > 160 KB) and does not spill them;
+  // the per-lane mesh kernels run 5 workgroups per CU, which leaves room.  (The local index in
+  // LDS cost C4 0.5 %: there it is recomputed.)
+  constexpr bool kPixLds = !LDSS || (MESH && !WAVE);
+  constexpr bool kPxLds = kPixLds && MESH;
+  // the refraction constants ior², (1/ior)², 1 - r0 from the host (RenderParams) in the same
+  // kernels: in the LDS-scene kernel they do not spill, and the in-kernel products are 0.8 %
+  // faster on C2 (same file)
+  constexpr bool kIorConst = kPixLds;
+  __shared__ float s_pix[kPxLds ? 21 : (kPixLds ? 20 : 18)][kTileThreads];
   __shared__ int s_hit0[kTileThreads];
   const f3 Dcam0 = camera_dir(p, u, v);
   s_pix[0][tid] = Dcam0.x; s_pix[1][tid] = Dcam0.y; s_pix[2][tid] = Dcam0.z;
+  if constexpr (kPixLds) {
+    s_pix[18][tid] = u; s_pix[19][tid] = v;
+    if constexpr (kPxLds) s_pix[20][tid] = __int_as_float(lr * p.W + x);   // < n_local_px <= 2^31 - 1 (mcpt_set_target*)
+  }
+  // (u, v) of this pixel for the seed of a new pass (seed_for): the same values as u, v above
+  auto pix_seed = [&](int ps) {
+    if constexpr (kPixLds) return seed_for(s_pix[18][tid], s_pix[19][tid], ps, p.date);
+    else return seed_for(((float)x + 0.5f) / (float)p.W, ((float)y + 0.5f) / (float)p.H, ps, p.date);
+  };
   s_pix[12][tid] = 0.0f; s_pix[13][tid] = 0.0f; s_pix[14][tid] = 0.0f;   // this segment's sum
   const f3 Ocam = mk(p.ox, p.oy, p.oz);
 
@@ -180,9 +202,14 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? kMinWavesMesh
   auto flush_sum = [&]() {
     // the pixel's address is recomputed at each flush (an empty asm makes the row opaque):
     // hoisted out of the render loop, its 64-bit index and pointer were 4 spilled VGPRs
-    int lrow = lr, col = x;
-    asm volatile("" : "+v"(lrow), "+v"(col));
-    const size_t px = (size_t)lrow * p.W + col;
+    size_t px;
+    if constexpr (kPxLds) {
+      px = (size_t)(unsigned)__float_as_int(s_pix[20][tid]);
+    } else {
+      int lrow = lr, col = x;
+      asm volatile("" : "+v"(lrow), "+v"(col));
+      px = (size_t)lrow * p.W + col;
+    }
     if (p.n_segments == 1) {
       float* accp = p.accum + px * 3;
       accp[0] = accp[0] + s_pix[12][tid]; accp[1] = accp[1] + s_pix[13][tid]; accp[2] = accp[2] + s_pix[14][tid];
@@ -284,7 +311,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? kMinWavesMesh
       pass++;
       next_chunk();
       if (pass < pass_end) {
-        rng = seed_for(((float)x + 0.5f) / (float)p.W, ((float)y + 0.5f) / (float)p.H, pass, p.date);
+        rng = pix_seed(pass);
         O = Ocam; D = mk(s_pix[0][tid], s_pix[1][tid], s_pix[2][tid]);
         att = mk(0.8f, 0.8f, 0.8f); total = mk(0.0f, 0.0f, 0.0f);
         bounce = 0;
@@ -337,7 +364,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? kMinWavesMesh
           f3 ray = random_ray(rng, N, 1.0f - m4.y);
           const f3 col = mk(c4.x, c4.y, c4.z);
           const float alpha = c4.w;
-          float rs = schlick(p.schlick_r0, D, N);
+          float rs = schlick(p.schlick_r0, kIorConst ? p.schlick_1mr0 : 1.0f - p.schlick_r0, D, N);
           f3 R = greflect(neg(ray), N);
           f3 E = normalize3(sub(O, P));
           float se = gmix(100.0f, 2.0f, m4.y);
@@ -354,7 +381,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? kMinWavesMesh
               // new_attenu of the pushed ray (att is not read again before the push)
               att = add(base, mulv(muls(muls(muls(att, 1.0f - alpha), 1.0f - rs), spec), mx));
               O = sub(P, muls(N, kBIAS));
-              D = grefract(D, N, ior);
+              D = grefract(D, N, ior, kIorConst ? p.ior_sq : ior * ior);
             } else if (alpha < 1.0f && m4.x > 0.0f) {
               float r = rnd(rng);
               if (r > 0.5f) {
@@ -403,7 +430,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? kMinWavesMesh
           P = mk(s_pix[15][tid], s_pix[16][tid], s_pix[17][tid]);
         }
         O = add(P, muls(N, kBIAS));
-        D = grefract(D, neg(N), p.inv_ior);
+        D = grefract(D, neg(N), p.inv_ior, kIorConst ? p.inv_ior_sq : p.inv_ior * p.inv_ior);
         phase = 0;
         bounce++;
         if (bounce >= B) done = true;
@@ -416,7 +443,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? kMinWavesMesh
       ev.inc(EV_SAMPLE);
       pass++;
       next_chunk();
-      rng = seed_for(((float)x + 0.5f) / (float)p.W, ((float)y + 0.5f) / (float)p.H, pass, p.date);   // = (u, v)
+      rng = pix_seed(pass);   // = (u, v)
       O = Ocam; D = mk(s_pix[0][tid], s_pix[1][tid], s_pix[2][tid]);
       att = mk(0.8f, 0.8f, 0.8f); total = mk(0.0f, 0.0f, 0.0f);
       bounce = 0; phase = 0;

@@ -163,14 +163,16 @@ __device__ __forceinline__ float gclamp(float x, float a, float b) { return gmin
 __device__ __forceinline__ float gmix(float x, float y, float a) { return x * (1.0f - a) + y * a; }
 __device__ __forceinline__ f3 gmix3(f3 x, f3 y, float a) { return mk(gmix(x.x, y.x, a), gmix(x.y, y.y, a), gmix(x.z, y.z, a)); }
 __device__ __forceinline__ f3 greflect(f3 I, f3 N) { return sub(I, muls(N, 2.0f * dot3(N, I))); }
-__device__ __forceinline__ f3 grefract(f3 I, f3 N, float eta) {
+// eta_sq = eta * eta (binary32), passed in when the caller has it as a host-computed constant
+__device__ __forceinline__ f3 grefract(f3 I, f3 N, float eta, float eta_sq) {
   float d = dot3(N, I);
-  float k = 1.0f - (eta * eta) * (1.0f - d * d);
+  float k = 1.0f - eta_sq * (1.0f - d * d);
   if (k < 0.0f) return mk(0.0f, 0.0f, 0.0f);
   // k >= 0 here is 0 or >= 2^-24 (1 - y for a float y < 1 is exact: y <= 1 - 2^-24, or
   // k > 0.5 when y < 0.5), or +inf / NaN: never in sqrt_core's inexact range (0, 2^-96)
   return sub(muls(I, eta), muls(N, eta * d + sqrt_core(k)));
 }
+__device__ __forceinline__ f3 grefract(f3 I, f3 N, float eta) { return grefract(I, N, eta, eta * eta); }
 
 // 3x4 affine rows (row r = (m[r], m[4+r], m[8+r], m[12+r]) of a column-major mat4)
 __device__ __forceinline__ f3 xpoint(float4 r0, float4 r1, float4 r2, f3 p) {

@@ -23,6 +23,8 @@ if ! has nopmc "${FLAGS[@]}"; then
   python tools/pmc_summary.py $O/pmc scene6_1920x1080_256spp_B8 $O/pmc_records.json > /dev/null &&
   bash tools/pmc.sh $O/pmc_c4 --config c4 && echo "pmc c4 ok" &&
   python tools/pmc_summary.py $O/pmc_c4 scene8_1920x1080_512spp_B12 $O/pmc_records.json > /dev/null &&
+  PMC_MEM=1 bash tools/pmc.sh $O/pmc_mesh --config mesh && echo "pmc mesh ok" &&
+  python tools/pmc_summary.py $O/pmc_mesh mesh1000k_1920x1080_64spp_B8 $O/pmc_records.json > /dev/null &&
   cp $O/pmc_records.json profiles/pmc_records.json || exit $?
 fi
 if has pmcall "${FLAGS[@]}"; then   # PMC records for the C3 line's dominant point, C5 and C1 too
@@ -38,6 +40,8 @@ has nobench "${FLAGS[@]}" && exit 0
 timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err && echo "bench ok" && cat $O/bench.json &&
 timeout -k 10 400 python bench.py --config c4 > $O/bench_c4.json 2> $O/bench_c4.err &&
 echo "bench c4 ok" && cat $O/bench_c4.json &&
+timeout -k 10 400 python bench.py --config mesh > $O/bench_mesh.json 2> $O/bench_mesh.err &&
+echo "bench mesh ok" && cat $O/bench_mesh.json &&
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline > $O/prof_bench.json 2> $O/prof.err && echo "prof ok" &&
 timeout -k 10 200 python bench.py --config c1 > $O/bench_c1.json 2> $O/bench_c1.err && echo "bench c1 ok" &&
 timeout -k 10 400 python bench.py --config c3 > $O/bench_c3.json 2> $O/bench_c3.err && echo "bench c3 ok" &&
@@ -51,6 +55,10 @@ MCPT_DIST_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 4 --steps 2 --wa
   > $O/bench_gloo4.json 2> $O/bench_gloo4.err && echo "gloo4 ok" &&
 MCPT_DIST_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 --steps 2 --warmup 1 --no-cpu-baseline --config c4 \
   > $O/bench_gloo2_c4.json 2> $O/bench_gloo2_c4.err && echo "gloo2 c4 ok" &&
+MCPT_DIST_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 8 --steps 2 --warmup 1 --no-cpu-baseline \
+  > $O/bench_gloo8.json 2> $O/bench_gloo8.err && echo "gloo8 ok" &&
+MCPT_DIST_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 8 --steps 2 --warmup 1 --no-cpu-baseline --scaling strong \
+  > $O/bench_gloo8_strong.json 2> $O/bench_gloo8_strong.err && echo "gloo8 strong ok" &&
 { timeout -k 10 120 python bench.py --gpus 2 --steps 1 --warmup 0 --no-cpu-baseline > $O/bench_nccl2_1gpu.json \
     2> $O/bench_nccl2_1gpu.err; rc=$?; echo "nccl2 on one GPU: exit $rc (expected non-zero, no line)";
   [ $rc -ne 0 ] && [ ! -s $O/bench_nccl2_1gpu.json ]; }
