@@ -7,7 +7,8 @@ montecarlo.frag.  A *step* = one full C2 frame: passes [k·256+1, (k+1)·256] ac
 into the device framebuffer, then the frame gathered to rank 0 (RCCL gather for N>1).
 Scene buffers and the framebuffer are resident in HBM before the timed region.
 
-    python bench.py [--gpus N --steps K --warmup W] [--config c1|c2|c3|c4|c5] [--rough R]
+    python bench.py [--gpus N --steps K --warmup W] [--config c1|c2|c3|c4|c5|mesh] [--rough R]
+                    [--scaling weak|strong] [--deadline S]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
 Launch: with ``--gpus N > 1`` and no launcher (``WORLD_SIZE`` unset) the process starts N
@@ -39,6 +40,17 @@ Configs (BASELINE.json ``configs``):
   as an extrapolation, not a measured run of the whole target).
 * c1 (configs[0], the reference's CPU case) — scene 1, 256², 4 spp, B 3: launch-bound on the
   GPU; its `cpu_baseline` times the whole config.
+* mesh (round 5; SURVEY §8 (f)2, the triangle-mesh row) — two instances of one 1 M-triangle UV
+  sphere (mesh BVH depth 20, 128 MB of mesh records: mcpt.meshes.big_mesh_scene), a ground
+  cube, a glass sphere and a light quad; 1080p, 64 spp, B 8, strong.  Its walk is a chain of
+  dependent mesh-record fetches from the Infinity Cache / HBM, so its `roofline.bound` is
+  "hbm": `achieved` = the §8d algorithmic bytes (counting build of the same kernel) ÷ the
+  launch time, `traffic` = the PMC fabric bytes, `traffic_ratio` = traffic ÷ algorithmic, the
+  VALU figures under `roofline.valu`.
+``--scaling strong`` runs c2 / c3 as one fixed frame split over the N ranks (the driver's
+default N-GPU runs stay weak); the line's `scaling` says which.  ``--deadline S`` bounds every
+rank's wall time (and the launcher's, + 15 s): a rank past it prints its current phase
+(``PHASES``) and exits 124, and the launcher names the least advanced rank and its phase.
 
 Prints ONE JSON line (rank 0) with
 * `roofline` for the dominant kernel (the path-tracing kernel).  Its limiter is VALU issue,
