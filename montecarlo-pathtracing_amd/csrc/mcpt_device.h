@@ -446,11 +446,9 @@ __device__ __forceinline__ void rcp6_rn(float4 wl, float4 wr, f3& il, f3& ir) {
 // round trip (all four rows issued together: a visit waits for one fetch), 1/w recomputed
 template <bool COUNT, class SR>
 __device__ __forceinline__ void mesh_pair_tests(const SR& s, size_t node, f3 O, f3 D, f3 invD, f3 Ol, float4 t0,
-                                                float4 t1, float4 t2, double cull2, bool& hl, bool& hr,
-                                                const int* prefetch = nullptr, int* prefetched = nullptr) {
+                                                float4 t1, float4 t2, double cull2, bool& hl, bool& hr) {
   const float4* q = s.mpairs + node * 4;
   const float4 a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
-  if (prefetch) *prefetched = *prefetch;   // issued after the rows: their wait does not include it
   MCPT_ROWS_IN("v"(a0.x), "v"(a0.y), "v"(a0.z), "v"(a0.w), "v"(a1.x), "v"(a1.y), "v"(a1.z));
   MCPT_ROWS_IN("v"(a2.x), "v"(a2.y), "v"(a2.z), "v"(a2.w), "v"(a3.x), "v"(a3.y), "v"(a3.z));
   MCPT_ROWS_IN("v"(t0.x), "v"(t0.y), "v"(t0.z), "v"(t0.w), "v"(t1.x), "v"(t1.y), "v"(t1.z), "v"(t1.w),
@@ -899,26 +897,37 @@ __device__ __forceinline__ bool walk_run_mesh(const SR& s, f3 O, f3 D, Hit& h, W
       const float4 t0 = tp[0], t1 = tp[1], t2 = tp[2];
       const int mleaf0 = (1 << mi.z) - 1;
       bool mpop = true;
-      if (w.mnode >= mleaf0) {
+      // one record per lane and step, node or leaf alike (64 B: a child-pair record, or a leaf's
+      // triangle record), issued before the lanes split into the node and leaf blocks: the wave
+      // waits once per iteration instead of once per block (measured neutral on the mesh
+      // workload, r05_ab_mesh_prefetch.jsonl session r05x; kept as the simpler form)
+      const bool mleaf = w.mnode >= mleaf0;
+      const size_t j = 2 * (size_t)w.mnode + 1;
+      const float4* q = mleaf ? s.mleaftris + ((size_t)mi.y + (w.mnode - mleaf0)) * 4
+                              : s.mpairs + ((size_t)mi.x + mesh_pair_slot(w.mnode)) * 4;
+      // node lanes also request their children's line (both pair records, or the two leaf
+      // records of the last level), consumed one step later: +0.9..1.4 % on the mesh workload;
+      // the grandchildren's two lines as well: -5..8 % (profiles/r05_ab_mesh_prefetch.jsonl)
+      const float4* qc = mleaf ? q
+                               : ((w.mlevel + 1 < mi.z) ? s.mpairs + ((size_t)mi.x + mesh_pair_slot((unsigned)j)) * 4
+                                                        : s.mleaftris + ((size_t)mi.y + (j - mleaf0)) * 4);
+      const float4 a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
+      asm volatile("" ::"v"(w.mpf));
+      w.mpf = *(const int*)qc;
+      MCPT_ROWS_IN("v"(a0.x), "v"(a0.y), "v"(a0.z), "v"(a0.w), "v"(a1.x), "v"(a1.y), "v"(a1.z));
+      MCPT_ROWS_IN("v"(a2.x), "v"(a2.y), "v"(a2.z), "v"(a2.w), "v"(a3.x), "v"(a3.y), "v"(a3.z));
+      MCPT_ROWS_IN("v"(t0.x), "v"(t0.y), "v"(t0.z), "v"(t0.w), "v"(t1.x), "v"(t1.y), "v"(t1.z), "v"(t1.w),
+                   "v"(t2.x), "v"(t2.y), "v"(t2.z), "v"(t2.w));
+      if (mleaf) {
         ev.inc(EV_LEAF);
-        mesh_leaf<COUNT>(s, (size_t)mi.y + (w.mnode - mleaf0), w.mprim, w.Om, w.Dm, O, t0, t1, t2, h, ev);
+        const int t = __float_as_int(a0.w);
+        if (t >= 0) tri_test<COUNT, SR>(t, a0, a1, a2, w.mprim, w.Om, w.Dm, O, t0, t1, t2, h, ev);
       } else {
         ev.inc(EV_NODE);
-        const size_t j = 2 * (size_t)w.mnode + 1;
-        bool hl, hr;
-        {
-          // the children's records (both in one 128-byte line: their pair records, or the leaf
-          // triangle records of the last level) are requested with this node's, so that the
-          // step that descends finds its record in L1/L2; the dummy value is consumed one step
-          // later, when the load has long returned.  +0.9..1.4 % on the mesh workload; the
-          // grandchildren's two lines as well: -5..8 % (profiles/r05_ab_mesh_prefetch.jsonl)
-          asm volatile("" ::"v"(w.mpf));
-          const size_t line = (w.mlevel + 1 < mi.z) ? ((size_t)mi.x + mesh_pair_slot((unsigned)j)) * 4
-                                                    : 0;
-          const float4* q = (w.mlevel + 1 < mi.z) ? s.mpairs + line : s.mleaftris + ((size_t)mi.y + (j - mleaf0)) * 4;
-          mesh_pair_tests<COUNT>(s, (size_t)mi.x + mesh_pair_slot(w.mnode), w.Om, w.Dm, w.invDm, O,
-                                 t0, t1, t2, h.cull2, hl, hr, (const int*)q, &w.mpf);
-        }
+        f3 il, ir;
+        rcp6_rn(a1, a3, il, ir);
+        const bool hl = (COUNT || a0.w != 0.0f) && box_test_mesh(a0, a1, il, w.Om, w.Dm, w.invDm, O, t0, t1, t2, h.cull2);
+        const bool hr = (COUNT || a2.w != 0.0f) && box_test_mesh(a2, a3, ir, w.Om, w.Dm, w.invDm, O, t0, t1, t2, h.cull2);
         mpop = !(hl || hr);
         if (hr) {
           if (hl) w.mpending |= 1u << (w.mlevel + 1);

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Section shares from the diagnostic stamp build (MCPT_LIB=.../libmcpt_stamps.so).
 
-Per scene/traversal mode: wave-cycles in the primary-ray prelude, in traversal rounds and
+Per scene/traversal mode (--mesh: the mesh workload, "scene" 0): wave-cycles in the primary-ray prelude, in traversal rounds and
 in shading rounds, and the lane utilisation of the rounds (participating lanes /
 (64 x rounds)).  Shares only: stamps perturb timing.
 """
@@ -37,8 +37,12 @@ if "--stream" in sys.argv:
     sys.exit(0)
 r.set_target(W, H)
 ipv, iv = mcpt.camera_canonical(W, H)
-for sid, B in [(6, 8), (3, 8), (8, 12)]:
-    r.upload_scene(mcpt.Scene.reference(sid))
+CASES = [(6, 8), (3, 8), (8, 12)]
+if "--mesh" in sys.argv:   # the mesh workload (bench.py --config mesh), per-lane walk
+    from mcpt import meshes
+    CASES = [(0, 8)]
+for sid, B in CASES:
+    r.upload_scene(meshes.big_mesh_scene(1_000_000)[0] if sid == 0 else mcpt.Scene.reference(sid))
     for mode in (1,):
         r.set_traversal(mode)
         r.debug_counters(reset=True)
