@@ -133,7 +133,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? kMinWavesMesh
   // 19 KB per workgroup, + the staged scene (LDSS, <= kLdsSceneBytes): 7 workgroups/CU.
   // Kernels without a staged scene also keep the pixel's (u, v) there (rows 18-19), the mesh
   // kernels its local index too (row 20): held in VGPRs across the render loop they were
-  // spilled registers, written to scratch once per lane and work item (C4: 1.16 -> 0.43 GB of
+  // spilled registers, written to scratch once per lane and work item (C4: 1.16 -> 0.50 GB of
   // HBM writes per launch, round 5, profiles/r05_ab_c4_spills.jsonl).  The LDS-scene kernel
   // at 7 waves/SIMD has no room for them (7 x (22 + 3) KB > 160 KB) and does not spill them;
   // the per-lane mesh kernels run 5 workgroups per CU, which leaves room.  (The local index in
