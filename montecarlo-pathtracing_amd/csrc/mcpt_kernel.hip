@@ -69,7 +69,11 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? kMinWavesMesh
     RenderParams p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
+  // (XCD-aware remaps of the item order measured slower or within noise: giving each XCD one
+  // contiguous 1/8 of the items unbalances the XCDs — C2 -39 %, mesh -10..18 %, C4 -4 % —
+  // and chunks of 4 / 32 items per XCD change nothing; profiles/r05_ab_xcd_item_order.jsonl)
   const int item = blockIdx.x;
+
   // segment-fastest item order: the pass segments of one tile are consecutive workgroups
   // (tile-fastest order was 1-12 % slower on one GPU and 7 % on a 1/8-row shard's launch:
   // profiles/r01_ab42_item_order.jsonl)

@@ -382,6 +382,11 @@ def test_set_target_rows_rejects_bad_rows(mcpt_mod, renderer):
             renderer.set_target_rows(8, 5, rows)
     renderer.set_target_rows(8, 5, [4, 0])
     assert renderer.local_row_ids().tolist() == [4, 0]
+    # a shard of 2^31 pixels or more is refused before any allocation (the kernels index a
+    # shard's pixels with 32-bit ints); the context keeps its target
+    with pytest.raises(mcpt_mod.MCPTError):
+        renderer.set_target(1 << 16, 1 << 15)
+    assert renderer.local_row_ids().tolist() == [4, 0]
 
 
 def test_empty_and_tiny_shards(mcpt_mod, renderer):
