@@ -57,6 +57,11 @@ int mcpt_err_bare(int status) {
 constexpr size_t kDefaultPartialBudget = size_t(4) << 30;
 // render calls whose events a context keeps (mcpt_kernel_ms_back)
 constexpr int kTimingRing = 64;
+// work-item order (mcpt_order.hip): launches with at least this many work items run in the
+// order sorted from an earlier launch of their shape; the order is re-sorted every
+// kOrderRefresh launches of the shape (costs drift little: the same tiles and pass counts)
+constexpr long long kOrderMinItems = 4096;
+constexpr int kOrderRefresh = 16;
 
 struct mcpt_ctx {
   int device = 0;
@@ -133,6 +138,18 @@ struct mcpt_ctx {
   int stream_slots = 0;             // MCPT_STREAM_SLOTS env / mcpt_set_stream_pool (0: default)
   int stream_refill = -1;           // MCPT_STREAM_REFILL env / mcpt_set_stream_pool (-1: default)
   long long stream_iters = 0;       // iterations of the last stream render (diagnostics)
+  // work-item order (mcpt_order.hip): item costs of the last ordered launch, the order sorted
+  // from them (costliest first) and the launch shape it belongs to
+  unsigned* d_item_cost = nullptr;
+  unsigned* d_cost_sorted = nullptr;
+  int* d_item_iota = nullptr;
+  int* d_item_perm = nullptr;
+  void* d_sort_tmp = nullptr;
+  size_t sort_tmp_bytes = 0;
+  long long item_cap = 0;
+  long long order_key[8] = {};
+  bool order_valid = false;
+  int order_age = 0;                // launches since the order was last sorted
 };
 
 // events of sub-launch k of the last call: start / mid / stop
@@ -252,6 +269,7 @@ static int cand_traversal(int cand) { return cand >= kCandLaneSeg2 ? MCPT_TRAVER
 static int resolve_traversal(const mcpt_ctx* c) { return cand_traversal(resolve_candidate(c, c->meas_segs)); }
 
 static void reset_tuning(mcpt_ctx* c) {
+  c->order_valid = false;           // a new scene / target: item costs start over
   c->tune_pending = 0;
   c->tune_samples = 0.0;
   c->tune_shape[0] = c->tune_shape[1] = c->meas_shape[0] = c->meas_shape[1] = 0;
@@ -339,8 +357,15 @@ int mcpt_create(int device_ordinal, mcpt_ctx** out) {
   hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = ensure_events(c, 0, 1);
   if (const char* pb = std::getenv("MCPT_PARTIAL_BYTES")) c->partial_budget = (size_t)std::strtoull(pb, nullptr, 10);
-  if (e == hipSuccess) e = hipMalloc(&c->d_events, sizeof(unsigned long long) * MCPT_DEBUG_SLOTS);
-  if (e == hipSuccess) e = hipMemset(c->d_events, 0, sizeof(unsigned long long) * MCPT_DEBUG_SLOTS);
+#ifdef MCPT_BLOCKTIMES
+  // diagnostic build: per-wave (start, end) clock pairs after the debug slots
+  static_assert(mcpt::kBlockTimeBase == MCPT_DEBUG_SLOTS, "block times follow the debug slots");
+  constexpr size_t kEventSlots = MCPT_DEBUG_SLOTS + mcpt::kBlockTimeSlots;
+#else
+  constexpr size_t kEventSlots = MCPT_DEBUG_SLOTS;
+#endif
+  if (e == hipSuccess) e = hipMalloc(&c->d_events, sizeof(unsigned long long) * kEventSlots);
+  if (e == hipSuccess) e = hipMemset(c->d_events, 0, sizeof(unsigned long long) * kEventSlots);
   if (e != hipSuccess) { mcpt_destroy(c); return set_err(MCPT_ERR_HIP, "mcpt_create", e); }
   c->stream = c->own_stream;
   *out = c;
@@ -371,6 +396,11 @@ int mcpt_destroy(mcpt_ctx* c) {
   (void)hipFree(c->d_rows);
   (void)hipFree(c->d_events);
   (void)hipFree(c->d_partial);
+  (void)hipFree(c->d_item_cost);
+  (void)hipFree(c->d_cost_sorted);
+  (void)hipFree(c->d_item_iota);
+  (void)hipFree(c->d_item_perm);
+  (void)hipFree(c->d_sort_tmp);
   (void)hipFree(c->d_slots);
   (void)hipFree(c->d_queue);
   (void)hipFree(c->d_sctr);
@@ -624,6 +654,7 @@ static int set_target_rows(mcpt_ctx* c, int W, int H, const int* rows, int n_row
   if (n_rows) HIP_OR_RETURN(hipMemcpy(c->d_rows, rows, sizeof(int) * (size_t)n_rows, hipMemcpyHostToDevice));
   c->W = W; c->H = H; c->band_rows = band_rows; c->world = world; c->rank = rank; c->n_local_rows = n_rows;
   c->has_target = true;
+  c->order_valid = false;   // other pixels: the item costs start over
   return mcpt_clear_accum(c);
 }
 
@@ -884,6 +915,31 @@ static int free_stream_pools(mcpt_ctx* c) {
   return MCPT_OK;
 }
 
+// Buffers of the work-item order for `items` items (grown on demand, with the identity values
+// the sort permutes and its temporary storage)
+static hipError_t ensure_item_order(mcpt_ctx* c, long long items) {
+  if (items <= c->item_cap) return hipSuccess;
+  hipError_t e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) return e;
+  (void)hipFree(c->d_item_cost); (void)hipFree(c->d_cost_sorted); (void)hipFree(c->d_item_iota);
+  (void)hipFree(c->d_item_perm); (void)hipFree(c->d_sort_tmp);
+  c->d_item_cost = c->d_cost_sorted = nullptr; c->d_item_iota = c->d_item_perm = nullptr; c->d_sort_tmp = nullptr;
+  c->item_cap = 0; c->sort_tmp_bytes = 0; c->order_valid = false;
+  const size_t n = (size_t)items;
+  size_t tmp = 0;
+  if ((e = hipMalloc(&c->d_item_cost, sizeof(unsigned) * n)) != hipSuccess) return e;
+  if ((e = hipMalloc(&c->d_cost_sorted, sizeof(unsigned) * n)) != hipSuccess) return e;
+  if ((e = hipMalloc(&c->d_item_iota, sizeof(int) * n)) != hipSuccess) return e;
+  if ((e = hipMalloc(&c->d_item_perm, sizeof(int) * n)) != hipSuccess) return e;
+  if ((e = mcpt_order_items(nullptr, nullptr, nullptr, nullptr, (int)items, nullptr, &tmp, c->stream)) != hipSuccess)
+    return e;
+  if ((e = hipMalloc(&c->d_sort_tmp, std::max<size_t>(tmp, 1))) != hipSuccess) return e;
+  if ((e = mcpt_iota(c->d_item_iota, (int)items, c->stream)) != hipSuccess) return e;
+  c->sort_tmp_bytes = tmp;
+  c->item_cap = items;
+  return hipSuccess;
+}
+
 static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_pass, int n_passes, float date,
                   int bounces, float refract_ind, int variant, bool count, unsigned long long* events) {
   if (!c || !invPV || !invV || n_passes < 0 || variant < 0 || variant > 2)
@@ -1006,6 +1062,22 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
     p.first_pass = (int)lo;
     p.n_passes = (int)(hi - lo);
     p.n_segments = split ? p.n_passes : fdiv((int)(hi - 2), mcpt::kPassChunk) - (int)c0 + 1;
+    // work-item order (mcpt_order.hip): launches of >= kOrderMinItems items run the order
+    // sorted from an earlier launch of the same shape and measure their items for the next sort
+    const int kseg = p.seg_per_item > 1 ? p.seg_per_item : 1;
+    const long long items = (long long)p.n_tiles * ((p.n_segments + kseg - 1) / kseg);
+    const long long key[8] = {items, p.n_segments, kseg, p.wave_traversal, p.walk_exit, bounces, variant,
+                              (long long)p.pass_split};
+    // (MCPT_ITEM_ORDER=0: dispatch order b = item, tests and A/B; the same bits either way)
+    const bool order = !count && !stream && items >= kOrderMinItems && env_int("MCPT_ITEM_ORDER", 1) != 0;
+    p.item_perm = nullptr;
+    p.item_cost = nullptr;
+    if (order) {
+      HIP_OR_RETURN(ensure_item_order(c, items));
+      if (c->order_valid && std::equal(key, key + 8, c->order_key)) p.item_perm = c->d_item_perm;
+      HIP_OR_RETURN(hipMemsetAsync(c->d_item_cost, 0, sizeof(unsigned) * (size_t)items, c->stream));
+      p.item_cost = c->d_item_cost;
+    }
     HIP_OR_RETURN(hipEventRecord(ev_at(c, slot, (int)k, 0), c->stream));
     if (stream) {
       const int st = stream_run(c, p);
@@ -1016,6 +1088,16 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
     HIP_OR_RETURN(hipEventRecord(ev_at(c, slot, (int)k, 1), c->stream));
     HIP_OR_RETURN(mcpt_launch_combine(p, c->stream));
     HIP_OR_RETURN(hipEventRecord(ev_at(c, slot, (int)k, 2), c->stream));
+    if (order && (!p.item_perm || ++c->order_age >= kOrderRefresh)) {
+      // sorted after this launch (outside its timed events); the next launch of this shape
+      // reads the order in stream order, so no host wait
+      size_t tmp = c->sort_tmp_bytes;
+      HIP_OR_RETURN(mcpt_order_items(c->d_item_cost, c->d_cost_sorted, c->d_item_iota, c->d_item_perm, (int)items,
+                                     c->d_sort_tmp, &tmp, c->stream));
+      std::copy(key, key + 8, c->order_key);
+      c->order_valid = true;
+      c->order_age = 0;
+    }
     lo = hi;
   }
   if (!count && c->traversal == MCPT_TRAVERSAL_AUTO && !c->tune_choice && samples >= kTuneMinSamples) {
@@ -1062,6 +1144,20 @@ int mcpt_debug_counters(mcpt_ctx* c, unsigned long long* out, int n_slots, int r
   HIP_OR_RETURN(hipStreamSynchronize(c->stream));
   return MCPT_OK;
 }
+
+#ifdef MCPT_BLOCKTIMES
+// diagnostic build only: the per-wave (start, end) clock pairs of the last render launch
+// (wave w of work item i at 2 (4 i + w)), zeroed after the copy
+extern "C" int mcpt_debug_blocktimes(mcpt_ctx* c, unsigned long long* out, long long n) {
+  if (!c || !out || n < 0 || (size_t)n > mcpt::kBlockTimeSlots) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
+  HIP_OR_RETURN(hipSetDevice(c->device));
+  HIP_OR_RETURN(hipMemcpyAsync(out, c->d_events + MCPT_DEBUG_SLOTS, sizeof(unsigned long long) * n,
+                               hipMemcpyDeviceToHost, c->stream));
+  HIP_OR_RETURN(hipMemsetAsync(c->d_events + MCPT_DEBUG_SLOTS, 0, sizeof(unsigned long long) * mcpt::kBlockTimeSlots, c->stream));
+  HIP_OR_RETURN(hipStreamSynchronize(c->stream));
+  return MCPT_OK;
+}
+#endif
 
 int mcpt_event_bytes(int e) {
   if (e < 0 || e >= mcpt::EV_COUNT) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);

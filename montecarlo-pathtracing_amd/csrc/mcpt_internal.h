@@ -36,6 +36,10 @@ constexpr int kNodeF4 = 3;
 // inside each chunk of kPassChunk consecutive absolute pass numbers, chunk sums added to
 // the accumulator in chunk order
 constexpr int kPassChunk = 32;
+#ifdef MCPT_BLOCKTIMES
+constexpr size_t kBlockTimeSlots = size_t(8) << 20;   // diagnostic build: per-wave clock pairs
+constexpr size_t kBlockTimeBase = 64;                   // after the debug slots (= MCPT_DEBUG_SLOTS)
+#endif
 // largest scene render_kernel stages into LDS: 160 KB / 7 workgroups - 19 KB of per-pixel rows
 constexpr int kLdsSceneBytes = 3584;
 constexpr int kPrimF4 = 8;
@@ -98,6 +102,11 @@ struct RenderParams {
   // ~0.4 GB of HBM writes per C4 launch, round 5)
   float inv_ior, schlick_r0;
   float ior_sq, inv_ior_sq, schlick_1mr0;
+  // work-item order (mcpt_order.hip): workgroup b runs item item_perm[b] (null: item b), the
+  // items sorted costliest first from an earlier launch of the same shape; item_cost[i] gets
+  // item i's longest wave time of this launch (100 MHz clock ticks; null: not measured)
+  const int* item_perm;
+  unsigned* item_cost;
   double cull2_max;
 };
 
@@ -180,6 +189,9 @@ hipError_t mcpt_launch_trace(const mcpt::TraceParams& q, bool any_hit, hipStream
 hipError_t mcpt_launch_sample(const mcpt::SampleParams& q, hipStream_t stream);
 hipError_t mcpt_launch_render(const mcpt::RenderParams& p, bool count, hipStream_t stream);
 hipError_t mcpt_launch_combine(const mcpt::RenderParams& p, hipStream_t stream);
+hipError_t mcpt_iota(int* a, int n, hipStream_t stream);
+hipError_t mcpt_order_items(const unsigned* cost, unsigned* cost_sorted, const int* iota, int* perm, int n,
+                            void* tmp, size_t* tmp_bytes, hipStream_t stream);
 // stream schedule: slot set-up (queue[0] = every slot with a unit), then one iteration = the
 // trace kernel over queue[parity] + the shade kernel appending to queue[parity ^ 1]
 hipError_t mcpt_launch_stream_init(const mcpt::StreamParams& q, hipStream_t stream);

@@ -72,7 +72,14 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? kMinWavesMesh
   // (XCD-aware remaps of the item order measured slower or within noise: giving each XCD one
   // contiguous 1/8 of the items unbalances the XCDs — C2 -39 %, mesh -10..18 %, C4 -4 % —
   // and chunks of 4 / 32 items per XCD change nothing; profiles/r05_ab_xcd_item_order.jsonl)
-  const int item = blockIdx.x;
+  // the launch's work-item order (mcpt_order.hip): costliest items of an earlier launch first
+  const int item = p.item_perm ? p.item_perm[blockIdx.x] : (int)blockIdx.x;
+  const unsigned long long t_item0 = __builtin_amdgcn_s_memrealtime();
+#ifdef MCPT_BLOCKTIMES
+  // diagnostic build only (tools/blocktimes.py; never timed): each wave's start and end on the
+  // 100 MHz real-time clock, for the launch's occupancy over time (tail, XCD balance)
+  const unsigned long long bt0 = __builtin_amdgcn_s_memrealtime();
+#endif
 
   // segment-fastest item order: the pass segments of one tile are consecutive workgroups
   // (tile-fastest order was 1-12 % slower on one GPU and 7 % on a 1/8-row shard's launch:
@@ -488,6 +495,19 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? kMinWavesMesh
   }
 #endif
 
+  if (p.item_cost && (int)__lane_id() == __builtin_ffsll((long long)__ballot(1)) - 1) {
+    // this item's cost for the next launch's order: its longest wave (100 MHz ticks)
+    const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t_item0;
+    atomicMax(p.item_cost + item, dt < 0xffffffffull ? (unsigned)dt : 0xffffffffu);
+  }
+#ifdef MCPT_BLOCKTIMES
+  {
+    const unsigned long long bt1 = __builtin_amdgcn_s_memrealtime();
+    const int lead = __builtin_ffsll((long long)__ballot(1)) - 1, k = (int)__lane_id() - lead;
+    if ((k == 0 || k == 1) && p.events)   // two lanes, one value each (vector stores)
+      p.events[kBlockTimeBase + 2ull * ((unsigned long long)item * (kTileThreads / 64) + wave) + k] = k ? bt1 : bt0;
+  }
+#endif
 #ifdef MCPT_LANESTATS
   if (ls_lead() && p.events)
     for (int k = 0; k < LS_COUNT; ++k) atomicAdd(p.events + 16 + k, (unsigned long long)ls_row()[k]);

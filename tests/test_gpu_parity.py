@@ -546,3 +546,20 @@ def test_kernel_ms_back_ring(mcpt_mod, renderer):
             r2.kernel_ms_back(0)
     finally:
         r2.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene_id,traversal", [(6, 1), (8, 1), (3, 2)])
+def test_item_order_same_bits(mcpt_mod, renderer, monkeypatch, scene_id, traversal):
+    """The work-item order (mcpt_order.hip): launches of >= 4,096 items run their items
+    costliest-first, sorted from the previous launch of the same shape.  Which workgroup runs an
+    item never changes what it computes: three chunked calls (the first in launch order, the
+    others in the measured order, one of them re-sorted) equal the same passes with the order
+    off (MCPT_ITEM_ORDER=0), bit for bit (the unordered path is the one the oracle tests pin)."""
+    W, H, B = 1920, 1080, 4
+    chunks = [32, 32, 64]   # 8,100 tiles x 1-2 segments per launch
+    monkeypatch.setenv("MCPT_ITEM_ORDER", "1")
+    ordered = _gpu(mcpt_mod, renderer, scene_id, W, H, 1, 128, B, split=chunks, traversal=traversal)
+    monkeypatch.setenv("MCPT_ITEM_ORDER", "0")
+    plain = _gpu(mcpt_mod, renderer, scene_id, W, H, 1, 128, B, split=chunks, traversal=traversal)
+    assert np.array_equal(ordered.view(np.uint32), plain.view(np.uint32))
