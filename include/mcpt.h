@@ -149,8 +149,9 @@ int mcpt_event_bytes(int event);
 #define MCPT_DEBUG_SLOTS 64
 /* Diagnostics: read the first min(n_slots, MCPT_DEBUG_SLOTS) of the context's device counter
  * slots into `out` (which holds n_slots values; the first MCPT_EV_COUNT are the event counters)
- * and optionally zero them all.  Only the counting launches and diagnostic builds
- * (-DMCPT_STAMPS: wave-cycle section totals; -DMCPT_LANESTATS) write them.  Synchronizes the
+ * and optionally zero them all.  The counting launches and diagnostic builds (-DMCPT_STAMPS:
+ * wave-cycle section totals; -DMCPT_LANESTATS) write them; slot 63 holds how many work items
+ * the last work-item sort of a mesh scene's launch chose to split.  Synchronizes the
  * context's stream.  (Version 2: the n_slots argument; version 1 copied MCPT_DEBUG_SLOTS
  * values, 16 before round 4, whatever the caller's buffer held.) */
 int mcpt_debug_counters(mcpt_ctx* ctx, unsigned long long* out, int n_slots, int reset);

@@ -62,6 +62,9 @@ constexpr int kTimingRing = 64;
 // kOrderRefresh launches of the shape (costs drift little: the same tiles and pass counts)
 constexpr long long kOrderMinItems = 4096;
 constexpr int kOrderRefresh = 16;
+// split items (mesh launches): at most this many of the costliest items run in
+// mcpt::kSplitPieces pass ranges each (RenderParams::split_n; 100 MB of per-pass values)
+constexpr int kSplitMax = 1024;
 
 struct mcpt_ctx {
   int device = 0;
@@ -144,6 +147,9 @@ struct mcpt_ctx {
   unsigned* d_cost_sorted = nullptr;
   int* d_item_iota = nullptr;
   int* d_item_perm = nullptr;
+  int* d_split_of = nullptr;        // split items: item -> split index (-1: whole)
+  float* d_split_pass = nullptr;    // split items: the later pieces' per-pass values
+  int* d_split_n = nullptr;         // split items: how many (from the last sort)
   void* d_sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
   long long item_cap = 0;
@@ -400,6 +406,9 @@ int mcpt_destroy(mcpt_ctx* c) {
   (void)hipFree(c->d_cost_sorted);
   (void)hipFree(c->d_item_iota);
   (void)hipFree(c->d_item_perm);
+  (void)hipFree(c->d_split_of);
+  (void)hipFree(c->d_split_pass);
+  (void)hipFree(c->d_split_n);
   (void)hipFree(c->d_sort_tmp);
   (void)hipFree(c->d_slots);
   (void)hipFree(c->d_queue);
@@ -922,8 +931,9 @@ static hipError_t ensure_item_order(mcpt_ctx* c, long long items) {
   hipError_t e = hipStreamSynchronize(c->stream);
   if (e != hipSuccess) return e;
   (void)hipFree(c->d_item_cost); (void)hipFree(c->d_cost_sorted); (void)hipFree(c->d_item_iota);
-  (void)hipFree(c->d_item_perm); (void)hipFree(c->d_sort_tmp);
+  (void)hipFree(c->d_item_perm); (void)hipFree(c->d_sort_tmp); (void)hipFree(c->d_split_of);
   c->d_item_cost = c->d_cost_sorted = nullptr; c->d_item_iota = c->d_item_perm = nullptr; c->d_sort_tmp = nullptr;
+  c->d_split_of = nullptr;
   c->item_cap = 0; c->sort_tmp_bytes = 0; c->order_valid = false;
   const size_t n = (size_t)items;
   size_t tmp = 0;
@@ -931,6 +941,9 @@ static hipError_t ensure_item_order(mcpt_ctx* c, long long items) {
   if ((e = hipMalloc(&c->d_cost_sorted, sizeof(unsigned) * n)) != hipSuccess) return e;
   if ((e = hipMalloc(&c->d_item_iota, sizeof(int) * n)) != hipSuccess) return e;
   if ((e = hipMalloc(&c->d_item_perm, sizeof(int) * n)) != hipSuccess) return e;
+  if ((e = hipMalloc(&c->d_split_of, sizeof(int) * n)) != hipSuccess) return e;
+  if (!c->d_split_n && (e = hipMalloc(&c->d_split_n, sizeof(int))) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(c->d_split_n, 0, sizeof(int), c->stream)) != hipSuccess) return e;
   if ((e = mcpt_order_items(nullptr, nullptr, nullptr, nullptr, (int)items, nullptr, &tmp, c->stream)) != hipSuccess)
     return e;
   if ((e = hipMalloc(&c->d_sort_tmp, std::max<size_t>(tmp, 1))) != hipSuccess) return e;
@@ -966,7 +979,8 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   p.mverts = c->d_mverts; p.mnorms = c->d_mnorms; p.n_meshes = c->n_meshes; p.flat_face = c->flat_face;
   HIP_OR_RETURN(collect_tuning(c));
   // (the counting build is not timed: AUTO counts with the per-lane walk)
-  p.n_tiles = ((c->W + mcpt::kTileW - 1) / mcpt::kTileW) * ((c->n_local_rows + mcpt::kTileH - 1) / mcpt::kTileH);
+  p.tile_w = mcpt::tile_w_for(c->n_meshes > 0, p.lds_scene_bytes > 0);
+  p.n_tiles = ((c->W + p.tile_w - 1) / p.tile_w) * ((c->n_local_rows + mcpt::kTileH - 1) / mcpt::kTileH);
   auto fdiv = [](int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); };
   const long long total_seg = n_passes > 0 ? fdiv(first_pass + n_passes - 2, mcpt::kPassChunk) -
                                                  fdiv(first_pass - 1, mcpt::kPassChunk) + 1
@@ -1014,7 +1028,7 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   // segment sums in one launch).  Chunk sums still reach the accumulator in chunk order, so
   // the result is bit-identical to one launch.
   const long long seg_bytes = p.n_local_px * 3 * (long long)sizeof(float);
-  const long long max_items = (1LL << 32) / mcpt::kTileThreads - 1;
+  const long long max_items = (1LL << 32) / (p.tile_w * mcpt::kTileH) - 1;
   if (p.n_tiles > max_items) return set_err(MCPT_ERR_INVALID_ARG, "render target too large for one launch");
   long long max_seg = seg_bytes > 0 ? (long long)(c->partial_budget / (size_t)seg_bytes) : (1LL << 30);
   max_seg = std::max(1LL, std::min(max_seg, p.n_tiles > 0 ? max_items / p.n_tiles : max_items));
@@ -1072,11 +1086,28 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
     const bool order = !count && !stream && items >= kOrderMinItems && env_int("MCPT_ITEM_ORDER", 1) != 0;
     p.item_perm = nullptr;
     p.item_cost = nullptr;
+    p.split_n = nullptr; p.split_of = nullptr; p.split_pass = nullptr; p.split_max = 0;
+    p.n_items = (int)items;
+    // split items: mesh launches of whole 32-pass segments, one per item (MCPT_SPLIT_ITEMS=0: off)
+    const bool split_items = order && c->n_meshes > 0 && !p.wave_traversal && kseg == 1 && !p.pass_split &&
+                             p.n_segments > 1 && (p.first_pass - 1) % mcpt::kPassChunk == 0 &&
+                             p.n_passes % mcpt::kPassChunk == 0 && env_int("MCPT_SPLIT_ITEMS", 1) != 0;
     if (order) {
       HIP_OR_RETURN(ensure_item_order(c, items));
       if (c->order_valid && std::equal(key, key + 8, c->order_key)) p.item_perm = c->d_item_perm;
       HIP_OR_RETURN(hipMemsetAsync(c->d_item_cost, 0, sizeof(unsigned) * (size_t)items, c->stream));
       p.item_cost = c->d_item_cost;
+    }
+    if (split_items) {
+      if (!c->d_split_pass) {
+        HIP_OR_RETURN(hipMalloc(&c->d_split_pass, sizeof(float) * 3 * (size_t)kSplitMax * mcpt::kPassChunk *
+                                                      mcpt::kTileThreads));
+      }
+      HIP_OR_RETURN(hipMemsetAsync(c->d_split_of, 0xff, sizeof(int) * (size_t)items, c->stream));
+      p.split_of = c->d_split_of;
+      p.split_pass = c->d_split_pass;
+      p.split_max = kSplitMax;
+      if (p.item_perm) p.split_n = c->d_split_n;
     }
     HIP_OR_RETURN(hipEventRecord(ev_at(c, slot, (int)k, 0), c->stream));
     if (stream) {
@@ -1094,6 +1125,11 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
       size_t tmp = c->sort_tmp_bytes;
       HIP_OR_RETURN(mcpt_order_items(c->d_item_cost, c->d_cost_sorted, c->d_item_iota, c->d_item_perm, (int)items,
                                      c->d_sort_tmp, &tmp, c->stream));
+      // mesh scenes: how many of the costliest to split next time (the mesh kernels run 5
+      // waves per SIMD: 20 per CU, in workgroups of tile_w / 8 waves)
+      if (c->n_meshes > 0)
+        HIP_OR_RETURN(mcpt_split_count(c->d_cost_sorted, (int)items, 20 / (p.tile_w / 8) * c->n_cu, kSplitMax, c->d_split_n,
+                                       c->d_events + kDebugSplitSlot, c->stream));
       std::copy(key, key + 8, c->order_key);
       c->order_valid = true;
       c->order_age = 0;

@@ -36,6 +36,7 @@ constexpr int kNodeF4 = 3;
 // inside each chunk of kPassChunk consecutive absolute pass numbers, chunk sums added to
 // the accumulator in chunk order
 constexpr int kPassChunk = 32;
+constexpr int kSplitPieces = 4;   // pass ranges of a split work item (RenderParams::split_n)
 #ifdef MCPT_BLOCKTIMES
 constexpr size_t kBlockTimeSlots = size_t(8) << 20;   // diagnostic build: per-wave clock pairs
 constexpr size_t kBlockTimeBase = 64;                   // after the debug slots (= MCPT_DEBUG_SLOTS)
@@ -48,8 +49,18 @@ constexpr int kPrimF4 = 8;
 // in a row-band shard (8-row bands) all waves of a workgroup lie in one band of the image (16x16
 // tiles: the slowest 8-GPU shard 2.4-4.1 % slower, profiles/r01_ab33_tile_shape.jsonl)
 constexpr int kTileW = 32, kTileH = 8;
-constexpr int kTileThreads = kTileW * kTileH;
+constexpr int kTileThreads = kTileW * kTileH;   // the widest tile (LDS-scene kernels)
 static_assert(kTileW % 8 == 0 && kTileH % 8 == 0 && kTileThreads <= 1024, "tiles are made of 8x8 waves");
+// Tile width of a render kernel: a workgroup holds its LDS (per-pixel rows, staged scene) until
+// its LAST wave ends, so the waves that end early leave their slots idle when no further
+// workgroup fits the LDS.  The kernels whose LDS allows it run narrower workgroups (round 5,
+// profiles/r05_ab_tile_width.jsonl): the L1/L2 walk kernels two waves (16x8; C4 +0.7 % over
+// 32x8, scene 3 +7 %; one wave: C4 -1.5 %), the mesh kernels one wave (8x8; the mesh workload
+// +6.5 % over 32x8, +1.5 % over 16x8).  The LDS-scene kernel keeps 32x8: 7 workgroups of
+// 22 KB fill the 160 KB.
+__host__ __device__ constexpr int tile_w_for(bool mesh, bool lds_scene) {
+  return mesh ? 8 : (lds_scene ? kTileW : 16);
+}
 
 // Slot of a mesh BVH internal node's child-pair record (64 B) from its mesh's first slot
 // (mcpt_upload_meshes; SceneT::mpairs): node i -> slot i + 1, so the records of two siblings
@@ -75,7 +86,7 @@ struct RenderParams {
   const int* rows;               // global row of each local row (n_local_rows)
   int n_local_rows;
   long long n_local_px;         // n_local_rows × W
-  int n_tiles, n_segments;      // 32x8 tiles of the local rows; pass segments of this launch
+  int n_tiles, n_segments;      // tile_w x 8 tiles of the local rows; pass segments of this launch
   int seg_per_item;             // consecutive segments one work item runs (>= 1)
   int pass_split;               // 1: one segment per pass (n_segments = n_passes; small launches)
   int depth, n_prims;
@@ -107,6 +118,18 @@ struct RenderParams {
   // item i's longest wave time of this launch (100 MHz clock ticks; null: not measured)
   const int* item_perm;
   unsigned* item_cost;
+  // split items (mesh kernels, mcpt_order.hip): the first (*split_n) x kSplitPieces workgroups
+  // run the (*split_n) costliest items of item_perm in kSplitPieces pass ranges each; the rest
+  // run item_perm[split_n ..] whole.  Piece 0 sums its passes from 0 into the segment's slot
+  // and marks split_of[item] = its split index; the later pieces store every pass's value in
+  // split_pass (kPassChunk x kTileThreads x 3 floats per split index), which the combine adds
+  // after piece 0's sum in pass order: the bits of the whole item.  split_n null: no split.
+  const int* split_n;
+  int* split_of;
+  float* split_pass;
+  int n_items;                  // work items of the launch (its grid may hold spare workgroups)
+  int tile_w;                   // the launch's tile width (tile_w_for of its kernel)
+  int split_max;                // most split items (grid = n_items + split_max x (kSplitPieces - 1))
   double cull2_max;
 };
 
@@ -190,6 +213,9 @@ hipError_t mcpt_launch_sample(const mcpt::SampleParams& q, hipStream_t stream);
 hipError_t mcpt_launch_render(const mcpt::RenderParams& p, bool count, hipStream_t stream);
 hipError_t mcpt_launch_combine(const mcpt::RenderParams& p, hipStream_t stream);
 hipError_t mcpt_iota(int* a, int n, hipStream_t stream);
+hipError_t mcpt_split_count(const unsigned* cost_sorted, int n, int capacity, int split_max, int* out,
+                            unsigned long long* dbg, hipStream_t stream);
+constexpr int kDebugSplitSlot = 63;   // debug counter slot: items split by the last sort (mesh scenes)
 hipError_t mcpt_order_items(const unsigned* cost, unsigned* cost_sorted, const int* iota, int* perm, int n,
                             void* tmp, size_t* tmp_bytes, hipStream_t stream);
 // stream schedule: slot set-up (queue[0] = every slot with a unit), then one iteration = the

@@ -64,16 +64,34 @@ constexpr int kMinWavesMesh = 5;
 // scene 3 +5 %: profiles/r02_ab4_spill_free.jsonl; 6 / 8 waves re-measured in round 4: -1.9 / -6.1 %)
 constexpr int kMinWavesL2 = 7;
 template <bool COUNT, bool WAVE, bool MESH, bool LDSS, bool SUSPEND>
-__global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? kMinWavesMesh
+__global__ __launch_bounds__(tile_w_for(MESH, LDSS) * kTileH, MESH && !WAVE ? kMinWavesMesh
                                            : (!WAVE && !LDSS ? kMinWavesL2 : kMinWaves)) void render_kernel(
     RenderParams p) {
+  constexpr int TW = tile_w_for(MESH, LDSS), TT = TW * kTileH;   // this kernel's tile
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   // (XCD-aware remaps of the item order measured slower or within noise: giving each XCD one
   // contiguous 1/8 of the items unbalances the XCDs — C2 -39 %, mesh -10..18 %, C4 -4 % —
   // and chunks of 4 / 32 items per XCD change nothing; profiles/r05_ab_xcd_item_order.jsonl)
-  // the launch's work-item order (mcpt_order.hip): costliest items of an earlier launch first
-  const int item = p.item_perm ? p.item_perm[blockIdx.x] : (int)blockIdx.x;
+  // the launch's work-item order (mcpt_order.hip): costliest items of an earlier launch first;
+  // in the mesh kernels the costliest of them split in kSplitPieces pass ranges (piece >= 0)
+  constexpr bool kSplit = MESH && !WAVE && !COUNT;
+  int item, piece = -1, sj = -1;
+  if constexpr (kSplit) {
+    const int b = blockIdx.x;
+    const int sn = (p.item_perm && p.split_n) ? *p.split_n : 0;
+    if (b < sn * kSplitPieces) {
+      sj = b / kSplitPieces;
+      piece = b - sj * kSplitPieces;
+      item = p.item_perm[sj];
+    } else {
+      const int r = sn + (b - sn * kSplitPieces);
+      if (r >= p.n_items) return;   // a spare workgroup (the grid holds the most pieces)
+      item = p.item_perm ? p.item_perm[r] : r;
+    }
+  } else {
+    item = p.item_perm ? p.item_perm[blockIdx.x] : (int)blockIdx.x;
+  }
   const unsigned long long t_item0 = __builtin_amdgcn_s_memrealtime();
 #ifdef MCPT_BLOCKTIMES
   // diagnostic build only (tools/blocktimes.py; never timed): each wave's start and end on the
@@ -91,9 +109,9 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? kMinWavesMesh
   const int tile = item / n_groups, seg_lo = (item % n_groups) * K;
   const int seg_n = min(K, p.n_segments - seg_lo);
   int seg = seg_lo;
-  const int tiles_x = (p.W + kTileW - 1) / kTileW;
-  const int bx0 = (tile % tiles_x) * kTileW + (wave % (kTileW / 8)) * 8;   // this wave's 8x8 block
-  const int by0 = (tile / tiles_x) * kTileH + (wave / (kTileW / 8)) * 8;
+  const int tiles_x = (p.W + TW - 1) / TW;
+  const int bx0 = (tile % tiles_x) * TW + (wave % (TW / 8)) * 8;   // this wave's 8x8 block
+  const int by0 = (tile / tiles_x) * kTileH + (wave / (TW / 8)) * 8;
   const int x = bx0 + (lane & 7);
   const int lr = by0 + (lane >> 3);
   const bool live = x < p.W && lr < p.n_local_rows;   // (no early return: LDS staging barrier)
@@ -105,6 +123,15 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? kMinWavesMesh
     pass_begin = p.first_pass + seg_lo;
     pass_end = pass_begin + 1;
   }
+  int b1 = 0;   // a split item's first pass of piece 1 (its later pieces store per-pass values)
+  if (kSplit && piece >= 0) {   // (split launches: full 32-pass segments, one per item)
+    const int n = pass_end - pass_begin;
+    b1 = pass_begin + n / kSplitPieces;
+    const int lo = pass_begin + (piece * n) / kSplitPieces, hi = pass_begin + ((piece + 1) * n) / kSplitPieces;
+    pass_begin = lo;
+    pass_end = hi;
+    if (piece == 0 && tid == 0) p.split_of[item] = sj;
+  }
   const int y = live ? p.rows[lr] : 0;   // this shard's local row -> image row (mcpt_set_target*)
 
   SceneT<MESH, LDSS> s{p.nodes, p.leaves, p.ptype, p.prims, p.depth, p.minfo, p.mpairs, p.mleaftris, p.mtris,
@@ -114,9 +141,9 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? kMinWavesMesh
     extern __shared__ float4 s_scene[];
     const int n_nodes = (2 << p.depth) - 1, n_leaves = 1 << p.depth;
     const int n4 = 3 * n_nodes + 8 * p.n_prims;
-    for (int i = tid; i < n4; i += kTileThreads) s_scene[i] = i < 3 * n_nodes ? p.nodes[i] : p.prims[i - 3 * n_nodes];
+    for (int i = tid; i < n4; i += TT) s_scene[i] = i < 3 * n_nodes ? p.nodes[i] : p.prims[i - 3 * n_nodes];
     int* s_int = (int*)(s_scene + n4);
-    for (int i = tid; i < n_leaves + p.n_prims; i += kTileThreads)
+    for (int i = tid; i < n_leaves + p.n_prims; i += TT)
       s_int[i] = i < n_leaves ? p.leaves[i] : p.ptype[i - n_leaves];
     __syncthreads();
     s.nodes = s_scene;
@@ -155,8 +182,8 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? kMinWavesMesh
   // kernels: in the LDS-scene kernel they do not spill, and the in-kernel products are 0.8 %
   // faster on C2 (same file)
   constexpr bool kIorConst = kPixLds;
-  __shared__ float s_pix[kPxLds ? 21 : (kPixLds ? 20 : 18)][kTileThreads];
-  __shared__ int s_hit0[kTileThreads];
+  __shared__ float s_pix[kPxLds ? 21 : (kPixLds ? 20 : 18)][TT];
+  __shared__ int s_hit0[TT];
   const f3 Dcam0 = camera_dir(p, u, v);
   s_pix[0][tid] = Dcam0.x; s_pix[1][tid] = Dcam0.y; s_pix[2][tid] = Dcam0.z;
   if constexpr (kPixLds) {
@@ -211,6 +238,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? kMinWavesMesh
 #endif
   // this segment's sum -> accumulator (one-segment launch) or its segment slot
   auto flush_sum = [&]() {
+    if (kSplit && piece > 0) return;   // a later piece's passes are stored one by one (add_pass)
     // the pixel's address is recomputed at each flush (an empty asm makes the row opaque):
     // hoisted out of the render loop, its 64-bit index and pointer were 4 spilled VGPRs
     size_t px;
@@ -232,6 +260,18 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? kMinWavesMesh
   // after pass++: the segment's last pass closes it (its sum to the segment slot) and the lane
   // goes on with its pixel's next segment of the work item.  With none left, pass stays at
   // pass_end and the lane leaves the loop.
+  // a finished pass's value: into this segment's sum, or (a split item's later pieces) stored
+  // for the combine, which adds it after piece 0's sum in pass order
+  auto add_pass = [&](f3 v) {
+    if (kSplit && piece > 0) {
+      float* q = p.split_pass + (((size_t)sj * kPassChunk + (pass - b1)) * kTileThreads + tid) * 3;
+      q[0] = v.x; q[1] = v.y; q[2] = v.z;
+    } else {
+      s_pix[12][tid] = s_pix[12][tid] + v.x;
+      s_pix[13][tid] = s_pix[13][tid] + v.y;
+      s_pix[14][tid] = s_pix[14][tid] + v.z;
+    }
+  };
   auto next_chunk = [&]() {
     if (pass >= pass_end) {
       flush_sum();
@@ -315,9 +355,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? kMinWavesMesh
       }
     }
     if (fold_end) {
-      s_pix[12][tid] = s_pix[12][tid] + fres.x;
-      s_pix[13][tid] = s_pix[13][tid] + fres.y;
-      s_pix[14][tid] = s_pix[14][tid] + fres.z;
+      add_pass(fres);
       ev.inc(EV_SAMPLE);
       pass++;
       next_chunk();
@@ -448,9 +486,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? kMinWavesMesh
       }
     }
     if (done) {
-      s_pix[12][tid] = s_pix[12][tid] + res.x;
-      s_pix[13][tid] = s_pix[13][tid] + res.y;
-      s_pix[14][tid] = s_pix[14][tid] + res.z;
+      add_pass(res);
       ev.inc(EV_SAMPLE);
       pass++;
       next_chunk();
@@ -497,7 +533,8 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? kMinWavesMesh
 
   if (p.item_cost && (int)__lane_id() == __builtin_ffsll((long long)__ballot(1)) - 1) {
     // this item's cost for the next launch's order: its longest wave (100 MHz ticks)
-    const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t_item0;
+    unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t_item0;
+    if (kSplit && piece >= 0) dt *= kSplitPieces;   // a piece stands for its whole item
     atomicMax(p.item_cost + item, dt < 0xffffffffull ? (unsigned)dt : 0xffffffffu);
   }
 #ifdef MCPT_BLOCKTIMES
@@ -505,7 +542,7 @@ __global__ __launch_bounds__(kTileThreads, MESH && !WAVE ? kMinWavesMesh
     const unsigned long long bt1 = __builtin_amdgcn_s_memrealtime();
     const int lead = __builtin_ffsll((long long)__ballot(1)) - 1, k = (int)__lane_id() - lead;
     if ((k == 0 || k == 1) && p.events)   // two lanes, one value each (vector stores)
-      p.events[kBlockTimeBase + 2ull * ((unsigned long long)item * (kTileThreads / 64) + wave) + k] = k ? bt1 : bt0;
+      p.events[kBlockTimeBase + 2ull * ((unsigned long long)item * (TT / 64) + wave) + k] = k ? bt1 : bt0;
   }
 #endif
 #ifdef MCPT_LANESTATS
@@ -553,6 +590,36 @@ __global__ __launch_bounds__(256) void combine_kernel(float* __restrict__ accum,
   for (int s = 0; s < n_seg; ++s) {
     const float* q = partial + ((size_t)s * n_px + i) * 3;
     a0 = a0 + q[0]; a1 = a1 + q[1]; a2 = a2 + q[2];
+  }
+  accum[i * 3] = a0; accum[i * 3 + 1] = a1; accum[i * 3 + 2] = a2;
+}
+
+// combine_kernel for launches with split items (mesh kernels; one segment per item, full
+// 32-pass segments): a split segment's sum is piece 0's sum, then the later pieces' stored
+// pass values added in pass order (the sequence one lane would have summed)
+__global__ __launch_bounds__(256) void combine_items_kernel(float* __restrict__ accum, const float* __restrict__ partial,
+                                                            long long n_px, int n_seg, int W, int TW,
+                                                            const int* __restrict__ split_of,
+                                                            const float* __restrict__ split_pass) {
+  long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n_px) return;
+  const int lr = (int)(i / W), x = (int)(i - (long long)lr * W);
+  const int tiles_x = (W + TW - 1) / TW;
+  const int tile = (lr / kTileH) * tiles_x + x / TW;
+  const int t = (((lr % kTileH) / 8) * (TW / 8) + (x % TW) / 8) * 64 + (lr % 8) * 8 + (x % 8);   // its thread
+  constexpr int p1 = kPassChunk / kSplitPieces;   // piece 1's first pass within the segment
+  float a0 = accum[i * 3], a1 = accum[i * 3 + 1], a2 = accum[i * 3 + 2];
+  for (int s = 0; s < n_seg; ++s) {
+    const float* q = partial + ((size_t)s * n_px + i) * 3;
+    float s0 = q[0], s1 = q[1], s2 = q[2];
+    const int j = split_of[(size_t)tile * n_seg + s];
+    if (j >= 0) {
+      for (int k = 0; k < kPassChunk - p1; ++k) {
+        const float* v = split_pass + (((size_t)j * kPassChunk + k) * kTileThreads + t) * 3;
+        s0 = s0 + v[0]; s1 = s1 + v[1]; s2 = s2 + v[2];
+      }
+    }
+    a0 = a0 + s0; a1 = a1 + s1; a2 = a2 + s2;
   }
   accum[i * 3] = a0; accum[i * 3 + 1] = a1; accum[i * 3 + 2] = a2;
 }
@@ -646,9 +713,12 @@ hipError_t mcpt_launch_render(const mcpt::RenderParams& p, bool count, hipStream
   const int K = p.seg_per_item > 1 ? p.seg_per_item : 1;
   const long long items = (long long)p.n_tiles * ((p.n_segments + K - 1) / K);
   if (items <= 0) return hipSuccess;
-  dim3 block(mcpt::kTileThreads), grid((unsigned)items);
+  // split items: spare workgroups for the most pieces (the kernel skips the unused ones)
+  const long long blocks = items + (p.split_of ? (long long)p.split_max * (mcpt::kSplitPieces - 1) : 0);
+  dim3 block(p.tile_w * mcpt::kTileH), grid((unsigned)blocks);
   const bool wave = p.wave_traversal != 0, mesh = p.n_meshes > 0;
   const bool lds = p.lds_scene_bytes > 0;
+  if (p.tile_w != mcpt::tile_w_for(mesh, lds)) return hipErrorInvalidValue;   // (launch() sets it)
   // deep-BVH walk kernel: suspendable walks and/or batched leaf visits (walk_run)
   const bool susp = !count && !wave && (p.walk_exit > 0 || p.leaf_batch > 0);
   const size_t shm = lds ? (size_t)p.lds_scene_bytes : 0;
@@ -679,6 +749,9 @@ hipError_t mcpt_launch_combine(const mcpt::RenderParams& p, hipStream_t stream) 
   if (p.pass_split)
     hipLaunchKernelGGL(mcpt::combine_split_kernel, grid, block, 0, stream, p.accum, p.partial, p.n_local_px,
                        p.first_pass, p.n_passes);
+  else if (p.split_of)
+    hipLaunchKernelGGL(mcpt::combine_items_kernel, grid, block, 0, stream, p.accum, p.partial, p.n_local_px,
+                       p.n_segments, p.W, p.tile_w, p.split_of, p.split_pass);
   else
     hipLaunchKernelGGL(mcpt::combine_kernel, grid, block, 0, stream, p.accum, p.partial, p.n_local_px, p.n_segments);
   return hipGetLastError();

@@ -16,7 +16,40 @@ __global__ void iota_kernel(int* a, int n) {
   if (i < n) a[i] = i;
 }
 
+// How many of the costliest items to split (mesh launches): those costing more than half the
+// launch's ideal span, sum(costs) / capacity (the concurrent workgroups), at most split_max.
+// A launch cannot end before its longest item does; split in kSplitPieces pass ranges, a costly
+// item's pieces run side by side instead of one after another.
+__global__ __launch_bounds__(1024) void split_count_kernel(const unsigned* cost_sorted, int n, int capacity,
+                                                           int split_max, int* out, unsigned long long* dbg) {
+  __shared__ double s_sum[1024];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < n; i += 1024) acc += (double)cost_sorted[i];
+  s_sum[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 512; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) s_sum[threadIdx.x] += s_sum[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  const double lim = 0.5 * s_sum[0] / (double)(capacity > 0 ? capacity : 1);
+  int lo = 0, hi = n < split_max ? n : split_max;   // first index whose cost <= lim
+  while (lo < hi) {
+    const int mid = (lo + hi) / 2;
+    if ((double)cost_sorted[mid] > lim) lo = mid + 1; else hi = mid;
+  }
+  *out = lo;
+  if (dbg) *dbg = (unsigned long long)lo;   // debug slot kDebugSplitSlot (mcpt_debug_counters)
+}
+
 }  // namespace mcpt
+
+hipError_t mcpt_split_count(const unsigned* cost_sorted, int n, int capacity, int split_max, int* out,
+                            unsigned long long* dbg, hipStream_t stream) {
+  hipLaunchKernelGGL(mcpt::split_count_kernel, dim3(1), dim3(1024), 0, stream, cost_sorted, n, capacity, split_max, out,
+                     dbg);
+  return hipGetLastError();
+}
 
 hipError_t mcpt_iota(int* a, int n, hipStream_t stream) {
   if (n <= 0) return hipSuccess;

@@ -133,3 +133,23 @@ def test_mesh_1m_rows(mcpt_mod, oracle_mod, renderer, big_mesh, traversal):
                                    row_step=H, row_offset=int(y), meshes=mv)
         assert np.array_equal(bits(img[y]), bits(ref[int(y)])), f"1 M-triangle mesh scene row {y}"
     assert np.isfinite(img).all()
+
+
+def test_mesh_split_items_same_bits(mcpt_mod, renderer, big_mesh, monkeypatch):
+    """Work-item order + split items on the 1 M-triangle mesh workload (mcpt_order.hip): after
+    the first launch the costliest items run first and the costliest of those in 4 pass
+    ranges (the later pieces' per-pass values added by the combine after piece 0's sum).  Three
+    64-pass calls equal the same passes in launch order without splits, bit for bit; debug slot
+    63 shows that items were split."""
+    W, H, B = 1920, 1080, 8
+    renderer.set_traversal(1)
+    try:
+        monkeypatch.setenv("MCPT_ITEM_ORDER", "1")
+        a = render(mcpt_mod, renderer, big_mesh, W, H, 1, 192, B, split=[64, 64, 64])
+        n_split = int(renderer.debug_counters()[63])
+        monkeypatch.setenv("MCPT_ITEM_ORDER", "0")
+        b = render(mcpt_mod, renderer, big_mesh, W, H, 1, 192, B, split=[64, 64, 64])
+    finally:
+        renderer.set_traversal(0)
+    assert n_split > 0
+    assert np.array_equal(bits(a), bits(b))
