@@ -979,7 +979,7 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   p.mverts = c->d_mverts; p.mnorms = c->d_mnorms; p.n_meshes = c->n_meshes; p.flat_face = c->flat_face;
   HIP_OR_RETURN(collect_tuning(c));
   // (the counting build is not timed: AUTO counts with the per-lane walk)
-  p.tile_w = mcpt::tile_w_for(c->n_meshes > 0, p.lds_scene_bytes > 0);
+  p.tile_w = mcpt::tile_w_for(c->n_meshes > 0, p.lds_scene_bytes);
   p.n_tiles = ((c->W + p.tile_w - 1) / p.tile_w) * ((c->n_local_rows + mcpt::kTileH - 1) / mcpt::kTileH);
   auto fdiv = [](int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); };
   const long long total_seg = n_passes > 0 ? fdiv(first_pass + n_passes - 2, mcpt::kPassChunk) -

@@ -51,17 +51,18 @@ constexpr int kPrimF4 = 8;
 constexpr int kTileW = 32, kTileH = 8;
 constexpr int kTileThreads = kTileW * kTileH;   // the widest tile (LDS-scene kernels)
 static_assert(kTileW % 8 == 0 && kTileH % 8 == 0 && kTileThreads <= 1024, "tiles are made of 8x8 waves");
-// Tile width of a render kernel: a workgroup holds its LDS (per-pixel rows, staged scene) until
+// Tile width of a render launch: a workgroup holds its LDS (per-pixel rows, staged scene) until
 // its LAST wave ends, so the waves that end early leave their slots idle when no further
-// workgroup fits the LDS.  The kernels whose LDS allows it run narrower workgroups (round 5,
+// workgroup fits the LDS.  Launches whose LDS allows it run narrower workgroups (round 5,
 // profiles/r05_ab_tile_width.jsonl): the L1/L2 walk kernels two waves (16x8; C4 +0.7 % over
 // 32x8, scene 3 +7 %; one wave: C4 -1.5 %), the mesh kernels one wave (8x8; the mesh workload
-// +6.5 % over 32x8, +1.5 % over 16x8).  The LDS-scene kernel keeps 32x8: 7 workgroups of
-// 22 KB fill the 160 KB.
-__host__ __device__ constexpr int tile_w_for(bool mesh, bool lds_scene) {
-  return mesh ? 8 : (lds_scene ? kTileW : 16);
+// +7 % over 32x8, +1.7 % over 16x8).  The LDS-scene kernel (7 waves/SIMD = 14 two-wave
+// workgroups per CU, 9.5 KB of per-pixel rows each) runs 16x8 when the staged scene fits the
+// rest of the 160 KB (kLdsScene16: scene 6, i.e. C2 / C3 / C5: +0.3..0.9 %), else 32x8.
+constexpr int kLdsScene16 = (163840 / 14 - 16 * kTileH * 76) / 16 * 16;
+__host__ __device__ constexpr int tile_w_for(bool mesh, int lds_scene_bytes) {
+  return mesh ? 8 : (lds_scene_bytes > 0 ? (lds_scene_bytes <= kLdsScene16 ? 16 : kTileW) : 16);
 }
-
 // Slot of a mesh BVH internal node's child-pair record (64 B) from its mesh's first slot
 // (mcpt_upload_meshes; SceneT::mpairs): node i -> slot i + 1, so the records of two siblings
 // (2i+1, 2i+2: the left child's pending pop follows the right child's subtree) share one
@@ -128,7 +129,7 @@ struct RenderParams {
   int* split_of;
   float* split_pass;
   int n_items;                  // work items of the launch (its grid may hold spare workgroups)
-  int tile_w;                   // the launch's tile width (tile_w_for of its kernel)
+  int tile_w;                   // the launch's tile width (tile_w_for)
   int split_max;                // most split items (grid = n_items + split_max x (kSplitPieces - 1))
   double cull2_max;
 };

@@ -63,11 +63,11 @@ constexpr int kMinWavesMesh = 5;
 // record they fit 72 VGPRs and 7 waves hide more of the dependent node loads (scene 8 +4 %,
 // scene 3 +5 %: profiles/r02_ab4_spill_free.jsonl; 6 / 8 waves re-measured in round 4: -1.9 / -6.1 %)
 constexpr int kMinWavesL2 = 7;
-template <bool COUNT, bool WAVE, bool MESH, bool LDSS, bool SUSPEND>
-__global__ __launch_bounds__(tile_w_for(MESH, LDSS) * kTileH, MESH && !WAVE ? kMinWavesMesh
+template <bool COUNT, bool WAVE, bool MESH, bool LDSS, bool SUSPEND, int TW>
+__global__ __launch_bounds__(TW * kTileH, MESH && !WAVE ? kMinWavesMesh
                                            : (!WAVE && !LDSS ? kMinWavesL2 : kMinWaves)) void render_kernel(
     RenderParams p) {
-  constexpr int TW = tile_w_for(MESH, LDSS), TT = TW * kTileH;   // this kernel's tile
+  constexpr int TT = TW * kTileH;   // this kernel's tile (tile_w_for)
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   // (XCD-aware remaps of the item order measured slower or within noise: giving each XCD one
@@ -718,17 +718,18 @@ hipError_t mcpt_launch_render(const mcpt::RenderParams& p, bool count, hipStream
   dim3 block(p.tile_w * mcpt::kTileH), grid((unsigned)blocks);
   const bool wave = p.wave_traversal != 0, mesh = p.n_meshes > 0;
   const bool lds = p.lds_scene_bytes > 0;
-  if (p.tile_w != mcpt::tile_w_for(mesh, lds)) return hipErrorInvalidValue;   // (launch() sets it)
+  if (p.tile_w != mcpt::tile_w_for(mesh, p.lds_scene_bytes)) return hipErrorInvalidValue;   // (launch() sets it)
   // deep-BVH walk kernel: suspendable walks and/or batched leaf visits (walk_run)
   const bool susp = !count && !wave && (p.walk_exit > 0 || p.leaf_batch > 0);
   const size_t shm = lds ? (size_t)p.lds_scene_bytes : 0;
-#define MCPT_RENDER(C, W, M, L, S) \
-  hipLaunchKernelGGL((mcpt::render_kernel<C, W, M, L, S>), grid, block, shm, stream, p)
-#define MCPT_RENDER_CW(C, W, S)                              \
-  if (mesh && lds) MCPT_RENDER(C, W, true, true, S);         \
-  else if (mesh) MCPT_RENDER(C, W, true, false, S);          \
-  else if (lds) MCPT_RENDER(C, W, false, true, S);           \
-  else MCPT_RENDER(C, W, false, false, S)
+#define MCPT_RENDER(C, W, M, L, S, T) \
+  hipLaunchKernelGGL((mcpt::render_kernel<C, W, M, L, S, T>), grid, block, shm, stream, p)
+#define MCPT_RENDER_CW(C, W, S)                                          \
+  if (mesh && lds) MCPT_RENDER(C, W, true, true, S, 8);                  \
+  else if (mesh) MCPT_RENDER(C, W, true, false, S, 8);                   \
+  else if (lds && p.tile_w == 16) MCPT_RENDER(C, W, false, true, S, 16); \
+  else if (lds) MCPT_RENDER(C, W, false, true, S, 32);                   \
+  else MCPT_RENDER(C, W, false, false, S, 16)
   if (count) {
     if (wave) { MCPT_RENDER_CW(true, true, false); } else { MCPT_RENDER_CW(true, false, false); }
   } else if (wave) {
