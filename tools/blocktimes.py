@@ -81,7 +81,7 @@ def main():
         L.mcpt_debug_blocktimes(r._h, buf, n)
         t = np.frombuffer(buf, dtype=np.uint64)
         res = {"workload": name, "scene": sid, "spp": S, "bounces": B, "seg_per_item_env": seg or None}
-        res.update(analyse(t))
+        res.update(analyse(t, waves_per_item=1 if sid == 0 else 2))   # waves per workgroup (tile_w_for)
         print(json.dumps(res), flush=True)
         r.close()
 
