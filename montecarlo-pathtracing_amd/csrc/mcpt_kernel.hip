@@ -9,7 +9,7 @@
 //    a lane whose path terminates immediately regenerates the next pass's path
 //    (persistent-lane regeneration), so a wave runs until its lanes' *sums* of path
 //    lengths are exhausted, not the max path per pass — the 4 material branches and
-//    the 0..B bounce lengths average out.  Work items = (32x8 tile, pass segment), so
+//    the 0..B bounce lengths average out.  Work items = (pixel tile, pass segment), so
 //    a shard has enough items to fill the chip even at 8-way row-band sharding;
 //  * the bounce loop and the mixed/refraction branch's inner traversal are folded into
 //    ONE traversal site per loop iteration (a 2-phase state machine), so lanes doing an
@@ -41,7 +41,8 @@ namespace mcpt {
 // ------------------------------------------------------------------------------------
 // the kernel
 // ------------------------------------------------------------------------------------
-// Work item = (32x8 pixel tile of four 8x8 waves, group of seg_per_item pass segments).  A
+// Work item = (TW x 8 pixel tile of TW/8 8x8 waves, group of seg_per_item pass segments; TW per
+// launch, tile_w_for).  A
 // segment is the part of the launch's pass range inside one accumulation chunk of kPassChunk
 // absolute passes: segments of one pixel are independent (strong-scaling
 // parallelism beyond one lane per pixel); their sums are combined in chunk order by
@@ -168,7 +169,7 @@ __global__ __launch_bounds__(TW * kTileH, MESH && !WAVE ? kMinWavesMesh
   // out of the register file is what lets 7 waves/SIMD fit.  rows: 0-2 Dcam, 3-5 N0, 6-8 P0
   // (primary hit), 9-11 N / 15-17 P saved across the inner traversal, 12-14 this segment's
   // sum (from 0 in pass order); s_hit0 = primary hit shape << 28 | index (-1: miss).
-  // 19 KB per workgroup, + the staged scene (LDSS, <= kLdsSceneBytes): 7 workgroups/CU.
+  // 76 B per thread (19 KB per 32x8 workgroup), + the staged scene (LDSS, <= kLdsSceneBytes).
   // Kernels without a staged scene also keep the pixel's (u, v) there (rows 18-19), the mesh
   // kernels its local index too (row 20): held in VGPRs across the render loop they were
   // spilled registers, written to scratch once per lane and work item (C4: 1.16 -> 0.50 GB of
