@@ -1088,13 +1088,25 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
     p.item_cost = nullptr;
     p.split_n = nullptr; p.split_of = nullptr; p.split_pass = nullptr; p.split_max = 0;
     p.n_items = (int)items;
+    p.tail_m = 0;
     // split items: mesh launches of whole 32-pass segments, one per item (MCPT_SPLIT_ITEMS=0: off)
     const bool split_items = order && c->n_meshes > 0 && !p.wave_traversal && kseg == 1 && !p.pass_split &&
                              p.n_segments > 1 && (p.first_pass - 1) % mcpt::kPassChunk == 0 &&
                              p.n_passes % mcpt::kPassChunk == 0 && env_int("MCPT_SPLIT_ITEMS", 1) != 0;
     if (order) {
       HIP_OR_RETURN(ensure_item_order(c, items));
-      if (c->order_valid && std::equal(key, key + 8, c->order_key)) p.item_perm = c->d_item_perm;
+      if (c->order_valid && std::equal(key, key + 8, c->order_key)) {
+        p.item_perm = c->d_item_perm;
+        // items of several segments: the cheapest (last) one workgroup-generation of the order
+        // runs one segment per workgroup, so the launch does not end on whole long items
+        if (kseg > 1 && !p.pass_split && env_int("MCPT_TAIL_PIECES", 1) != 0) {
+          const int waves_simd = c->n_meshes > 0 ? 5 : 7;
+          const long long per_cu = 4LL * waves_simd / (p.tile_w / 8);
+          // (one generation: C4 +2.0 %, C2 +0.3 %; 0.5 / 2 / 3 generations no better on C4:
+          // profiles/r05_ab_tail_pieces.jsonl)
+          p.tail_m = (int)std::min(items / 2, per_cu * c->n_cu);
+        }
+      }
       HIP_OR_RETURN(hipMemsetAsync(c->d_item_cost, 0, sizeof(unsigned) * (size_t)items, c->stream));
       p.item_cost = c->d_item_cost;
     }

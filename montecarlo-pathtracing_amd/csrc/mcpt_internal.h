@@ -129,6 +129,7 @@ struct RenderParams {
   int* split_of;
   float* split_pass;
   int n_items;                  // work items of the launch (its grid may hold spare workgroups)
+  int tail_m;                   // seg_per_item > 1: the last tail_m items of item_perm run one segment per workgroup
   int tile_w;                   // the launch's tile width (tile_w_for)
   int split_max;                // most split items (grid = n_items + split_max x (kSplitPieces - 1))
   double cull2_max;

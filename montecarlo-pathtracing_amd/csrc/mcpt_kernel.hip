@@ -93,6 +93,17 @@ __global__ __launch_bounds__(TW * kTileH, MESH && !WAVE ? kMinWavesMesh
   } else {
     item = p.item_perm ? p.item_perm[blockIdx.x] : (int)blockIdx.x;
   }
+  // tail pieces (launches of several segments per item, mcpt_order.hip): the last tail_m items of
+  // the order — the cheapest — run one segment per workgroup, so the launch ends on short pieces
+  int seg_only = -1;
+  if (!kSplit && p.tail_m > 0) {
+    const int head = p.n_items - p.tail_m, b = blockIdx.x;
+    if (b >= head) {
+      const int q = b - head, j = q / p.seg_per_item;
+      item = p.item_perm[head + j];
+      seg_only = q - j * p.seg_per_item;
+    }
+  }
   const unsigned long long t_item0 = __builtin_amdgcn_s_memrealtime();
 #ifdef MCPT_BLOCKTIMES
   // diagnostic build only (tools/blocktimes.py; never timed): each wave's start and end on the
@@ -107,8 +118,14 @@ __global__ __launch_bounds__(TW * kTileH, MESH && !WAVE ? kMinWavesMesh
   // segments one after another (each summed from 0 in pass order, written when it ends).
   const int K = p.seg_per_item > 1 ? p.seg_per_item : 1;
   const int n_groups = (p.n_segments + K - 1) / K;
-  const int tile = item / n_groups, seg_lo = (item % n_groups) * K;
-  const int seg_n = min(K, p.n_segments - seg_lo);
+  const int tile = item / n_groups;
+  int seg_lo = (item % n_groups) * K;
+  int seg_n = min(K, p.n_segments - seg_lo);
+  if (seg_only >= 0) {   // a tail piece: one segment of its item
+    if (seg_only >= seg_n) return;   // (the item has fewer segments: an empty piece)
+    seg_lo += seg_only;
+    seg_n = 1;
+  }
   int seg = seg_lo;
   const int tiles_x = (p.W + TW - 1) / TW;
   const int bx0 = (tile % tiles_x) * TW + (wave % (TW / 8)) * 8;   // this wave's 8x8 block
@@ -536,6 +553,7 @@ __global__ __launch_bounds__(TW * kTileH, MESH && !WAVE ? kMinWavesMesh
     // this item's cost for the next launch's order: its longest wave (100 MHz ticks)
     unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t_item0;
     if (kSplit && piece >= 0) dt *= kSplitPieces;   // a piece stands for its whole item
+    if (seg_only >= 0) dt *= (unsigned)p.seg_per_item;
     atomicMax(p.item_cost + item, dt < 0xffffffffull ? (unsigned)dt : 0xffffffffu);
   }
 #ifdef MCPT_BLOCKTIMES
@@ -715,7 +733,8 @@ hipError_t mcpt_launch_render(const mcpt::RenderParams& p, bool count, hipStream
   const long long items = (long long)p.n_tiles * ((p.n_segments + K - 1) / K);
   if (items <= 0) return hipSuccess;
   // split items: spare workgroups for the most pieces (the kernel skips the unused ones)
-  const long long blocks = items + (p.split_of ? (long long)p.split_max * (mcpt::kSplitPieces - 1) : 0);
+  const long long blocks = items + (p.split_of ? (long long)p.split_max * (mcpt::kSplitPieces - 1) : 0) +
+                           (long long)p.tail_m * (K - 1);
   dim3 block(p.tile_w * mcpt::kTileH), grid((unsigned)blocks);
   const bool wave = p.wave_traversal != 0, mesh = p.n_meshes > 0;
   const bool lds = p.lds_scene_bytes > 0;

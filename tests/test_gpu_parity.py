@@ -563,3 +563,19 @@ def test_item_order_same_bits(mcpt_mod, renderer, monkeypatch, scene_id, travers
     monkeypatch.setenv("MCPT_ITEM_ORDER", "0")
     plain = _gpu(mcpt_mod, renderer, scene_id, W, H, 1, 128, B, split=chunks, traversal=traversal)
     assert np.array_equal(ordered.view(np.uint32), plain.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene_id,traversal", [(6, 1), (8, 1)])
+def test_tail_pieces_same_bits(mcpt_mod, renderer, monkeypatch, scene_id, traversal):
+    """Items of several pass segments (MCPT_SEG_PER_ITEM=4): once ordered, the cheapest
+    generation of items at the end of the order runs one segment per workgroup (tail pieces).
+    Each segment still sums its passes from 0 into its own slot, so three 128-pass calls equal
+    the same calls with the order off, bit for bit."""
+    W, H, B = 1920, 1080, 4
+    monkeypatch.setenv("MCPT_SEG_PER_ITEM", "4")
+    monkeypatch.setenv("MCPT_ITEM_ORDER", "1")
+    ordered = _gpu(mcpt_mod, renderer, scene_id, W, H, 1, 384, B, split=[128, 128, 128], traversal=traversal)
+    monkeypatch.setenv("MCPT_ITEM_ORDER", "0")
+    plain = _gpu(mcpt_mod, renderer, scene_id, W, H, 1, 384, B, split=[128, 128, 128], traversal=traversal)
+    assert np.array_equal(ordered.view(np.uint32), plain.view(np.uint32))

@@ -7,7 +7,7 @@ from the moment the running-wave count falls below 90 % of its peak for good to 
 each XCD group's (blockIdx % 8) last end.
 
     MCPT_LIB=montecarlo-pathtracing_amd/mcpt/variants/libmcpt_blocktimes.so \\
-        python tools/blocktimes.py [c2] [c4] [mesh] [--seg K]
+        python tools/blocktimes.py [c2] [c4] [mesh] [--seg K] [--auto]
 """
 import ctypes
 import json
@@ -70,17 +70,22 @@ def main():
         else:
             r.upload_scene(mcpt.Scene.reference(sid))
         r.set_target(W, H)
-        r.set_traversal(mcpt.TRAVERSAL_LANE)
+        auto = "--auto" in sys.argv
+        r.set_traversal(mcpt.TRAVERSAL_AUTO if auto else mcpt.TRAVERSAL_LANE)
         if seg:
             os.environ["MCPT_SEG_PER_ITEM"] = str(seg)
-        r.render(ipv, iv, 1, S, 0.0, B, 1.0, 0)   # warm-up (and first-touch of the scene)
+        # warm-up (first touch of the scene; with --auto, AUTO's timing trials until it settles)
+        for k in range(12 if auto else 1):   # (LANE: one warm-up; the timed launch is the 13th pass range either way)
+            r.render(ipv, iv, 1 + k * S, S, 0.0, B, 1.0, 0)
         n = 8 << 20
         buf = (ctypes.c_ulonglong * n)()
         L.mcpt_debug_blocktimes(r._h, buf, n)   # (zeroes the slots)
-        r.render(ipv, iv, 1 + S, S, 0.0, B, 1.0, 0)
+        r.render(ipv, iv, 1 + 12 * S, S, 0.0, B, 1.0, 0)
         L.mcpt_debug_blocktimes(r._h, buf, n)
+        sched = r.schedule()
         t = np.frombuffer(buf, dtype=np.uint64)
-        res = {"workload": name, "scene": sid, "spp": S, "bounces": B, "seg_per_item_env": seg or None}
+        res = {"workload": name, "scene": sid, "spp": S, "bounces": B, "seg_per_item_env": seg or None,
+               "traversal": "AUTO" if auto else "LANE", "schedule": sched}
         res.update(analyse(t, waves_per_item=1 if sid == 0 else 2))   # waves per workgroup (tile_w_for)
         print(json.dumps(res), flush=True)
         r.close()
