@@ -1195,7 +1195,7 @@ int mcpt_debug_counters(mcpt_ctx* c, unsigned long long* out, int n_slots, int r
 
 #ifdef MCPT_BLOCKTIMES
 // diagnostic build only: the per-wave (start, end) clock pairs of the last render launch
-// (wave w of work item i at 2 (4 i + w)), zeroed after the copy
+// (wave w of workgroup b at 2 (b * waves per workgroup + w)), zeroed after the copy
 extern "C" int mcpt_debug_blocktimes(mcpt_ctx* c, unsigned long long* out, long long n) {
   if (!c || !out || n < 0 || (size_t)n > mcpt::kBlockTimeSlots) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   HIP_OR_RETURN(hipSetDevice(c->device));

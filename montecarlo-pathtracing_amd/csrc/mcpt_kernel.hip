@@ -561,7 +561,7 @@ __global__ __launch_bounds__(TW * kTileH, MESH && !WAVE ? kMinWavesMesh
     const unsigned long long bt1 = __builtin_amdgcn_s_memrealtime();
     const int lead = __builtin_ffsll((long long)__ballot(1)) - 1, k = (int)__lane_id() - lead;
     if ((k == 0 || k == 1) && p.events)   // two lanes, one value each (vector stores)
-      p.events[kBlockTimeBase + 2ull * ((unsigned long long)item * (TT / 64) + wave) + k] = k ? bt1 : bt0;
+      p.events[kBlockTimeBase + 2ull * ((unsigned long long)blockIdx.x * (TT / 64) + wave) + k] = k ? bt1 : bt0;
   }
 #endif
 #ifdef MCPT_LANESTATS

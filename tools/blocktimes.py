@@ -44,7 +44,11 @@ def analyse(t: np.ndarray, waves_per_item: int = 4) -> dict:
     items = idx // waves_per_item
     xcd = items % 8
     xcd_end = [round(float(en[xcd == k].max()), 3) for k in range(8) if (xcd == k).any()]
+    # running waves (fraction of the peak) at 20 evenly spaced instants of the launch
+    grid = np.linspace(0.0, span, 21)[:-1] + span / 40
+    prof = [round(float(((st <= g) & (en > g)).sum()) / peak, 3) for g in grid]
     return {"waves": int(live.sum()), "span_ms": round(float(span), 3), "peak_waves": int(peak),
+            "occupancy_profile": prof,
             "fill": round(float(life.sum() / (peak * span)), 4),
             "tail_ms": round(float(span - t_drop), 3), "tail_frac": round(float((span - t_drop) / span), 4),
             "wave_life_ms": {"mean": round(float(life.mean()), 3), "p50": round(float(np.median(life)), 3),
@@ -86,7 +90,7 @@ def main():
         t = np.frombuffer(buf, dtype=np.uint64)
         res = {"workload": name, "scene": sid, "spp": S, "bounces": B, "seg_per_item_env": seg or None,
                "traversal": "AUTO" if auto else "LANE", "schedule": sched}
-        res.update(analyse(t, waves_per_item=1 if sid == 0 else 2))   # waves per workgroup (tile_w_for)
+        res.update(analyse(t, waves_per_item=1 if sid == 0 else 2))   # waves per workgroup (tile_w_for; records by workgroup)
         print(json.dumps(res), flush=True)
         r.close()
 
