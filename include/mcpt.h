@@ -138,10 +138,12 @@ int mcpt_local_row_ids(mcpt_ctx* ctx, int* rows_out);
  * refract_ind(24); variant = tp/ shader.  Asynchronous on the context's stream.
  * Scheduling (never the bits): a launch of >= 4,096 work items times its items
  * and the next launch of the same shape runs them costliest first (a device sort on the
- * context's stream: no host wait; env MCPT_ITEM_ORDER=0 turns it off); in mesh scenes, launches
- * of whole 32-pass chunks also run their costliest items in 4 pass ranges side by side (env
- * MCPT_SPLIT_ITEMS=0 turns that off).  Device memory for it: 16 B per work item, and 100 MB of
- * per-pass values once a mesh launch splits items. */
+ * context's stream: no host wait; env MCPT_ITEM_ORDER=0 turns it off); launches whose work items
+ * hold several pass segments run the last workgroup-generation of that order one segment per
+ * workgroup (env MCPT_TAIL_PIECES=0 turns that off); in mesh scenes, launches of whole 32-pass
+ * chunks also run their costliest items in 4 pass ranges side by side (env MCPT_SPLIT_ITEMS=0
+ * turns that off).  Device memory for it: 20 B per work item, and 100 MB of per-pass values
+ * once a mesh launch splits items. */
 int mcpt_render(mcpt_ctx* ctx, const float* invPV, const float* invV, int first_pass,
                 int n_passes, float date, int bounces, float refract_ind, int variant);
 
