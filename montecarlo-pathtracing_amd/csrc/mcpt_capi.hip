@@ -1099,7 +1099,7 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
         p.item_perm = c->d_item_perm;
         // items of several segments: the cheapest (last) one workgroup-generation of the order
         // runs one segment per workgroup, so the launch does not end on whole long items
-        if (kseg > 1 && !p.pass_split && env_int("MCPT_TAIL_PIECES", 1) != 0) {
+        if (kseg > 1 && !p.pass_split && c->n_meshes == 0 && env_int("MCPT_TAIL_PIECES", 1) != 0) {   // (the mesh kernels split items their own way)
           const int waves_simd = c->n_meshes > 0 ? 5 : 7;
           const long long per_cu = 4LL * waves_simd / (p.tile_w / 8);
           // (one generation: C4 +2.0 %, C2 +0.3 %; 0.5 / 2 / 3 generations no better on C4:

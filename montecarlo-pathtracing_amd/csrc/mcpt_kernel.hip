@@ -90,18 +90,20 @@ __global__ __launch_bounds__(TW * kTileH, MESH && !WAVE ? kMinWavesMesh
       if (r >= p.n_items) return;   // a spare workgroup (the grid holds the most pieces)
       item = p.item_perm ? p.item_perm[r] : r;
     }
-  } else {
-    item = p.item_perm ? p.item_perm[blockIdx.x] : (int)blockIdx.x;
   }
   // tail pieces (launches of several segments per item, mcpt_order.hip): the last tail_m items of
-  // the order — the cheapest — run one segment per workgroup, so the launch ends on short pieces
+  // the order — the cheapest — run one segment per workgroup, so the launch ends on short pieces.
+  // (The grid holds n_items + tail_m (K - 1) workgroups: item_perm is read at b < n_items only.)
   int seg_only = -1;
-  if (!kSplit && p.tail_m > 0) {
-    const int head = p.n_items - p.tail_m, b = blockIdx.x;
-    if (b >= head) {
+  if constexpr (!kSplit) {
+    const int b = blockIdx.x;
+    const int head = p.tail_m > 0 ? p.n_items - p.tail_m : p.n_items;
+    if (b >= head && p.tail_m > 0) {
       const int q = b - head, j = q / p.seg_per_item;
       item = p.item_perm[head + j];
       seg_only = q - j * p.seg_per_item;
+    } else {
+      item = p.item_perm ? p.item_perm[b] : b;
     }
   }
   const unsigned long long t_item0 = __builtin_amdgcn_s_memrealtime();
