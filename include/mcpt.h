@@ -73,6 +73,14 @@ typedef struct mcpt_scene mcpt_scene;
 
 const char* mcpt_error_string(int status);
 int mcpt_version(void);
+/* Which diagnostic build this library is (never a timed build): bit MCPT_BUILD_CHECKED the
+ * bounds-checked build (make checked: out-of-range work-item / split / segment indices are counted
+ * and skipped, every sub-launch is waited for and a fault or count fails the render call with the
+ * sub-launch named), MCPT_BUILD_STAMPS / _LANESTATS / _BLOCKTIMES the instrumented builds,
+ * MCPT_BUILD_DRIVER_MATH a GL-driver-arithmetic build.  0: the shipped library. */
+enum { MCPT_BUILD_CHECKED = 1, MCPT_BUILD_STAMPS = 2, MCPT_BUILD_LANESTATS = 4, MCPT_BUILD_BLOCKTIMES = 8,
+       MCPT_BUILD_DRIVER_MATH = 16 };
+int mcpt_build_flags(void);
 
 /* ---------------------------------------------------------------------------------
  * 1. device renderer

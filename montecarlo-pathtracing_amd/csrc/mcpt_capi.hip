@@ -344,6 +344,26 @@ const char* mcpt_error_string(int status) {
 
 int mcpt_version(void) { return 2; }
 
+int mcpt_build_flags(void) {
+  int f = 0;
+#ifdef MCPT_CHECKED
+  f |= MCPT_BUILD_CHECKED;
+#endif
+#ifdef MCPT_STAMPS
+  f |= MCPT_BUILD_STAMPS;
+#endif
+#ifdef MCPT_LANESTATS
+  f |= MCPT_BUILD_LANESTATS;
+#endif
+#ifdef MCPT_BLOCKTIMES
+  f |= MCPT_BUILD_BLOCKTIMES;
+#endif
+#if MCPT_DRIVER_MATH   // (mcpt_math.h: 0 in the shipped build)
+  f |= MCPT_BUILD_DRIVER_MATH;
+#endif
+  return f;
+}
+
 int mcpt_create(int device_ordinal, mcpt_ctx** out) {
   if (!out) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   *out = nullptr;
@@ -953,6 +973,30 @@ static hipError_t ensure_item_order(mcpt_ctx* c, long long items) {
   return hipSuccess;
 }
 
+#ifdef MCPT_CHECKED
+// checked build (mcpt_internal.h, kCheckedCountSlot): wait for sub-launch k of n_sub and report a
+// HIP fault or an out-of-range index the kernels counted, naming the sub-launch and its shape
+static int checked_sub_launch(mcpt_ctx* c, int k, int n_sub, const mcpt::RenderParams& p) {
+  char what[200];
+  std::snprintf(what, sizeof(what),
+                "checked build: sub-launch %d of %d (passes %d+%d, %d segments, %d items, K %d, tail %d, split max %d)",
+                k, n_sub, p.first_pass, p.n_passes, p.n_segments, p.n_items, p.seg_per_item, p.tail_m, p.split_max);
+  hipError_t e = hipStreamSynchronize(c->stream);
+  if (e != hipSuccess) return set_err(MCPT_ERR_HIP, what, e);
+  unsigned long long v[2] = {0, 0};
+  e = hipMemcpy(v, c->d_events + mcpt::kCheckedCountSlot, sizeof(v), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return set_err(MCPT_ERR_HIP, what, e);
+  if (v[0] != 0) {
+    char msg[256];
+    std::snprintf(msg, sizeof(msg), "%s: %llu out-of-range indices, first at site %llu index %lld", what, v[0],
+                  v[1] >> 48, (long long)(v[1] & 0xffffffffffffull));
+    (void)hipMemset(c->d_events + mcpt::kCheckedCountSlot, 0, sizeof(v));
+    return set_err(MCPT_ERR_HIP, msg);
+  }
+  return MCPT_OK;
+}
+#endif
+
 static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_pass, int n_passes, float date,
                   int bounces, float refract_ind, int variant, bool count, unsigned long long* events) {
   if (!c || !invPV || !invV || n_passes < 0 || variant < 0 || variant > 2)
@@ -1028,7 +1072,11 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   // segment sums in one launch).  Chunk sums still reach the accumulator in chunk order, so
   // the result is bit-identical to one launch.
   const long long seg_bytes = p.n_local_px * 3 * (long long)sizeof(float);
-  const long long max_items = (1LL << 32) / (p.tile_w * mcpt::kTileH) - 1;
+  // (the grid's spare workgroups — split pieces of mesh launches, tail pieces: mcpt_launch_render —
+  // are reserved: tail_m <= 4 x 7 workgroups per CU (tile_w >= 16 outside the mesh kernels))
+  const long long kseg_max = std::max(1, p.seg_per_item);
+  const long long spare = (long long)kSplitMax * (mcpt::kSplitPieces - 1) + 28LL * c->n_cu * (kseg_max - 1);
+  const long long max_items = (1LL << 32) / (p.tile_w * mcpt::kTileH) - 1 - spare;
   if (p.n_tiles > max_items) return set_err(MCPT_ERR_INVALID_ARG, "render target too large for one launch");
   long long max_seg = seg_bytes > 0 ? (long long)(c->partial_budget / (size_t)seg_bytes) : (1LL << 30);
   max_seg = std::max(1LL, std::min(max_seg, p.n_tiles > 0 ? max_items / p.n_tiles : max_items));
@@ -1089,6 +1137,9 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
     p.split_n = nullptr; p.split_of = nullptr; p.split_pass = nullptr; p.split_max = 0;
     p.n_items = (int)items;
     p.tail_m = 0;
+#ifdef MCPT_CHECKED
+    p.check_inject = env_int("MCPT_CHECKED_INJECT", 0);
+#endif
     // split items: mesh launches of whole 32-pass segments, one per item (MCPT_SPLIT_ITEMS=0: off)
     const bool split_items = order && c->n_meshes > 0 && !p.wave_traversal && kseg == 1 && !p.pass_split &&
                              p.n_segments > 1 && (p.first_pass - 1) % mcpt::kPassChunk == 0 &&
@@ -1146,6 +1197,14 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
       c->order_valid = true;
       c->order_age = 0;
     }
+#ifdef MCPT_CHECKED
+    {
+      // checked build: the sub-launch (render, combine, order sort) is waited for here, so a fault
+      // is reported with the sub-launch that caused it, and the kernels' bounds tests are read
+      const int st = checked_sub_launch(c, (int)k, n_sub, p);
+      if (st != MCPT_OK) return st;
+    }
+#endif
     lo = hi;
   }
   if (!count && c->traversal == MCPT_TRAVERSAL_AUTO && !c->tune_choice && samples >= kTuneMinSamples) {

@@ -37,10 +37,8 @@ constexpr int kNodeF4 = 3;
 // the accumulator in chunk order
 constexpr int kPassChunk = 32;
 constexpr int kSplitPieces = 4;   // pass ranges of a split work item (RenderParams::split_n)
-#ifdef MCPT_BLOCKTIMES
 constexpr size_t kBlockTimeSlots = size_t(8) << 20;   // diagnostic build: per-wave clock pairs
 constexpr size_t kBlockTimeBase = 64;                   // after the debug slots (= MCPT_DEBUG_SLOTS)
-#endif
 // largest scene render_kernel stages into LDS: 160 KB / 7 workgroups - 19 KB of per-pixel rows
 constexpr int kLdsSceneBytes = 3584;
 constexpr int kPrimF4 = 8;
@@ -132,6 +130,8 @@ struct RenderParams {
   int tail_m;                   // seg_per_item > 1: the last tail_m items of item_perm run one segment per workgroup
   int tile_w;                   // the launch's tile width (tile_w_for)
   int split_max;                // most split items (grid = n_items + split_max x (kSplitPieces - 1))
+  int check_inject;             // checked build only (MCPT_CHECKED_INJECT=1): test every workgroup id
+                                // against n_items as round 5's tail-piece form read item_perm[b]
   double cull2_max;
 };
 
@@ -218,6 +218,45 @@ hipError_t mcpt_iota(int* a, int n, hipStream_t stream);
 hipError_t mcpt_split_count(const unsigned* cost_sorted, int n, int capacity, int split_max, int* out,
                             unsigned long long* dbg, hipStream_t stream);
 constexpr int kDebugSplitSlot = 63;   // debug counter slot: items split by the last sort (mesh scenes)
+
+// Checked diagnostic build (make checked: -DMCPT_CHECKED; never timed).  Every index the render
+// and combine kernels derive from the work-item order, the split items and the segment slots is
+// tested against its array's length before the access; a violation is counted in debug slot
+// kCheckedCountSlot, the first one's site and index kept in kCheckedSiteSlot (site << 48 | index),
+// and the access is skipped — a bounds bug shows as a count, not as a memory fault that the next
+// HIP call reports.  launch() synchronises after every sub-launch in this build and fails with the
+// sub-launch's number and the site (mcpt_error_string).  Round 6: the tail-piece over-read of round
+// 5 (item_perm read at workgroups >= n_items) would have been site CK_PERM_HEAD.
+namespace mcpt {
+constexpr int kCheckedCountSlot = 60, kCheckedSiteSlot = 61;
+enum CheckSite {
+  CK_SPLIT_N = 1,     // *split_n <= split_max
+  CK_PERM_SPLIT,      // item_perm[sj], a split item's index (sj < n_items)
+  CK_PERM_TAIL,       // item_perm[head + j], a tail piece's item (< n_items)
+  CK_PERM_HEAD,       // item_perm[b] / item b, a whole item's workgroup (b < n_items)
+  CK_ITEM,            // the item a workgroup runs (< n_items)
+  CK_SPLIT_OF,        // split_of[item] (< n_items)
+  CK_SPLIT_PASS,      // split_pass slot: split index < split_max, pass within the chunk
+  CK_SEGMENT,         // segment slot of partial (< n_segments)
+  CK_PIXEL,           // local pixel of accum / partial (< n_local_px)
+  CK_COMBINE_SPLIT,   // combine_items_kernel: split index read from split_of (< split_max)
+  CK_COUNT
+};
+#ifdef MCPT_CHECKED
+constexpr bool kChecked = true;
+__device__ inline bool idx_ok(unsigned long long* ev, int site, long long i, long long n) {
+  if (i >= 0 && i < n) return true;
+  if (ev) {
+    atomicAdd(ev + kCheckedCountSlot, 1ull);
+    atomicCAS(ev + kCheckedSiteSlot, 0ull, ((unsigned long long)site << 48) | ((unsigned long long)i & 0xffffffffffffull));
+  }
+  return false;
+}
+#else
+constexpr bool kChecked = false;
+__device__ __forceinline__ bool idx_ok(unsigned long long*, int, long long, long long) { return true; }
+#endif
+}  // namespace mcpt
 hipError_t mcpt_order_items(const unsigned* cost, unsigned* cost_sorted, const int* iota, int* perm, int n,
                             void* tmp, size_t* tmp_bytes, hipStream_t stream);
 // stream schedule: slot set-up (queue[0] = every slot with a unit), then one iteration = the

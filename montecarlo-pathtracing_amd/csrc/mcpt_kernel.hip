@@ -78,12 +78,19 @@ __global__ __launch_bounds__(TW * kTileH, MESH && !WAVE ? kMinWavesMesh
   // in the mesh kernels the costliest of them split in kSplitPieces pass ranges (piece >= 0)
   constexpr bool kSplit = MESH && !WAVE && !COUNT;
   int item, piece = -1, sj = -1;
+  // (idx_ok: the checked build's bounds tests, mcpt_internal.h; true in the shipped build.  The
+  // workgroup-uniform ones return the whole workgroup before the LDS staging barrier.)
+  if constexpr (kChecked) {   // the checker's own test: round 5's form read item_perm[blockIdx.x] first
+    if (p.check_inject) (void)idx_ok(p.events, CK_PERM_HEAD, blockIdx.x, p.n_items);
+  }
   if constexpr (kSplit) {
     const int b = blockIdx.x;
-    const int sn = (p.item_perm && p.split_n) ? *p.split_n : 0;
+    int sn = (p.item_perm && p.split_n) ? *p.split_n : 0;
+    if (!idx_ok(p.events, CK_SPLIT_N, sn, (long long)p.split_max + 1)) sn = 0;
     if (b < sn * kSplitPieces) {
       sj = b / kSplitPieces;
       piece = b - sj * kSplitPieces;
+      if (!idx_ok(p.events, CK_PERM_SPLIT, sj, p.n_items)) return;
       item = p.item_perm[sj];
     } else {
       const int r = sn + (b - sn * kSplitPieces);
@@ -100,12 +107,15 @@ __global__ __launch_bounds__(TW * kTileH, MESH && !WAVE ? kMinWavesMesh
     const int head = p.tail_m > 0 ? p.n_items - p.tail_m : p.n_items;
     if (b >= head && p.tail_m > 0) {
       const int q = b - head, j = q / p.seg_per_item;
+      if (!idx_ok(p.events, CK_PERM_TAIL, head + j, p.n_items)) return;
       item = p.item_perm[head + j];
       seg_only = q - j * p.seg_per_item;
     } else {
+      if (!idx_ok(p.events, CK_PERM_HEAD, b, p.n_items)) return;
       item = p.item_perm ? p.item_perm[b] : b;
     }
   }
+  if (!idx_ok(p.events, CK_ITEM, item, p.n_items)) return;
   const unsigned long long t_item0 = __builtin_amdgcn_s_memrealtime();
 #ifdef MCPT_BLOCKTIMES
   // diagnostic build only (tools/blocktimes.py; never timed): each wave's start and end on the
@@ -150,7 +160,7 @@ __global__ __launch_bounds__(TW * kTileH, MESH && !WAVE ? kMinWavesMesh
     const int lo = pass_begin + (piece * n) / kSplitPieces, hi = pass_begin + ((piece + 1) * n) / kSplitPieces;
     pass_begin = lo;
     pass_end = hi;
-    if (piece == 0 && tid == 0) p.split_of[item] = sj;
+    if (piece == 0 && tid == 0 && idx_ok(p.events, CK_SPLIT_OF, item, p.n_items)) p.split_of[item] = sj;
   }
   const int y = live ? p.rows[lr] : 0;   // this shard's local row -> image row (mcpt_set_target*)
 
@@ -269,10 +279,12 @@ __global__ __launch_bounds__(TW * kTileH, MESH && !WAVE ? kMinWavesMesh
       asm volatile("" : "+v"(lrow), "+v"(col));
       px = (size_t)lrow * p.W + col;
     }
+    if (!idx_ok(p.events, CK_PIXEL, (long long)px, p.n_local_px)) return;
     if (p.n_segments == 1) {
       float* accp = p.accum + px * 3;
       accp[0] = accp[0] + s_pix[12][tid]; accp[1] = accp[1] + s_pix[13][tid]; accp[2] = accp[2] + s_pix[14][tid];
     } else {
+      if (!idx_ok(p.events, CK_SEGMENT, seg, p.n_segments)) return;
       float* part = p.partial + ((size_t)seg * p.n_local_px + px) * 3;
       part[0] = s_pix[12][tid]; part[1] = s_pix[13][tid]; part[2] = s_pix[14][tid];
     }
@@ -284,6 +296,11 @@ __global__ __launch_bounds__(TW * kTileH, MESH && !WAVE ? kMinWavesMesh
   // for the combine, which adds it after piece 0's sum in pass order
   auto add_pass = [&](f3 v) {
     if (kSplit && piece > 0) {
+      if constexpr (kChecked) {
+        if (!idx_ok(p.events, CK_SPLIT_PASS, sj, p.split_max) || !idx_ok(p.events, CK_SPLIT_PASS, pass - b1, kPassChunk) ||
+            !idx_ok(p.events, CK_SPLIT_PASS, tid, kTileThreads))
+          return;
+      }
       float* q = p.split_pass + (((size_t)sj * kPassChunk + (pass - b1)) * kTileThreads + tid) * 3;
       q[0] = v.x; q[1] = v.y; q[2] = v.z;
     } else {
@@ -562,8 +579,10 @@ __global__ __launch_bounds__(TW * kTileH, MESH && !WAVE ? kMinWavesMesh
   {
     const unsigned long long bt1 = __builtin_amdgcn_s_memrealtime();
     const int lead = __builtin_ffsll((long long)__ballot(1)) - 1, k = (int)__lane_id() - lead;
-    if ((k == 0 || k == 1) && p.events)   // two lanes, one value each (vector stores)
-      p.events[kBlockTimeBase + 2ull * ((unsigned long long)blockIdx.x * (TT / 64) + wave) + k] = k ? bt1 : bt0;
+    // (launches of more waves than the buffer holds drop the later waves' pairs)
+    const unsigned long long slot = 2ull * ((unsigned long long)blockIdx.x * (TT / 64) + wave) + k;
+    if ((k == 0 || k == 1) && p.events && slot < kBlockTimeSlots)   // two lanes, one value each (vector stores)
+      p.events[kBlockTimeBase + slot] = k ? bt1 : bt0;
   }
 #endif
 #ifdef MCPT_LANESTATS
@@ -621,7 +640,8 @@ __global__ __launch_bounds__(256) void combine_kernel(float* __restrict__ accum,
 __global__ __launch_bounds__(256) void combine_items_kernel(float* __restrict__ accum, const float* __restrict__ partial,
                                                             long long n_px, int n_seg, int W, int TW,
                                                             const int* __restrict__ split_of,
-                                                            const float* __restrict__ split_pass) {
+                                                            const float* __restrict__ split_pass, int split_max,
+                                                            unsigned long long* ev) {
   long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   if (i >= n_px) return;
   const int lr = (int)(i / W), x = (int)(i - (long long)lr * W);
@@ -634,7 +654,7 @@ __global__ __launch_bounds__(256) void combine_items_kernel(float* __restrict__ 
     const float* q = partial + ((size_t)s * n_px + i) * 3;
     float s0 = q[0], s1 = q[1], s2 = q[2];
     const int j = split_of[(size_t)tile * n_seg + s];
-    if (j >= 0) {
+    if (j >= 0 && idx_ok(ev, CK_COMBINE_SPLIT, j, split_max)) {
       for (int k = 0; k < kPassChunk - p1; ++k) {
         const float* v = split_pass + (((size_t)j * kPassChunk + k) * kTileThreads + t) * 3;
         s0 = s0 + v[0]; s1 = s1 + v[1]; s2 = s2 + v[2];
@@ -774,7 +794,7 @@ hipError_t mcpt_launch_combine(const mcpt::RenderParams& p, hipStream_t stream) 
                        p.first_pass, p.n_passes);
   else if (p.split_of)
     hipLaunchKernelGGL(mcpt::combine_items_kernel, grid, block, 0, stream, p.accum, p.partial, p.n_local_px,
-                       p.n_segments, p.W, p.tile_w, p.split_of, p.split_pass);
+                       p.n_segments, p.W, p.tile_w, p.split_of, p.split_pass, p.split_max, p.events);
   else
     hipLaunchKernelGGL(mcpt::combine_kernel, grid, block, 0, stream, p.accum, p.partial, p.n_local_px, p.n_segments);
   return hipGetLastError();

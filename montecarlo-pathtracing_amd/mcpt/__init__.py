@@ -77,6 +77,7 @@ def _declare(L: ctypes.CDLL) -> None:
     sig = {
         "mcpt_error_string": (ctypes.c_char_p, [i]),
         "mcpt_version": (i, []),
+        "mcpt_build_flags": (i, []),
         "mcpt_create": (i, [i, ctypes.POINTER(_vp)]),
         "mcpt_destroy": (i, [_vp]),
         "mcpt_upload_scene": (i, [_vp, fp, i, fp, ip, i, i]),
@@ -167,6 +168,14 @@ def lib() -> ctypes.CDLL:
         _declare(L)
         _lib = L
     return _lib
+
+
+BUILD_CHECKED, BUILD_STAMPS, BUILD_LANESTATS, BUILD_BLOCKTIMES, BUILD_DRIVER_MATH = 1, 2, 4, 8, 16
+
+
+def build_flags() -> int:
+    """mcpt_build_flags: which diagnostic build the loaded library is (0: the shipped build)."""
+    return int(lib().mcpt_build_flags())
 
 
 def _check(status: int, what: str) -> None:
