@@ -20,19 +20,20 @@ line.  A rank whose world size differs from ``--gpus``, or that sees fewer GPUs 
 with ranks sharing the visible GPUs (host-staged gloo gather; the line says so).
 
 Configs (BASELINE.json ``configs``):
-* c2 (configs[1], default) — weak scaling: per-GPU work fixed at one C2 frame's worth of
-  samples: at N GPUs a step accumulates 256·N passes of the 1080p frame (progressive
-  accumulation), the frame split into balanced row shards across ranks (mcpt_balanced_rows:
-  rotated 8-row bands; each rank H/N rows × 256·N passes = one C2 frame of samples), then one
-  RCCL gather of the fp32 RGB shards to rank 0 inside the timed region.  Bit-identical to
-  rendering the same passes on one GPU; rank 0 checks that after the timed region
-  (`self_check`: rows owned by every rank of the gathered frame against a single-rank render
-  of those rows).
+* c2 (configs[1], default) — strong scaling (round 6; verdict r05 #4): a step renders ONE fixed
+  1080p × 256-spp frame; at N GPUs the frame's rows are split into balanced row shards across
+  ranks (mcpt_balanced_rows: rotated 8-row bands, H/N rows each, all 256 passes), then one RCCL
+  gather of the fp32 RGB shards to rank 0 inside the timed region, so launch, AUTO-trial, gather
+  and tail overheads count against the N-GPU figure.  ``--scaling weak`` keeps one C2 frame's
+  worth of samples per GPU instead (256·N passes per step, progressive accumulation).
+  Bit-identical to rendering the same passes on one GPU; rank 0 checks that after the timed
+  region (`self_check`: rows owned by every rank of the gathered frame against a single-rank
+  render of those rows).
 * c3 (configs[2]) — scene 6, 1080p, 1024 spp per step, B 8, IOR 1.5, roughness sweep: the
   roughness (material .y) of every non-emissive primitive set to each of 0, 0.5, 0.9, 0.99, 1
   (SURVEY §8d), one measurement per point (``--rough R`` runs one point); `value` = the
-  sweep's samples ÷ its timed seconds, each point listed under ``config.roughness_points``.  Weak
-  scaling like c2.
+  sweep's samples ÷ its timed seconds, each point listed under ``config.roughness_points``.  Strong
+  scaling like c2 (``--scaling weak``: 1024·N passes per step).
 * c4 (configs[3]) — scene 8, 1080p, 512 spp, B 12, the same frame split over N ranks: strong.
 * c5 (configs[4]) — scene 6, 3840×2160, B 8, progressive accumulation toward 84,000 spp: a
   step = 1,024 passes (a bounded slice of the target), the 4K frame split over N ranks
@@ -47,10 +48,13 @@ Configs (BASELINE.json ``configs``):
   "hbm": `achieved` = the §8d algorithmic bytes (counting build of the same kernel) ÷ the
   launch time, `traffic` = the PMC fabric bytes, `traffic_ratio` = traffic ÷ algorithmic, the
   VALU figures under `roofline.valu`.
-``--scaling strong`` runs c2 / c3 as one fixed frame split over the N ranks (the driver's
-default N-GPU runs stay weak); the line's `scaling` says which.  ``--deadline S`` bounds every
-rank's wall time (and the launcher's, + 15 s): a rank past it prints its current phase
-(``PHASES``) and exits 124, and the launcher names the least advanced rank and its phase.
+* mesh_big (round 6; verdict r05 #2) — the mesh workload past the 256 MiB Infinity Cache: four
+  distinct ~1 M-triangle meshes (two UV spheres, two tori), one instance each
+  (mcpt.meshes.big_mesh4_scene), 1080p, 64 spp, B 8, strong; roofline as for mesh.
+``--scaling weak`` runs c2 / c3 with one frame's worth of samples per GPU; the line's `scaling`
+says which.  ``--deadline S`` bounds every rank's wall time (and the launcher's, + 15 s; default
+600 s + 30 s per step and roughness point, <= 0 no limit): a rank past it prints its current
+phase (``PHASES``) and exits 124, and the launcher names the least advanced rank and its phase.
 
 Prints ONE JSON line (rank 0) with
 * `roofline` for the dominant kernel (the path-tracing kernel).  Its limiter is VALU issue,
@@ -102,8 +106,8 @@ C5_TARGET_SPP = 84000
 
 CONFIGS = {   # BASELINE.json configs[0..4]
     "c1": dict(scene=1, width=256, height=256, spp=4, bounces=3, ior=1.0, scaling="weak"),
-    "c2": dict(scene=6, width=1920, height=1080, spp=256, bounces=8, ior=1.0, scaling="weak"),
-    "c3": dict(scene=6, width=1920, height=1080, spp=1024, bounces=8, ior=1.5, scaling="weak",
+    "c2": dict(scene=6, width=1920, height=1080, spp=256, bounces=8, ior=1.0, scaling="strong"),
+    "c3": dict(scene=6, width=1920, height=1080, spp=1024, bounces=8, ior=1.5, scaling="strong",
                rough_sweep=C3_ROUGHNESS),
     "c4": dict(scene=8, width=1920, height=1080, spp=512, bounces=12, ior=1.0, scaling="strong"),
     "c5": dict(scene=6, width=3840, height=2160, spp=1024, bounces=8, ior=1.0, scaling="strong",
@@ -113,6 +117,10 @@ CONFIGS = {   # BASELINE.json configs[0..4]
     # ~130 MB of device mesh records), 1080p, B 8 (mcpt.meshes.big_mesh_scene)
     "mesh": dict(scene="mesh", width=1920, height=1080, spp=64, bounces=8, ior=1.0, scaling="strong",
                  mesh_tris=1_000_000),
+    # past the 256 MiB Infinity Cache (verdict r05 #2): four distinct ~1 M-triangle meshes, one
+    # instance each (mcpt.meshes.big_mesh4_scene), 1080p, 64 spp, B 8
+    "mesh_big": dict(scene="mesh4", width=1920, height=1080, spp=64, bounces=8, ior=1.0, scaling="strong",
+                     mesh_tris=1_000_000),
 }
 # the phases a rank stamps on stderr, in order (the launcher names the rank that stalls, and where)
 PHASES = ("start", "init", "upload", "auto", "warmup", "timed", "stats", "count", "self_check", "cpu_baseline",
@@ -133,17 +141,23 @@ def parse(argv=None):
     ap.add_argument("--no-count", action="store_true", help="skip the reference-byte counting launch")
     ap.add_argument("--no-check", action="store_true", help="skip rank 0's post-run self check")
     ap.add_argument("--scaling", choices=("weak", "strong"), default=None,
-                    help="c2/c3: weak (default: one C2 frame of samples per GPU) or strong (one fixed frame "
-                         "split over the N GPUs)")
-    ap.add_argument("--deadline", type=float, default=480.0,
+                    help="c2/c3: strong (default: one fixed frame split over the N GPUs) or weak (one C2 frame "
+                         "of samples per GPU)")
+    ap.add_argument("--deadline", type=float, default=None,
                     help="wall-clock limit (s) of every rank (and of the launcher, +15 s): a rank past it names "
-                         "its phase on stderr and exits 124")
+                         "its phase on stderr and exits 124.  Default: 600 s + 30 s per warm-up or timed step "
+                         "and roughness point; <= 0: no limit")
     ap.add_argument("--drill-stall", default=None, metavar="RANK:PHASE[:SECONDS]",
                     help="launcher drill (CPU only, MCPT_DIST_BACKEND=gloo): the ranks walk the phases with "
                          "gloo barriers and no GPU work; RANK sleeps SECONDS (default 3600) before PHASE")
     a = ap.parse_args(argv)
     if a.gpus < 1:
         ap.error("--gpus must be >= 1")
+    if a.deadline is None:
+        n_pts = 1 if a.config != "c3" or a.rough is not None else len(C3_ROUGHNESS)
+        a.deadline = 600.0 + 30.0 * (a.steps + a.warmup) * n_pts
+    elif a.deadline <= 0:
+        a.deadline = None   # no limit
     scaling = a.scaling
     for k, v in CONFIGS[a.config].items():
         setattr(a, k, v)
@@ -324,7 +338,7 @@ def launch(args) -> int:
     print(f"bench: starting {args.gpus} ranks (one process per GPU)", file=sys.stderr, flush=True)
     # the ranks stop themselves at --deadline (naming their phase); the launcher's own limit is a
     # little later, for a rank that cannot
-    status, out = spawn_ranks(cmd, args.gpus, deadline_s=args.deadline + 15.0)
+    status, out = spawn_ranks(cmd, args.gpus, deadline_s=None if args.deadline is None else args.deadline + 15.0)
     if status:
         print(f"bench: a rank failed (exit {status}); no result", file=sys.stderr, flush=True)
         return status if status > 0 else 1
@@ -352,7 +366,8 @@ def check_world(gpus: int, world: int, backend: str, n_devices: int, local_world
 # workload
 # ------------------------------------------------------------------------------------------
 def workload_key(args, passes_per_step: int, rough=None) -> str:
-    scene = f"mesh{args.mesh_tris // 1000}k" if args.scene == "mesh" else f"scene{args.scene}"
+    scene = (f"mesh{args.mesh_tris // 1000}k" if args.scene == "mesh" else
+             f"mesh4x{args.mesh_tris // 1000}k" if args.scene == "mesh4" else f"scene{args.scene}")
     k = f"{scene}_{args.width}x{args.height}_{passes_per_step}spp_B{args.bounces}"
     if getattr(args, "ior", 1.0) != 1.0:
         k += f"_ior{args.ior:g}"
@@ -367,6 +382,9 @@ def build_scene(args, rough=None) -> "mcpt.Scene":
     if args.scene == "mesh":
         from mcpt import meshes
         return meshes.big_mesh_scene(args.mesh_tris)[0]
+    if args.scene == "mesh4":
+        from mcpt import meshes
+        return meshes.big_mesh4_scene(args.mesh_tris)[0]
     sc = mcpt.Scene.reference(args.scene, args.light)
     if rough is not None:
         prims, _, _ = sc.buffers()
@@ -443,7 +461,7 @@ def cpu_baseline_run(args, seconds: float, rough=None, threads=None, scene=None)
     from oracle import oracle as orc
     nproc, model = host_cpu()
     mv = None
-    if args.scene == "mesh":   # the mesh workload: its buffers from the scene producer, oracle mesh walk
+    if args.scene in ("mesh", "mesh4"):   # the mesh workloads: buffers from the scene producer, oracle mesh walk
         prims, nodes, leaves = scene.buffers()
         depth = scene.depth()
         mv = orc.MeshView(scene.mesh_buffers())
@@ -466,7 +484,8 @@ def cpu_baseline_run(args, seconds: float, rough=None, threads=None, scene=None)
         dt = time.perf_counter() - t0
         if dt >= seconds or p > args.spp:
             break
-    scene_name = "the mesh workload (mcpt.meshes.big_mesh_scene)" if args.scene == "mesh" else f"scene {args.scene}"
+    scene_name = {"mesh": "the mesh workload (mcpt.meshes.big_mesh_scene)",
+                  "mesh4": "the four-mesh workload (mcpt.meshes.big_mesh4_scene)"}.get(args.scene, f"scene {args.scene}")
     return {"value": round(samples / dt / 1e6, 4), "threads": threads,
             "sample": f"oracle/oracle.cpp, {scene_name} {W}x{H} "
                       f"{'every row' if row_step == 1 else f'every {row_step}nd row'} ({rows} rows), "
@@ -582,6 +601,17 @@ def roofline(workload: str, sha: str, avg_trace_ms: float, ref_bytes: float, byt
                 "valu": valu, "pmc": pmc}
         refb["note"] = ("SURVEY §8d texel-fetch model (incl. the mesh events), counted exactly by the counting "
                         "build of the same kernel: the algorithmic bytes of `achieved`")
+        # which roof binds, from the same-build PMC record (advisor r05): VALU issue against the
+        # measured fabric bytes.  The fabric (L2 -> memory side) counters include Infinity-Cache
+        # hits (MI355X_MICROARCH.md §HBM; TCC_EA0_RDREQ_DRAM = TCC_EA0_RDREQ on gfx950), so
+        # `traffic` is an upper bound on the HBM bytes, never a split of L3 and HBM
+        if valu["frac"] is not None and hbm["frac"] is not None:
+            roof["traffic_frac"] = hbm["frac"]
+            roof["limiter"] = {"valu_issue_frac": valu["frac"], "fabric_frac": hbm["frac"],
+                               "bound_by": "valu issue" if valu["frac"] > hbm["frac"] else "memory",
+                               "note": ("frac prices the algorithmic bytes against the HBM peak (the north "
+                                        "star's roofline); bound_by says which measured rate is closer to its "
+                                        "own peak: VALU lane-instructions / 78.64 T, or fabric bytes (L3 + HBM) / 8 TB/s")}
     else:
         roof = dict(bound="valu", **{k: valu[k] for k in ("achieved", "peak", "unit", "frac", "lane_utilisation",
                                                            "useful_frac")})
@@ -685,7 +715,8 @@ class Watchdog:
         self.t0 = time.time()
         self.phase, self.t_phase = "start", self.t0
         stamp(rank, "start", self.t0)
-        threading.Thread(target=self._run, daemon=True).start()
+        if deadline_s is not None:   # (None: --deadline <= 0, no limit)
+            threading.Thread(target=self._run, daemon=True).start()
 
     def enter(self, phase: str) -> None:
         self.phase, self.t_phase = phase, time.time()
@@ -709,7 +740,7 @@ def init_group(backend: str, local_rank: int, deadline_s: float) -> None:
     """The process group, with a timeout bounded by the deadline (RCCL init and collectives
     fail instead of hanging; gloo likewise)."""
     import datetime
-    to = datetime.timedelta(seconds=max(10.0, min(300.0, deadline_s)))
+    to = datetime.timedelta(seconds=300.0 if deadline_s is None else max(10.0, min(300.0, deadline_s)))
     if backend == "nccl":
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank), timeout=to)
     else:
@@ -730,7 +761,8 @@ def drill(args, world: int, rank: int, wd: Watchdog) -> None:
             dist.barrier()
     wd.enter("done")
     if rank == 0:
-        print(json.dumps({"metric": "drill", "n_gpus": world, "drill": True, "phases": list(PHASES)}), flush=True)
+        print(json.dumps({"metric": "drill", "n_gpus": world, "drill": True, "phases": list(PHASES),
+                          "config": args.config, "scaling": args.scaling}), flush=True)
     dist.destroy_process_group()
 
 
@@ -769,8 +801,8 @@ def main():
             sys.exit(3)
 
     W, H, B = args.width, args.height, args.bounces
-    # passes per step: weak (C2/C3 default) = one frame of samples per GPU; strong (C4/C5/mesh,
-    # or --scaling strong) = one frame in total
+    # passes per step: strong (the default: one frame in total, split over the ranks) or weak
+    # (--scaling weak, c2 / c3; c1) = one frame of samples per GPU
     S = args.spp * world if args.scaling == "weak" else args.spp
     sr = ShardedRenderer(W, H, args.band_rows, world, rank, local_rank)
     stat_dev = sr.device if backend == "nccl" else torch.device("cpu")
@@ -793,7 +825,7 @@ def main():
             a = pt["allstats"]
             pt["roof"] = roofline(workload_key(args, S, pt["rough"]), sha, pt["avg_trace_ms"], float(a[0, 0]),
                                   float(a[:, 0].sum() / max(a[:, 3].sum(), 1.0)), world, pt["launches"],
-                                  bound="hbm" if args.scene == "mesh" else "valu")
+                                  bound="hbm" if args.scene in ("mesh", "mesh4") else "valu")
         config = {
             "workload": workload_key(args, S, main_pt["rough"] if len(points) == 1 else None)
                         + ("_rough-sweep" if len(points) > 1 else ""),

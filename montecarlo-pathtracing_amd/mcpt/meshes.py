@@ -15,7 +15,7 @@ from __future__ import annotations
 
 import numpy as np
 
-__all__ = ["cube", "uv_sphere", "torus", "big_mesh_scene"]
+__all__ = ["cube", "uv_sphere", "torus", "big_mesh_scene", "big_mesh4_scene"]
 
 
 def cube():
@@ -61,15 +61,14 @@ def torus(n_major: int = 32, n_minor: int = 16, r: float = 0.35):
     nrm = np.stack([np.cos(Vv) * np.cos(U), np.cos(Vv) * np.sin(U), np.sin(Vv)], -1)
     pos = ring + r * nrm
     w = n_minor + 1
-    tris = []
-    for i in range(n_major):
-        for j in range(n_minor):
-            a, b, c, d = i * w + j, i * w + j + 1, (i + 1) * w + j, (i + 1) * w + j + 1
-            tris.append((a, c, b))
-            tris.append((b, c, d))
+    # per (i, j): (a, c, b) then (b, c, d), i-major
+    i, j = np.meshgrid(np.arange(n_major, dtype=np.int64), np.arange(n_minor, dtype=np.int64), indexing="ij")
+    a, b = i * w + j, i * w + j + 1
+    c, d = a + w, b + w
+    tris = np.stack([np.stack([a, c, b], -1), np.stack([b, c, d], -1)], 2).reshape(-1, 3)
     bb = np.array([-1 - r, -1 - r, -r, 1 + r, 1 + r, r], np.float32)
     return (pos.reshape(-1, 3).astype(np.float32), nrm.reshape(-1, 3).astype(np.float32),
-            np.array(tris, np.uint32), bb)
+            tris.astype(np.uint32), bb)
 
 
 def big_mesh_scene(n_tris: int = 1_000_000, mcpt_mod=None):
@@ -93,3 +92,31 @@ def big_mesh_scene(n_tris: int = 1_000_000, mcpt_mod=None):
                         m.light([0.9, 0.9, 0.9, 1], 24))
     s.finalize()
     return s, len(t)
+
+
+def big_mesh4_scene(n_tris: int = 1_000_000, mcpt_mod=None):
+    """The mesh workload past the Infinity Cache (bench.py --config mesh_big; verdict r05 item 2):
+    the ground cube, glass sphere and light quad of big_mesh_scene, with FOUR distinct meshes of
+    about `n_tris` triangles each, one instance of each — two UV spheres of different
+    tessellation and two tori — so the instances' walks read four separate mesh BVHs (depth 20
+    at 1 M triangles: 4 x 128 MB of device mesh records in round 5's layout, more than the
+    256 MiB Infinity Cache).  Returns (finalized Scene, triangles of the four meshes)."""
+    import mcpt as m
+    m = mcpt_mod or m
+    n_lat = max(3, int(round((n_tris / 4.0) ** 0.5)))
+    n_minor = max(3, int(round((n_tris / 4.0) ** 0.5)))
+    meshes = [uv_sphere(2 * n_lat, n_lat), uv_sphere(2 * (n_lat + 1), n_lat + 1),
+              torus(2 * n_minor, n_minor, 0.35), torus(2 * (n_minor + 1), n_minor + 1, 0.25)]
+    T, M = m.Transfo, m.material
+    s = m.Scene()
+    s.add_cube(T.mul(T.translate(0, 0, -51), T.scale(500, 500, 1)), M([0.9, 0.9, 0.9, 1], 0.3, 0.95))
+    ids = [s.add_mesh(*mm) for mm in meshes]
+    s.place_mesh(ids[0], T.mul(T.translate(60, -20, 0), T.scale(45)), M([0.1, 0.9, 0.9, 0.4], 0.7, 0.9))
+    s.place_mesh(ids[1], T.mul(T.translate(-70, 40, 10), T.scale(35)), M([0.9, 0.3, 0.1, 1], 0.5, 0.8))
+    s.place_mesh(ids[2], T.mul(T.translate(-60, -55, -20), T.rotateX(30), T.scale(32)), M([0.2, 0.8, 0.3, 1], 0.4, 0.6))
+    s.place_mesh(ids[3], T.mul(T.translate(115, 45, 15), T.rotateX(70), T.scale(30)), M([0.8, 0.8, 0.2, 0.5], 0.6, 0.9))
+    s.add_sphere(T.mul(T.translate(0, 0, 20), T.scale(20)), M([0.9, 0, 0.9, 0.2], 0.6, 0.7))
+    s.add_oriented_quad(T.mul(T.translate(0, 0, 160), T.rotateX(180), T.scale(70, 70, 1)),
+                        m.light([0.9, 0.9, 0.9, 1], 24))
+    s.finalize()
+    return s, [len(mm[2]) for mm in meshes]

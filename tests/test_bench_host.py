@@ -217,6 +217,29 @@ def test_drill_success_relays_the_line():
     assert p.stderr.count("phase=done") == 2
 
 
+def test_default_multi_gpu_run_is_strong_scaling():
+    """`bench.py --gpus N` (the driver's N-GPU command) renders ONE fixed C2 frame split N ways
+    (verdict r05 #4); weak scaling is the opt-in.  The gloo rehearsal of the default 2-rank run
+    reports it in its line."""
+    import subprocess
+    for argv, want in ((["--gpus", "2"], "strong"), (["--gpus", "8", "--config", "c3"], "strong"),
+                       (["--gpus", "2", "--scaling", "weak"], "weak"), (["--config", "c4"], "strong")):
+        assert bench.parse(argv).scaling == want, argv
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--deadline", "60",
+                        "--drill-stall", "1:done:0"], env=_drill_env(), capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads(p.stdout.strip().splitlines()[-1])
+    assert d["n_gpus"] == 2 and d["config"] == "c2" and d["scaling"] == "strong"
+
+
+def test_deadline_default_and_off():
+    a = bench.parse([])
+    assert a.deadline == 600.0 + 30.0 * (a.steps + a.warmup)
+    assert bench.parse(["--config", "c3", "--steps", "2", "--warmup", "1"]).deadline == 600.0 + 30.0 * 3 * 5
+    assert bench.parse(["--deadline", "0"]).deadline is None
+    assert bench.parse(["--deadline", "42"]).deadline == 42.0
+
+
 def test_drill_rank_deadline_under_torchrun():
     """Launched by torch.distributed.run (the driver's N-GPU command), a rank past --deadline
     names its phase and exits 124 by itself."""

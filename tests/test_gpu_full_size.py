@@ -153,3 +153,49 @@ def test_mesh_split_items_same_bits(mcpt_mod, renderer, big_mesh, monkeypatch):
         renderer.set_traversal(0)
     assert n_split > 0
     assert np.array_equal(bits(a), bits(b))
+
+
+@pytest.fixture(scope="module")
+def big_mesh4(mcpt_mod):
+    from mcpt import meshes
+    return meshes.big_mesh4_scene(1_000_000)[0]
+
+
+@pytest.mark.parametrize("traversal", [0, 1])
+def test_mesh_big_rows(mcpt_mod, oracle_mod, renderer, big_mesh4, traversal):
+    """The mesh workload past the Infinity Cache (bench.py --config mesh_big: four distinct meshes
+    of ~1 M triangles, one instance each, mesh BVHs of depth 20), 1080p, B 8, late passes,
+    against the oracle's own mesh DFS on a row subset."""
+    sc = big_mesh4
+    W, H, first, S, B = 1920, 1080, 6_145, 2, 8
+    renderer.set_traversal(traversal)
+    try:
+        img = render(mcpt_mod, renderer, sc, W, H, first, S, B)
+    finally:
+        renderer.set_traversal(0)
+    rows = np.arange(13, H, 151)
+    prims, nodes, leaves = sc.buffers()
+    ipv, iv = oracle_mod.camera(W, H)
+    mv = oracle_mod.MeshView(sc.mesh_buffers())
+    for y in rows:
+        ref, _ = oracle_mod.render(prims, nodes, leaves, sc.depth(), ipv, iv, W, H, first, S, 0.0, B, 1.0, 0,
+                                   row_step=H, row_offset=int(y), meshes=mv)
+        assert np.array_equal(bits(img[y]), bits(ref[int(y)])), f"four-mesh scene row {y}"
+    assert np.isfinite(img).all() and img.mean() > 0
+
+
+def test_mesh_big_split_items_same_bits(mcpt_mod, renderer, big_mesh4, monkeypatch):
+    """Work-item order + split items on the four-mesh workload: three 64-pass calls equal the same
+    passes in launch order without splits, bit for bit."""
+    W, H, B = 1920, 1080, 8
+    renderer.set_traversal(1)
+    try:
+        monkeypatch.setenv("MCPT_ITEM_ORDER", "1")
+        a = render(mcpt_mod, renderer, big_mesh4, W, H, 1, 192, B, split=[64, 64, 64])
+        n_split = int(renderer.debug_counters()[63])
+        monkeypatch.setenv("MCPT_ITEM_ORDER", "0")
+        b = render(mcpt_mod, renderer, big_mesh4, W, H, 1, 192, B, split=[64, 64, 64])
+    finally:
+        renderer.set_traversal(0)
+    assert n_split > 0
+    assert np.array_equal(bits(a), bits(b))

@@ -6,7 +6,8 @@ clock and cache drift hit every candidate alike.  Kernel time from each library'
 
     python tools/ab_interleave.py --scene 0 --libs main variants/libmcpt_mw5.so --walk-exit 16 40
 
---scene 0 is the mesh workload (mcpt.meshes.big_mesh_scene), 1..8 the reference scenes.
+--scene 0 is the mesh workload (mcpt.meshes.big_mesh_scene), -1 the four-mesh workload
+(big_mesh4_scene), 1..8 the reference scenes.
 Prints one JSON line per (library, walk exit): median / mean / min kernel ms and Msamples/s.
 """
 import argparse
@@ -23,7 +24,7 @@ import torch  # noqa: E402,F401  (HIP runtime first)
 
 import mcpt  # noqa: E402
 
-BOUNCES = {0: 8, 1: 3, 2: 8, 3: 8, 4: 8, 5: 8, 6: 8, 7: 8, 8: 12}
+BOUNCES = {-1: 8, 0: 8, 1: 3, 2: 8, 3: 8, 4: 8, 5: 8, 6: 8, 7: 8, 8: 12}
 MAIN = os.path.join(REPO, "montecarlo-pathtracing_amd", "mcpt", "libmcpt.so")
 
 
@@ -90,6 +91,9 @@ def main():
     if a.scene == 0:
         from mcpt import meshes
         sc = meshes.big_mesh_scene(a.mesh_tris)[0]
+    elif a.scene == -1:   # bench.py --config mesh_big
+        from mcpt import meshes
+        sc = meshes.big_mesh4_scene(a.mesh_tris)[0]
     else:
         sc = mcpt.Scene.reference(a.scene)
     prims, nodes, leaves = sc.buffers()
