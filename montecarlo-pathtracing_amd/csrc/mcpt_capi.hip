@@ -80,7 +80,7 @@ struct mcpt_ctx {
   // triangle meshes
   int4* d_minfo = nullptr;
   float4* d_mpairs = nullptr;      // mesh BVH child-pair records (SceneT::mpairs)
-  int* d_mleafid = nullptr;        // mesh-local triangle id per global leaf (SceneT::mleafid)
+  float4* d_mleaftris = nullptr;   // mesh leaf triangle records (SceneT::mleaftris)
   int4* d_mtris = nullptr;
   float4* d_mverts = nullptr;
   float4* d_mnorms = nullptr;
@@ -399,9 +399,9 @@ int mcpt_create(int device_ordinal, mcpt_ctx** out) {
 }
 
 static void free_meshes(mcpt_ctx* c) {
-  (void)hipFree(c->d_minfo); (void)hipFree(c->d_mpairs); (void)hipFree(c->d_mleafid);
+  (void)hipFree(c->d_minfo); (void)hipFree(c->d_mpairs); (void)hipFree(c->d_mleaftris);
   (void)hipFree(c->d_mtris); (void)hipFree(c->d_mverts); (void)hipFree(c->d_mnorms);
-  c->d_minfo = nullptr; c->d_mpairs = nullptr; c->d_mleafid = nullptr;
+  c->d_minfo = nullptr; c->d_mpairs = nullptr; c->d_mleaftris = nullptr;
   c->d_mtris = nullptr; c->d_mverts = nullptr; c->d_mnorms = nullptr;
   c->n_meshes = 0;
 }
@@ -539,53 +539,22 @@ static float int_bits_f(int v) {
   return f;
 }
 
-// A mesh BVH's records (mcpt_internal.h, mesh_pair_slot / mesh_last_slot), `out` at the mesh's
-// first slot.  Internal node i of levels 0 .. d-2 -> 4 rows: (c_left, has_left) (w_left, 0)
-// (c_right, has_right) (w_right, 0).  Last-level node i -> 8 rows: the same four with vertex A's x
-// of each leaf's triangle in the w rows' .w, then (A_l.y, A_l.z, e1_l.x, e1_l.y) (e1_l.z, e2_l)
-// (A_r.y, A_r.z, e1_r.x, e1_r.y) (e1_r.z, e2_r): Triangle_intersect's vertex A and edges
-// B - A, C - A (raytracer_func.frag:354-396) as the binary32 subtractions the device did (same
-// bits).  has = the leaf holds a triangle.  c and w computed as pack_nodes does; 1/w is
-// recomputed on the device (rcp_rn, correctly rounded: the bits of the host's 1/w).
-// d == 0: the root leaf's triangle in the right half of one 8-row record (has_right = 1).
-// tris: the mesh's vertex-id triplets, verts: the vertices (float4).
-static void pack_mesh_records(const float* nodes, const int* leaves, int depth, float4* out, const int4* tris,
-                              const float4* verts) {
-  const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  auto put_tri = [&](float4* r, int k, bool right) {   // r: the record's 8 rows; k: the mesh's leaf k
-    const int t = leaves[k];
-    if (t < 0) return;   // an empty leaf
-    const float4 A = verts[tris[t].x], B = verts[tris[t].y], C = verts[tris[t].z];
-    const float4 e1 = make_float4(B.x - A.x, B.y - A.y, B.z - A.z, 0.0f);
-    const float4 e2 = make_float4(C.x - A.x, C.y - A.y, C.z - A.z, 0.0f);
-    (right ? r[3] : r[1]).w = A.x;
-    (right ? r[2] : r[0]).w = int_bits_f(t + 1);   // has = the triangle id + 1 as int bits (0: empty)
-    r[right ? 6 : 4] = make_float4(A.y, A.z, e1.x, e1.y);
-    r[right ? 7 : 5] = make_float4(e1.z, e2.x, e2.y, e2.z);
-  };
-  if (depth == 0) {
-    float4* r = out;
-    for (int k = 0; k < 8; ++k) r[k] = z;
-    put_tri(r, 0, true);
-    return;
-  }
-  const int n_leaf = 1 << depth, n_node = 2 * n_leaf - 1, first_last = (1 << (depth - 1)) - 1;
+// A mesh BVH's child-pair records: internal node i -> 4 rows (the device's one 64-byte fetch per
+// visit): (c_left, has_left) (w_left, 0) (c_right, has_right) (w_right, 0), c and w computed as
+// pack_nodes does; 1/w is recomputed on the device (rcp_rn, correctly rounded: the bits of the
+// host's 1/w)
+static void pack_mesh_pairs(const float* nodes, const int* leaves, int depth, float4* out) {
+  const int n_leaf = 1 << depth, n_node = 2 * n_leaf - 1;
   std::vector<float4> rec((size_t)n_node * 3);
   pack_nodes(nodes, leaves, depth, rec.data());
   for (int i = 0; i + 1 < n_leaf; ++i) {   // internal nodes 0 .. n_leaf - 2
     const float4* l = &rec[(size_t)(2 * i + 1) * 3];
     const float4* r = &rec[(size_t)(2 * i + 2) * 3];
-    const bool last = i >= first_last;
-    float4* o = out + (size_t)(last ? mcpt::mesh_last_slot(depth, (unsigned)i) : mcpt::mesh_pair_slot((unsigned)i)) * 4;
+    float4* o = out + (size_t)mcpt::mesh_pair_slot((unsigned)i) * 4;
     o[0] = l[0];
     o[1] = make_float4(l[1].x, l[1].y, l[1].z, 0.0f);
     o[2] = r[0];
     o[3] = make_float4(r[1].x, r[1].y, r[1].z, 0.0f);
-    if (last) {
-      for (int k = 4; k < 8; ++k) o[k] = z;
-      put_tri(o, 2 * i + 1 - (n_leaf - 1), false);
-      put_tri(o, 2 * i + 2 - (n_leaf - 1), true);
-    }
   }
 }
 
@@ -607,18 +576,35 @@ int mcpt_upload_meshes(mcpt_ctx* c, int n_meshes, const int* info, int n_nodes, 
     return set_err(MCPT_ERR_INVALID_ARG, "mcpt_upload_meshes: bad arguments");
   // validate the layout: each mesh's BVH within the node / leaf arrays, leaf triangle ids
   // within the mesh's triangles, vertex ids within the vertex array
-  // records: each mesh's in its own run of slots (mesh_pair_slots), the run starting at an even
-  // slot so that two-slot lines are 128-byte aligned; leaf triangle ids indexed by the global leaf
+  // pair records: each mesh's in its own run of slots (mesh_pair_slot), the run starting at an
+  // even slot so that two-slot lines are 128-byte aligned; leaf triangle records indexed by the
+  // global leaf index
   std::vector<unsigned> pair_base(n_meshes);
   size_t n_slots = 0;
   for (int m = 0; m < n_meshes; ++m) {
     const int d = info[4 * m + 2];
     if (d < 0 || d > 24) return set_err(MCPT_ERR_BAD_SCENE, "bad mesh info");
     pair_base[m] = (unsigned)n_slots;
-    n_slots += mcpt::mesh_pair_slots(d);
+    n_slots = (n_slots + mcpt::mesh_pair_slots(d) + 1) & ~(size_t)1;
   }
   if (n_slots * 4 >= (size_t(1) << 31)) return set_err(MCPT_ERR_BAD_SCENE, "mesh BVHs too large");
+  std::vector<float4> hn(std::max<size_t>(n_slots, 2) * 4, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+  for (int m = 0; m < n_meshes; ++m) {
+    const int no = info[4 * m], lo = info[4 * m + 1], d = info[4 * m + 2], to = info[4 * m + 3];
+    if (d < 0 || d > 24 || no < 0 || lo < 0 || to < 0) return set_err(MCPT_ERR_BAD_SCENE, "bad mesh info");
+    const int nl = 1 << d, nn = 2 * nl - 1;
+    if (no + nn > n_nodes || lo + nl > n_leaves) return set_err(MCPT_ERR_BAD_SCENE, "mesh BVH out of range");
+    const int nt = (m + 1 < n_meshes ? info[4 * (m + 1) + 3] : n_tris) - to;
+    if (nt <= 0 || to + nt > n_tris) return set_err(MCPT_ERR_BAD_SCENE, "mesh triangles out of range");
+    for (int k = 0; k < nl; ++k)
+      if (leaves[lo + k] < -1 || leaves[lo + k] >= nt) return set_err(MCPT_ERR_BAD_SCENE, "mesh leaf id out of range");
+    pack_mesh_pairs(nodes + (size_t)no * 6, leaves + lo, d, &hn[(size_t)pair_base[m] * 4]);
+  }
+  for (int id : c->mesh_ids)
+    if (id >= n_meshes) return set_err(MCPT_ERR_BAD_SCENE, "mesh instance refers to a missing mesh");
   std::vector<int4> hi(n_meshes), ht(n_tris);
+  // device mesh info: (first pair slot, first leaf, depth, first triangle)
+  for (int m = 0; m < n_meshes; ++m) hi[m] = make_int4((int)pair_base[m], info[4 * m + 1], info[4 * m + 2], info[4 * m + 3]);
   for (int t = 0; t < n_tris; ++t) {
     const int* v = tris + (size_t)t * 3;
     for (int k = 0; k < 3; ++k)
@@ -630,34 +616,34 @@ int mcpt_upload_meshes(mcpt_ctx* c, int n_meshes, const int* info, int n_nodes, 
     hv[i] = make_float4(verts[3 * i], verts[3 * i + 1], verts[3 * i + 2], 0.0f);
     hm[i] = make_float4(normals[3 * i], normals[3 * i + 1], normals[3 * i + 2], 0.0f);
   }
-  std::vector<float4> hn(std::max<size_t>(n_slots, 2) * 4, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
-  // leaf -> mesh-local triangle id (-1: an empty leaf), read by the device on a triangle's acceptance
-  std::vector<int> hl((size_t)n_leaves, -1);
+  // leaf triangle records (one 64-byte fetch per leaf visit, no index -> vertex indirection):
+  // (A, t) (B - A, 0) (C - A, 0) (0): Triangle_intersect's vertex A and its two edges, computed
+  // with the binary32 subtractions the device did (same bits), and the mesh-local triangle id t
+  // (-1: an empty leaf) as int bits
+  std::vector<float4> hl((size_t)n_leaves * 4, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+  for (int k = 0; k < n_leaves; ++k) hl[(size_t)k * 4].w = int_bits_f(-1);
   for (int m = 0; m < n_meshes; ++m) {
-    const int no = info[4 * m], lo = info[4 * m + 1], d = info[4 * m + 2], to = info[4 * m + 3];
-    if (d < 0 || d > 24 || no < 0 || lo < 0 || to < 0) return set_err(MCPT_ERR_BAD_SCENE, "bad mesh info");
-    const int nl = 1 << d, nn = 2 * nl - 1;
-    if (no + nn > n_nodes || lo + nl > n_leaves) return set_err(MCPT_ERR_BAD_SCENE, "mesh BVH out of range");
-    const int nt = (m + 1 < n_meshes ? info[4 * (m + 1) + 3] : n_tris) - to;
-    if (nt <= 0 || to + nt > n_tris) return set_err(MCPT_ERR_BAD_SCENE, "mesh triangles out of range");
-    for (int k = 0; k < nl; ++k)
-      if (leaves[lo + k] < -1 || leaves[lo + k] >= nt) return set_err(MCPT_ERR_BAD_SCENE, "mesh leaf id out of range");
-    for (int k = 0; k < nl; ++k) hl[(size_t)lo + k] = leaves[lo + k];
-    pack_mesh_records(nodes + (size_t)no * 6, leaves + lo, d, &hn[(size_t)pair_base[m] * 4], &ht[to], hv.data());
+    const int lo = info[4 * m + 1], d = info[4 * m + 2], to = info[4 * m + 3];
+    for (int k = 0; k < (1 << d); ++k) {
+      const int t = leaves[lo + k];
+      if (t < 0) continue;
+      const int4 vi = ht[to + t];
+      const float4 A = hv[vi.x], B = hv[vi.y], C = hv[vi.z];
+      float4* r = &hl[(size_t)(lo + k) * 4];
+      r[0] = make_float4(A.x, A.y, A.z, int_bits_f(t));
+      r[1] = make_float4(B.x - A.x, B.y - A.y, B.z - A.z, 0.0f);
+      r[2] = make_float4(C.x - A.x, C.y - A.y, C.z - A.z, 0.0f);
+    }
   }
-  for (int id : c->mesh_ids)
-    if (id >= n_meshes) return set_err(MCPT_ERR_BAD_SCENE, "mesh instance refers to a missing mesh");
-  // device mesh info: (first slot, first leaf, depth, first triangle)
-  for (int m = 0; m < n_meshes; ++m) hi[m] = make_int4((int)pair_base[m], info[4 * m + 1], info[4 * m + 2], info[4 * m + 3]);
   HIP_OR_RETURN(hipMalloc(&c->d_minfo, hi.size() * sizeof(int4)));
   HIP_OR_RETURN(hipMalloc(&c->d_mpairs, hn.size() * sizeof(float4)));
-  HIP_OR_RETURN(hipMalloc(&c->d_mleafid, hl.size() * sizeof(int)));
+  HIP_OR_RETURN(hipMalloc(&c->d_mleaftris, hl.size() * sizeof(float4)));
   HIP_OR_RETURN(hipMalloc(&c->d_mtris, ht.size() * sizeof(int4)));
   HIP_OR_RETURN(hipMalloc(&c->d_mverts, hv.size() * sizeof(float4)));
   HIP_OR_RETURN(hipMalloc(&c->d_mnorms, hm.size() * sizeof(float4)));
   HIP_OR_RETURN(hipMemcpy(c->d_minfo, hi.data(), hi.size() * sizeof(int4), hipMemcpyHostToDevice));
   HIP_OR_RETURN(hipMemcpy(c->d_mpairs, hn.data(), hn.size() * sizeof(float4), hipMemcpyHostToDevice));
-  HIP_OR_RETURN(hipMemcpy(c->d_mleafid, hl.data(), hl.size() * sizeof(int), hipMemcpyHostToDevice));
+  HIP_OR_RETURN(hipMemcpy(c->d_mleaftris, hl.data(), hl.size() * sizeof(float4), hipMemcpyHostToDevice));
   HIP_OR_RETURN(hipMemcpy(c->d_mtris, ht.data(), ht.size() * sizeof(int4), hipMemcpyHostToDevice));
   HIP_OR_RETURN(hipMemcpy(c->d_mverts, hv.data(), hv.size() * sizeof(float4), hipMemcpyHostToDevice));
   HIP_OR_RETURN(hipMemcpy(c->d_mnorms, hm.data(), hm.size() * sizeof(float4), hipMemcpyHostToDevice));
@@ -1033,7 +1019,7 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
                           (((1LL << c->depth) + c->n_prims) * 4);
     p.lds_scene_bytes = lds <= mcpt::kLdsSceneBytes ? (int)lds : 0;
   }
-  p.minfo = c->d_minfo; p.mpairs = c->d_mpairs; p.mleafid = c->d_mleafid; p.mtris = c->d_mtris;
+  p.minfo = c->d_minfo; p.mpairs = c->d_mpairs; p.mleaftris = c->d_mleaftris; p.mtris = c->d_mtris;
   p.mverts = c->d_mverts; p.mnorms = c->d_mnorms; p.n_meshes = c->n_meshes; p.flat_face = c->flat_face;
   HIP_OR_RETURN(collect_tuning(c));
   // (the counting build is not timed: AUTO counts with the per-lane walk)
@@ -1464,7 +1450,7 @@ int mcpt_trace(mcpt_ctx* c, const float* origins, const float* dirs, int n, int 
   mcpt::TraceParams q;
   q.nodes = c->d_nodes; q.leaves = c->d_leaves; q.ptype = c->d_ptype; q.prims = c->d_prims; q.depth = c->depth;
   q.prim = prim < 0 ? -1 : prim;
-  q.minfo = c->d_minfo; q.mpairs = c->d_mpairs; q.mleafid = c->d_mleafid; q.mtris = c->d_mtris;
+  q.minfo = c->d_minfo; q.mpairs = c->d_mpairs; q.mleaftris = c->d_mleaftris; q.mtris = c->d_mtris;
   q.mverts = c->d_mverts; q.mnorms = c->d_mnorms; q.n_meshes = c->n_meshes; q.flat_face = c->flat_face;
   q.orig = (const float*)buf; q.dir = (const float*)(buf + n3);
   q.out_i = (int*)(buf + 2 * n3); q.out = (float*)(buf + 2 * n3 + ni); q.n = n;

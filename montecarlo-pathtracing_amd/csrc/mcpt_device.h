@@ -94,15 +94,15 @@ struct SceneT {
   const int* __restrict__ ptype;      // type code | mesh id << 4
   const float4* __restrict__ prims;   // 8 per prim: inv r0..r2, trf r0..r2, colour, material
   int depth;
-  // meshes (mcpt_upload_meshes): per mesh (first slot, first leaf, depth, first triangle)
+  // meshes (mcpt_upload_meshes): per mesh (first pair slot, first leaf, depth, first triangle)
   const int4* __restrict__ minfo;
-  // mesh BVHs, mesh space (mcpt_internal.h, mesh_pair_slot / mesh_last_slot): a 64-byte record of
-  // 4 rows per internal node above the last level, both children's boxes, (c_left, has_left)
-  // (w_left, 0) (c_right, has_right) (w_right, 0); a 128-byte record of 8 rows per last-level node,
-  // the same 4 rows (with vertex A.x of the leaves' triangles in the w rows' .w) and the two leaf
-  // triangles (A.yz, B - A, C - A: mesh_rec_tri)
+  // mesh BVHs, mesh space: one 64-byte slot of 4 rows per internal node (slot: mesh_pair_slot,
+  // from the mesh's first slot), both children's boxes, (c_left, has_left) (w_left, 0)
+  // (c_right, has_right) (w_right, 0)
   const float4* __restrict__ mpairs;
-  const int* __restrict__ mleafid;    // per global leaf: the mesh-local triangle id (-1: empty)
+  // 4 rows per mesh leaf at its global leaf index: (A, t) (B - A, 0) (C - A, 0) (0) of the
+  // leaf's triangle, t = the mesh-local triangle id as int bits (-1: empty leaf)
+  const float4* __restrict__ mleaftris;
   const int4* __restrict__ mtris;     // global vertex ids (a, b, c, 0) (intersection_info)
   const float4* __restrict__ mverts;  // (x, y, z, 0)
   const float4* __restrict__ mnorms;
@@ -383,14 +383,14 @@ __device__ __forceinline__ void accept_cand(const SR& s, int index, int shape, i
                      ld4<U>(s.prims, b + 5), h, ev, SR::kFastLen);
 }
 
-// Triangle_intersect raytracer_func.frag:354-396 (Möller–Trumbore, mesh space) on a leaf's triangle
-// as stored (vertex A, edges B - A and C - A: the same binary32 values the test computed from the
-// vertices); a hit keeps the mesh-local triangle index in Hit::tri (the reference's tri_index; its
-// dir is 0), read from the leaf id array only when the test accepts
+// Triangle_intersect raytracer_func.frag:354-396 (Möller–Trumbore, mesh space) on a leaf record
+// (vertex A, edges B - A and C - A: the same binary32 values the test computed from the vertices);
+// a hit keeps the mesh-local triangle index in Hit::tri (the reference's tri_index; its dir is 0)
 template <bool COUNT, class SR>
-__device__ __forceinline__ void tri_test(const SR& s, int t, f3 vA, f3 edge1, f3 edge2, int index, f3 O,
-                                         f3 D, f3 Ol, float4 t0, float4 t1, float4 t2, Hit& h, Ev<COUNT>& ev) {
+__device__ __forceinline__ void tri_test(int t, float4 r0, float4 r1, float4 r2, int index, f3 O, f3 D, f3 Ol,
+                                         float4 t0, float4 t1, float4 t2, Hit& h, Ev<COUNT>& ev) {
   ev.inc(EV_TRI);
+  const f3 vA = mk(r0.x, r0.y, r0.z), edge1 = mk(r1.x, r1.y, r1.z), edge2 = mk(r2.x, r2.y, r2.z);
   const f3 hv = cross3(D, edge2);
   const float det = dot3(edge1, hv);
   if (__builtin_fabsf(det) < kEPS) return;
@@ -413,14 +413,18 @@ __device__ __forceinline__ void tri_test(const SR& s, int t, f3 vA, f3 edge1, f3
   }
 }
 
-// one leaf triangle of a last-level record (rows r0..r7; right: the second child's): vertex A,
-// edges B - A, C - A (pack_mesh_records)
-__device__ __forceinline__ void mesh_rec_tri(bool right, float4 r1, float4 r3, float4 r4, float4 r5, float4 r6,
-                                             float4 r7, f3& A, f3& e1, f3& e2) {
-  const float4 u = right ? r6 : r4, v = right ? r7 : r5;
-  A = mk(right ? r3.w : r1.w, u.x, u.y);
-  e1 = mk(u.z, u.w, v.x);
-  e2 = mk(v.y, v.z, v.w);
+// a mesh leaf visit: the leaf's triangle record in one round trip, then its test (t >= 0)
+template <bool COUNT, class SR>
+__device__ __forceinline__ void mesh_leaf(const SR& s, size_t leaf, int index, f3 O, f3 D, f3 Ol, float4 t0,
+                                          float4 t1, float4 t2, Hit& h, Ev<COUNT>& ev) {
+  const float4* q = s.mleaftris + leaf * 4;
+  const float4 r0 = q[0], r1 = q[1], r2 = q[2];
+  MCPT_ROWS_IN("v"(r0.x), "v"(r0.y), "v"(r0.z), "v"(r0.w), "v"(r1.x), "v"(r1.y), "v"(r1.z), "v"(r2.x),
+               "v"(r2.y), "v"(r2.z));
+  MCPT_ROWS_IN("v"(t0.x), "v"(t0.y), "v"(t0.z), "v"(t0.w), "v"(t1.x), "v"(t1.y), "v"(t1.z), "v"(t1.w),
+               "v"(t2.x), "v"(t2.y), "v"(t2.z), "v"(t2.w));
+  const int t = __float_as_int(r0.w);
+  if (t >= 0) tri_test<COUNT, SR>(t, r0, r1, r2, index, O, D, Ol, t0, t1, t2, h, ev);
 }
 
 // 1/w of a mesh child box, correctly rounded (= the host's 1.0f / w of pack_nodes): rcp_core on
@@ -438,60 +442,54 @@ __device__ __forceinline__ void rcp6_rn(float4 wl, float4 wr, f3& il, f3& ir) {
   }
 }
 
+// a mesh node visit (intersect_bvm for both children, :273-311): the child-pair record in one
+// round trip (all four rows issued together: a visit waits for one fetch), 1/w recomputed
+template <bool COUNT, class SR>
+__device__ __forceinline__ void mesh_pair_tests(const SR& s, size_t node, f3 O, f3 D, f3 invD, f3 Ol, float4 t0,
+                                                float4 t1, float4 t2, double cull2, bool& hl, bool& hr) {
+  const float4* q = s.mpairs + node * 4;
+  const float4 a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
+  MCPT_ROWS_IN("v"(a0.x), "v"(a0.y), "v"(a0.z), "v"(a0.w), "v"(a1.x), "v"(a1.y), "v"(a1.z));
+  MCPT_ROWS_IN("v"(a2.x), "v"(a2.y), "v"(a2.z), "v"(a2.w), "v"(a3.x), "v"(a3.y), "v"(a3.z));
+  MCPT_ROWS_IN("v"(t0.x), "v"(t0.y), "v"(t0.z), "v"(t0.w), "v"(t1.x), "v"(t1.y), "v"(t1.z), "v"(t1.w),
+               "v"(t2.x), "v"(t2.y), "v"(t2.z), "v"(t2.w));
+  f3 il, ir;
+  rcp6_rn(a1, a3, il, ir);
+  hl = (COUNT || a0.w != 0.0f) && box_test_mesh(a0, a1, il, O, D, invD, Ol, t0, t1, t2, cull2);
+  hr = (COUNT || a2.w != 0.0f) && box_test_mesh(a2, a3, ir, O, D, invD, Ol, t0, t1, t2, cull2);
+}
+
 // Mesh_intersect raytracer_func.frag:642-678: the instance's own BVH, same DFS as
-// intersect_bvh (right child first, cull at push with intersect_bvm), stackless per lane.  A
-// node visit reads its record in one round trip (intersect_bvm for both children, :273-311, 1/w
-// recomputed); at a last-level node the visits of its leaves follow in the same step — right
-// leaf, then left, the order the DFS pops them — with their triangles from the same record.
+// intersect_bvh (right child first, cull at push with intersect_bvm), stackless per lane
 template <bool COUNT, bool ANY, class SR>
 __device__ __forceinline__ void mesh_test(const SR& s, int mesh, int index, f3 O, f3 D, f3 Ol, Hit& h,
                                           Ev<COUNT>& ev) {
   ev.inc(EV_MESH);
-  const int4 mi = s.minfo[mesh];   // first slot, first leaf, depth, first triangle
+  const int4 mi = s.minfo[mesh];   // first node, first leaf, depth, first triangle
   const size_t b = (size_t)index * 8;
   const float4 t0 = s.prims[b + 3], t1 = s.prims[b + 4], t2 = s.prims[b + 5];   // read_mesh_transfo
   const f3 invD = mk(rcp_rn(D.x), rcp_rn(D.y), rcp_rn(D.z));
-  const int d = mi.z;
-  const unsigned fl = d > 0 ? (1u << (d - 1)) - 1u : 0u;   // first last-level node
+  const int leaf0 = (1 << mi.z) - 1;
   int node = 0, level = 0;
   uint32_t pending = 0;
   for (;;) {
     bool pop = true;
-    const bool last = level >= d - 1;   // (d == 0: the root is the leaf)
-    const unsigned slot = last ? (d > 0 ? mesh_last_slot(d, (unsigned)node) : 0u) : mesh_pair_slot((unsigned)node);
-    const float4* q = s.mpairs + ((size_t)mi.x + slot) * 4;
-    const float4 a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
-    MCPT_ROWS_IN("v"(a0.x), "v"(a0.y), "v"(a0.z), "v"(a0.w), "v"(a1.x), "v"(a1.y), "v"(a1.z));
-    MCPT_ROWS_IN("v"(a2.x), "v"(a2.y), "v"(a2.z), "v"(a2.w), "v"(a3.x), "v"(a3.y), "v"(a3.z));
-    bool hl = false, hr = true;
-    if (d > 0) {
+    if (node >= leaf0) {
+      ev.inc(EV_LEAF);
+      mesh_leaf<COUNT>(s, (size_t)mi.y + (node - leaf0), index, O, D, Ol, t0, t1, t2, h, ev);
+      if (ANY && h.hit()) return;   // hit_only (:664-665): only a triangle can have set it
+    } else {
       ev.inc(EV_NODE);
-      f3 il, ir;
-      rcp6_rn(a1, a3, il, ir);
-      hl = (COUNT || __float_as_int(a0.w) != 0) && box_test_mesh(a0, a1, il, O, D, invD, Ol, t0, t1, t2, h.cull2);
-      hr = (COUNT || __float_as_int(a2.w) != 0) && box_test_mesh(a2, a3, ir, O, D, invD, Ol, t0, t1, t2, h.cull2);
-    }
-    if (!last) {
+      const size_t j = 2 * (size_t)node + 1;
+      bool hl, hr;
+      mesh_pair_tests<COUNT>(s, (size_t)mi.x + mesh_pair_slot(node), O, D, invD, Ol, t0, t1, t2,
+                             h.cull2, hl, hr);
       pop = !(hl || hr);
-      const int j = 2 * node + 1;
       if (hr) {
         if (hl) pending |= 1u << (level + 1);
-        node = j + 1; level++;
+        node = (int)j + 1; level++;
       } else if (hl) {
-        node = j; level++;
-      }
-    } else {
-      const float4 r4 = q[4], r5 = q[5], r6 = q[6], r7 = q[7];
-      for (int side = 0; side < 2; ++side) {   // right leaf, then left
-        const bool right = side == 0;
-        if (!(right ? hr : hl)) continue;
-        ev.inc(EV_LEAF);
-        if (__float_as_int(right ? a2.w : a0.w) != 0) {   // the leaf holds a triangle
-          f3 A, e1, e2;
-          mesh_rec_tri(right, a1, a3, r4, r5, r6, r7, A, e1, e2);
-          tri_test<COUNT, SR>(s, __float_as_int(right ? a2.w : a0.w) - 1, A, e1, e2, index, O, D, Ol, t0, t1, t2, h, ev);
-        }
-        if (ANY && h.hit()) return;   // hit_only (:664-665): only a triangle can have set it
+        node = (int)j; level++;
       }
     }
     if (pop) {
@@ -732,7 +730,7 @@ struct Walk {
   int mpf;                 // mesh kernels: the last prefetch's dummy value (walk_run_mesh)
   uint32_t mpending;
   f3 Om, Dm, invDm;
-  int4 mi;                 // the mesh's walk bases (walk_mesh_info)
+  int4 mi;                 // the mesh's (first pair slot, first leaf, depth, first triangle)
 };
 
 template <bool COUNT, class SR>
@@ -874,17 +872,6 @@ __device__ __forceinline__ bool walk_run(const SR& s, f3 O, f3 D, Hit& h, Walk& 
 
 
 
-// A mesh's record bases for the per-lane walk, from its minfo (first slot, first leaf, depth, first
-// triangle): (x, y, z, w) = (slot of internal node i - i, slot of last-level node i - 2i, global
-// index of last-level node i's right leaf - 2i, depth); d == 0: node 0 is the root leaf, its
-// record at the mesh's first slot, its leaf the mesh's first
-__device__ __forceinline__ int4 walk_mesh_info(int4 mi) {
-  const int d = mi.z;
-  if (d <= 0) return make_int4(mi.x, mi.x, mi.y, d);
-  const int fl = (1 << (d - 1)) - 1;   // first last-level node
-  return make_int4(mi.x + 1, mi.x + (int)mesh_last_off(d) - 2 * fl, mi.y + 1 - 2 * fl, d);
-}
-
 // walk_run for scenes with mesh instances.  The reference runs an instance's whole mesh DFS
 // (Mesh_intersect raytracer_func.frag:642-678) inside the scene DFS's leaf visit; nested that
 // way on the GPU, only the lanes sitting on a mesh leaf walk their (long, divergent) mesh
@@ -902,21 +889,28 @@ __device__ __forceinline__ bool walk_run_mesh(const SR& s, f3 O, f3 D, Hit& h, W
     bool pop = false;   // the scene walk pops its stack this iteration
     if (w.mprim >= 0) {
       // one step of the instance's mesh walk (mesh_test's loop body)
-      const int4 mi = w.mi;   // (pair slot base, last-level slot base, right-leaf base, depth): walk_mesh_info
+      const int4 mi = w.mi;
       // the instance's transform rows are read again at every mesh step (LDS for small scenes,
       // else L1/L2 hits issued with the step's record) rather than held in the walk state: the
       // mesh workload +6 % (profiles/r05_ab_mesh_trf_reload_waves.jsonl: main vs trf0)
       const float4* tp = s.prims + (size_t)w.mprim * 8 + 3;
       const float4 t0 = tp[0], t1 = tp[1], t2 = tp[2];
-      const int d = mi.w;
-      // a last-level node (d == 0: the root leaf): its 128-byte record holds both leaves'
-      // triangles, tested in this step (round 6: mcpt_internal.h, mesh_last_slot)
-      const bool last = w.mlevel >= d - 1;
-      const float4* q = s.mpairs + (size_t)(unsigned)(last ? mi.y + 2 * w.mnode : mi.x + w.mnode) * 4;
-      // node lanes also request their next record, consumed one step later: the children's line
-      // (both pair records), or above the last level the right child's record (visited next)
-      const int j = 2 * w.mnode + 1;
-      const float4* qc = last ? q : s.mpairs + (size_t)(unsigned)(w.mlevel + 2 < d ? mi.x + j : mi.y + 2 * (j + 1)) * 4;
+      const int mleaf0 = (1 << mi.z) - 1;
+      bool mpop = true;
+      // one record per lane and step, node or leaf alike (64 B: a child-pair record, or a leaf's
+      // triangle record), issued before the lanes split into the node and leaf blocks: the wave
+      // waits once per iteration instead of once per block (measured neutral on the mesh
+      // workload, r05_ab_mesh_prefetch.jsonl session r05x; kept as the simpler form)
+      const bool mleaf = w.mnode >= mleaf0;
+      const size_t j = 2 * (size_t)w.mnode + 1;
+      const float4* q = mleaf ? s.mleaftris + ((size_t)mi.y + (w.mnode - mleaf0)) * 4
+                              : s.mpairs + ((size_t)mi.x + mesh_pair_slot(w.mnode)) * 4;
+      // node lanes also request their children's line (both pair records, or the two leaf
+      // records of the last level), consumed one step later: +0.9..1.4 % on the mesh workload;
+      // the grandchildren's two lines as well: -5..8 % (profiles/r05_ab_mesh_prefetch.jsonl)
+      const float4* qc = mleaf ? q
+                               : ((w.mlevel + 1 < mi.z) ? s.mpairs + ((size_t)mi.x + mesh_pair_slot((unsigned)j)) * 4
+                                                        : s.mleaftris + ((size_t)mi.y + (j - mleaf0)) * 4);
       const float4 a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
       asm volatile("" ::"v"(w.mpf));
       w.mpf = *(const int*)qc;
@@ -924,36 +918,22 @@ __device__ __forceinline__ bool walk_run_mesh(const SR& s, f3 O, f3 D, Hit& h, W
       MCPT_ROWS_IN("v"(a2.x), "v"(a2.y), "v"(a2.z), "v"(a2.w), "v"(a3.x), "v"(a3.y), "v"(a3.z));
       MCPT_ROWS_IN("v"(t0.x), "v"(t0.y), "v"(t0.z), "v"(t0.w), "v"(t1.x), "v"(t1.y), "v"(t1.z), "v"(t1.w),
                    "v"(t2.x), "v"(t2.y), "v"(t2.z), "v"(t2.w));
-      bool hl = false, hr = true;
-      if (d > 0) {
+      if (mleaf) {
+        ev.inc(EV_LEAF);
+        const int t = __float_as_int(a0.w);
+        if (t >= 0) tri_test<COUNT, SR>(t, a0, a1, a2, w.mprim, w.Om, w.Dm, O, t0, t1, t2, h, ev);
+      } else {
         ev.inc(EV_NODE);
         f3 il, ir;
         rcp6_rn(a1, a3, il, ir);
-        hl = (COUNT || __float_as_int(a0.w) != 0) && box_test_mesh(a0, a1, il, w.Om, w.Dm, w.invDm, O, t0, t1, t2, h.cull2);
-        hr = (COUNT || __float_as_int(a2.w) != 0) && box_test_mesh(a2, a3, ir, w.Om, w.Dm, w.invDm, O, t0, t1, t2, h.cull2);
-      }
-      bool mpop = true;
-      if (!last) {
+        const bool hl = (COUNT || a0.w != 0.0f) && box_test_mesh(a0, a1, il, w.Om, w.Dm, w.invDm, O, t0, t1, t2, h.cull2);
+        const bool hr = (COUNT || a2.w != 0.0f) && box_test_mesh(a2, a3, ir, w.Om, w.Dm, w.invDm, O, t0, t1, t2, h.cull2);
         mpop = !(hl || hr);
         if (hr) {
           if (hl) w.mpending |= 1u << (w.mlevel + 1);
-          w.mnode = j + 1; w.mlevel++;
+          w.mnode = (int)j + 1; w.mlevel++;
         } else if (hl) {
-          w.mnode = j; w.mlevel++;
-        }
-      } else if (hl || hr) {
-        // the leaves' visits (the DFS pops the right leaf, then the pending left one): their
-        // triangles from the record's second half
-#pragma nounroll
-        for (int side = 0; side < 2; ++side) {
-          const bool right = side == 0;
-          if (!(right ? hr : hl)) continue;
-          ev.inc(EV_LEAF);
-          if (__float_as_int(right ? a2.w : a0.w) != 0) {   // the leaf holds a triangle
-            const float4 u = q[right ? 6 : 4], v = q[right ? 7 : 5];
-            const f3 A = mk(right ? a3.w : a1.w, u.x, u.y), e1 = mk(u.z, u.w, v.x), e2 = mk(v.y, v.z, v.w);
-            tri_test<COUNT, SR>(s, __float_as_int(right ? a2.w : a0.w) - 1, A, e1, e2, w.mprim, w.Om, w.Dm, O, t0, t1, t2, h, ev);
-          }
+          w.mnode = (int)j; w.mlevel++;
         }
       }
       if (mpop) {
@@ -982,7 +962,7 @@ __device__ __forceinline__ bool walk_run_mesh(const SR& s, f3 O, f3 D, Hit& h, W
           w.Om = xpoint(r0, r1, r2, O);
           w.Dm = wnormalize3<SR::kFastNorm>(xdir(r0, r1, r2, D));
           w.invDm = mk(rcp_rn(w.Dm.x), rcp_rn(w.Dm.y), rcp_rn(w.Dm.z));
-          w.mprim = p; w.mi = walk_mesh_info(s.minfo[pt >> 4]);
+          w.mprim = p; w.mi = s.minfo[pt >> 4];
           w.mnode = 0; w.mlevel = 0; w.mpending = 0;
           pop = false;
         } else {

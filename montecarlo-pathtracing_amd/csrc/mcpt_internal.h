@@ -61,30 +61,15 @@ constexpr int kLdsScene16 = (163840 / 14 - 16 * kTileH * 76) / 16 * 16;
 __host__ __device__ constexpr int tile_w_for(bool mesh, int lds_scene_bytes) {
   return mesh ? 8 : (lds_scene_bytes > 0 ? (lds_scene_bytes <= kLdsScene16 ? 16 : kTileW) : 16);
 }
-// Mesh BVH records (mcpt_upload_meshes; SceneT::mpairs): each mesh owns a run of 64-byte slots
-// from an even slot (its minfo.x), so every two-slot line is 128-byte aligned.
-// * Internal nodes of levels 0 .. d-2: node i -> slot i + 1, a 64-byte child-pair record, so the
-//   records of two siblings (2i+1, 2i+2: the left child's pending pop follows the right child's
-//   subtree) share one 128-byte line.  (Round 5, profiles/r05_ab_mesh_layouts.jsonl: heap order
-//   (slot i) within noise of it, two-level treelets 2-8 % slower.)
-// * Last-level nodes (level d-1, whose children are the leaves), round 6: node i -> slots
-//   mesh_last_off(d) + 2k, k = i - (2^(d-1) - 1), a 128-byte record holding both children's boxes
-//   AND both leaf triangles, so the walk tests the two triangles in the node's own step — the
-//   leaf visits are no longer loop iterations of their own, and the last level's three dependent
-//   fetches (node, right leaf, left leaf) are one.  The mesh-local triangle id of a leaf is in a
-//   side array (SceneT::mleafid), read only when a triangle test accepts a hit.
-// * d == 0 (one triangle, the root is a leaf): one 128-byte record at the run's slot 0, the
-//   triangle in its right half.
-// Records per mesh: 96 B per leaf (round 5: 128 B) — 2^(d-1) x 64 B of pair records (slot 0
-// unused) + 2^(d-1) x 128 B of last-level records.
+// Slot of a mesh BVH internal node's child-pair record (64 B) from its mesh's first slot
+// (mcpt_upload_meshes; SceneT::mpairs): node i -> slot i + 1, so the records of two siblings
+// (2i+1, 2i+2: the left child's pending pop follows the right child's subtree) share one
+// 128-byte line.  Measured interleaved on the mesh workload (tools/ab_interleave.py,
+// profiles/r05_ab_mesh_layouts.jsonl): heap order (slot i) within noise of it, two-level
+// treelets (a node and its right child, the reference's first descent, in one line) 2-8 %
+// slower.
 __host__ __device__ inline unsigned mesh_pair_slot(unsigned i) { return i + 1u; }
-__host__ __device__ inline unsigned mesh_last_off(int d) { return d <= 0 ? 0u : ((1u << (d - 1)) + 1u) & ~1u; }
-__host__ __device__ inline unsigned mesh_last_slot(int d, unsigned i) {   // (d >= 1, i on level d-1)
-  return mesh_last_off(d) + 2u * (i - ((1u << (d - 1)) - 1u));
-}
-__host__ __device__ inline unsigned mesh_pair_slots(int depth) {   // slots one mesh spans (even)
-  return depth <= 0 ? 2u : mesh_last_off(depth) + (1u << depth);
-}
+__host__ __device__ inline unsigned mesh_pair_slots(int depth) { return 1u << depth; }   // slots one mesh spans
 
 struct RenderParams {
   const float4* nodes;
@@ -108,7 +93,7 @@ struct RenderParams {
   // triangle meshes (mcpt_upload_meshes; layouts: SceneT); n_meshes == 0: none
   const int4* minfo;
   const float4* mpairs;
-  const int* mleafid;
+  const float4* mleaftris;
   const int4* mtris;
   const float4* mverts;
   const float4* mnorms;
@@ -202,7 +187,7 @@ struct TraceParams {
   // triangle meshes (mcpt_upload_meshes; layouts: SceneT); n_meshes == 0: none
   const int4* minfo;
   const float4* mpairs;
-  const int* mleafid;
+  const float4* mleaftris;
   const int4* mtris;
   const float4* mverts;
   const float4* mnorms;

@@ -164,7 +164,7 @@ __global__ __launch_bounds__(TW * kTileH, MESH && !WAVE ? kMinWavesMesh
   }
   const int y = live ? p.rows[lr] : 0;   // this shard's local row -> image row (mcpt_set_target*)
 
-  SceneT<MESH, LDSS> s{p.nodes, p.leaves, p.ptype, p.prims, p.depth, p.minfo, p.mpairs, p.mleafid, p.mtris,
+  SceneT<MESH, LDSS> s{p.nodes, p.leaves, p.ptype, p.prims, p.depth, p.minfo, p.mpairs, p.mleaftris, p.mtris,
                        p.mverts, p.mnorms, p.flat_face};
   if constexpr (LDSS) {
     // staged layout: nodes (3 float4 each), prims (8 float4 each), leaves, type codes
@@ -674,7 +674,7 @@ template <bool ANY, bool MESH>
 __global__ __launch_bounds__(256) void trace_kernel(TraceParams q) {
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   if (i >= q.n) return;
-  SceneT<MESH> s{q.nodes, q.leaves, q.ptype, q.prims, q.depth, q.minfo, q.mpairs, q.mleafid, q.mtris, q.mverts,
+  SceneT<MESH> s{q.nodes, q.leaves, q.ptype, q.prims, q.depth, q.minfo, q.mpairs, q.mleaftris, q.mtris, q.mverts,
                  q.mnorms, q.flat_face};
   Ev<false> ev;
   const f3 O = mk(q.orig[3 * i], q.orig[3 * i + 1], q.orig[3 * i + 2]);

@@ -160,7 +160,7 @@ void stream_trace_kernel(StreamParams q) {
   typedef TraceCfg<LDSN> C;
   constexpr int kChunkT = C::kChunk;
   const RenderParams& p = q.r;
-  SceneT<MESH, false> s{p.nodes, p.leaves, p.ptype, p.prims, p.depth, p.minfo, p.mpairs, p.mleafid,
+  SceneT<MESH, false> s{p.nodes, p.leaves, p.ptype, p.prims, p.depth, p.minfo, p.mpairs, p.mleaftris,
                         p.mtris, p.mverts, p.mnorms, p.flat_face};
   if constexpr (LDSN) {
     extern __shared__ float4 s_bvh[];
@@ -303,7 +303,7 @@ template <bool MESH>
 __device__ __forceinline__ bool stream_shade(const StreamParams& q, const Cols& Qi, uint32_t i, const SlotCols& Sl,
                                              int slot, Payload& out) {
   const RenderParams& p = q.r;
-  const SceneT<MESH, false> s{p.nodes, p.leaves, p.ptype, p.prims, p.depth, p.minfo, p.mpairs, p.mleafid,
+  const SceneT<MESH, false> s{p.nodes, p.leaves, p.ptype, p.prims, p.depth, p.minfo, p.mpairs, p.mleaftris,
                               p.mtris, p.mverts, p.mnorms, p.flat_face};
   Ev<false> ev;
   ev.init();
