@@ -702,7 +702,8 @@ def run_point(args, sr, rough, S, world, barrier, stat_dev, wd):
     if args.rank == 0 and not args.no_check:
         check = self_check(args, scene, ipv, iv, frame, args.warmup + args.steps, S, args.local_rank)
     return dict(rough=rough, elapsed=elapsed, sched=sched, launches=launches, gather_ms=gather_ms, avg_trace_ms=avg_trace_ms,
-                avg_combine_ms=avg_combine_ms, allstats=allstats, check=check, scene=scene)
+                avg_combine_ms=avg_combine_ms, allstats=allstats, check=check, scene=scene,
+                events={n: int(v) for n, v in zip(mcpt.EVENT_NAMES, ev_local)})
 
 
 class Watchdog:
@@ -854,6 +855,8 @@ def main():
                                              f"{t_step * 1e3:.1f} ms per step (render + gather); not a measured run "
                                              "of the whole target")
         a = main_pt["allstats"]
+        if not args.no_count:   # the counting launch's events on rank 0 (its rows; all rows at N = 1)
+            main_pt["roof"]["reference_equivalent_bytes"]["events_rank0"] = main_pt["events"]
         checks = [pt["check"] for pt in points if pt["check"] is not None]
         out = {
             "metric": METRIC,

@@ -23,6 +23,28 @@ def test_header_symbols_exported(mcpt_mod):
     assert not missing, missing
 
 
+VARIANTS = os.path.join(REPO, "montecarlo-pathtracing_amd", "mcpt", "variants")
+
+
+@pytest.mark.parametrize("name", ["checked", "stamps", "lanestats", "blocktimes", "drvmath1", "drvmath2", "drvmath4",
+                                  "drvmath7"])
+def test_diagnostic_builds_current(name):
+    """The in-tree diagnostic builds the GPU tests and tools load (round 6: a stale round-5 build
+    lacked a symbol the binding declares): each exports every header symbol and says which build
+    it is (mcpt_build_flags)."""
+    path = os.path.join(VARIANTS, f"libmcpt_{name}.so")
+    assert os.path.exists(path), f"make -C montecarlo-pathtracing_amd/csrc {name}: {path}"
+    L = ctypes.CDLL(path)
+    missing = [n for n in declared() if not hasattr(L, n)]
+    assert not missing, (name, missing)
+    want = {"checked": 1, "stamps": 2, "lanestats": 4, "blocktimes": 8}.get(name, 16)
+    assert L.mcpt_build_flags() == want
+
+
+def test_shipped_build_flags(mcpt_mod):
+    assert mcpt_mod.build_flags() == 0   # the shipped library is no diagnostic build
+
+
 def test_python_binding_covers_header(mcpt_mod):
     L = mcpt_mod.lib()
     for n in declared():

@@ -3,12 +3,18 @@
 shards of an 8-GPU run (the balanced partition bench.py uses, mcpt_balanced_rows), each rendered on this GPU as ONE mcpt_render call of 84,000 passes
 (the library cuts it into chunk-aligned launches within its segment-sum budget).
 
+Whole frame (round 6, verdict r05 #6): the 3840x2160 frame as ONE mcpt_render call of 84,000
+passes on this GPU — the measured one-GPU time to target — and `--oracle-pixels` pixels of its
+accumulator checked bit for bit against the CPU oracle's sums of the same 84,000 passes
+(oracle.render_pixels, the chunked accumulation contract), so the last passes are covered too.
+
 Per shard: kernel time (sum over the call's launches, HIP events), wall time of the call,
 launch count.  The slowest shard is the 8-GPU time to 84,000 spp (shards are independent;
 the one RCCL gather of the 99.5 MB frame is not included).  Rank 0 is also rendered as the
 progressive sequence of 1,024-pass calls C5 describes, which must give the same bits.
 
     python tools/c5_full.py [--passes 84000] [--ranks 0 1 ... 7] [--no-progressive-check]
+                            [--no-whole] [--oracle-pixels 256]
 """
 import argparse
 import json
@@ -35,6 +41,8 @@ def main():
     ap.add_argument("--no-progressive-check", action="store_true")
     ap.add_argument("--traversal", type=int, default=0, help="0 AUTO (trials on 256-pass launches), 1 lane, 2 wave")
     ap.add_argument("--seg-per-item", type=int, default=0, help="> 0: MCPT_SEG_PER_ITEM for every launch")
+    ap.add_argument("--no-whole", action="store_true", help="skip the whole-frame one-GPU run")
+    ap.add_argument("--oracle-pixels", type=int, default=256, help="whole-frame pixels checked against the oracle")
     a = ap.parse_args()
     if a.seg_per_item > 0:
         os.environ["MCPT_SEG_PER_ITEM"] = str(a.seg_per_item)
@@ -46,6 +54,44 @@ def main():
     # AUTO traversal trials on this launch shape first (same bits either way)
     for _ in range(mcpt.AUTO_TRIALS):
         r.render(ipv, iv, 1, 256, 0.0, B, 1.0, 0)
+    whole = None
+    if not a.no_whole:
+        # the whole frame in one call: the one-GPU time to target, measured
+        r.set_target(W, H)
+        for _ in range(mcpt.AUTO_TRIALS):   # AUTO's trials on this target's 256-pass launches
+            r.render(ipv, iv, 1, 256, 0.0, B, 1.0, 0)
+        r.clear_accum()
+        r.synchronize()
+        t0 = time.perf_counter()
+        r.render(ipv, iv, 1, a.passes, 0.0, B, 1.0, 0)
+        r.synchronize()
+        wall = time.perf_counter() - t0
+        kms, cms = r.last_kernel_ms()
+        acc, n = r.read_accum()
+        assert n == a.passes and np.isfinite(acc).all()
+        whole = {"config": "C5", "whole_frame": True, "width": W, "height": H, "spp": a.passes, "bounces": B,
+                 "launches": r.last_launch_count(), "kernel_ms": round(kms, 1), "combine_ms": round(cms, 2),
+                 "time_to_target_s": round(wall, 3), "msamples_s_wall": round(W * H * a.passes / wall / 1e6, 1),
+                 "schedule": r.schedule(),
+                 "mean_radiance": [round(float(v), 5) for v in (acc.reshape(-1, 3).mean(0) / a.passes)]}
+        if a.oracle_pixels > 0:
+            sys.path.insert(0, REPO)
+            from oracle import oracle as orc   # the checker (test infrastructure), after the timed call
+            rng = np.random.default_rng(84000)
+            xs = rng.integers(0, W, a.oracle_pixels)
+            ys = rng.integers(0, H, a.oracle_pixels)
+            prims, nodes, leaves, depth, _ = orc.scene(6)
+            oipv, oiv = orc.camera(W, H)
+            t1 = time.perf_counter()
+            ref = orc.render_pixels(prims, nodes, leaves, depth, oipv, oiv, W, H, np.stack([xs, ys], 1), 1, a.passes,
+                                    0.0, B, 1.0, 0, n_threads=16)
+            got = acc[ys, xs]
+            diff = int((got.view(np.uint32) != ref.view(np.uint32)).sum())
+            whole["oracle_check"] = {"pixels": int(a.oracle_pixels), "passes": f"1..{a.passes}",
+                                     "channels_differing": diff, "bit_equal": diff == 0,
+                                     "oracle_s": round(time.perf_counter() - t1, 1),
+                                     "pixels_seed": 84000}
+        print(json.dumps(whole), flush=True)
     shard_ms = []
     for rank in a.ranks:
         r.set_target_rows(W, H, local_rows(H, BAND, WORLD, rank, "balanced"))
@@ -79,6 +125,8 @@ def main():
                       "traversal": a.traversal, "seg_per_item": a.seg_per_item,
                       "slowest_shard_wall_s": round(max(shard_ms) / 1e3, 2),
                       "shard_balance": round(min(shard_ms) / max(shard_ms), 3),
+                      "one_gpu_time_to_target_s": whole["time_to_target_s"] if whole else None,
+                      "one_gpu_oracle_bit_equal": whole.get("oracle_check", {}).get("bit_equal") if whole else None,
                       "projected_8gpu_msamples_s": round(W * H * a.passes / max(shard_ms) / 1e3, 1),
                       "note": "8-GPU time to target = slowest shard (independent shards, measured one after "
                               "another on one GPU); excludes the one RCCL gather of the 99.5 MB frame"}),
