@@ -248,6 +248,14 @@ int mcpt_stream_iterations(mcpt_ctx* ctx, long long* iterations);
 int mcpt_set_leaf_batch(mcpt_ctx* ctx, int lanes);
 int mcpt_get_leaf_batch(mcpt_ctx* ctx, int* resolved_lanes);
 
+/* Render lanes (round 6): once the schedule is settled, the sub-launches of render calls
+ * alternate between two internal lanes (HIP streams with their own segment-sum buffers and
+ * work-item order state), so a launch's render kernel starts while the previous launch's last
+ * workgroups still run; the combines stay in call order on the context's stream, which is
+ * ordered after all lane work (results are the same bits).  on = 0: every launch in order on the
+ * context's stream.  Default 1 (environment MCPT_OVERLAP=0: 0). */
+int mcpt_set_render_lanes(mcpt_ctx* ctx, int on);
+
 /* Bound (bytes) of the device buffer holding the per-chunk partial sums of one launch.  A
  * render call whose pass range spans more 32-pass chunks than fit is run as several launches
  * cut at chunk boundaries (e.g. 84,000 passes at 4K in one call); the accumulator is

@@ -95,8 +95,6 @@ struct mcpt_ctx {
   int pass_count = 0;
   bool has_target = false;
   unsigned long long* d_events = nullptr;
-  float* d_partial = nullptr;       // pass-segment sums (launches spanning > 1 chunk)
-  size_t partial_bytes = 0;
   // per sub-launch of a render call: (start, after the path-tracing kernel, after the combine
   // kernel); a call is split into sub-launches at chunk boundaries (partial_budget).  The last
   // kTimingRing calls keep their events (mcpt_kernel_ms_back), so a caller can time a run of
@@ -141,21 +139,38 @@ struct mcpt_ctx {
   int stream_slots = 0;             // MCPT_STREAM_SLOTS env / mcpt_set_stream_pool (0: default)
   int stream_refill = -1;           // MCPT_STREAM_REFILL env / mcpt_set_stream_pool (-1: default)
   long long stream_iters = 0;       // iterations of the last stream render (diagnostics)
-  // work-item order (mcpt_order.hip): item costs of the last ordered launch, the order sorted
-  // from them (costliest first) and the launch shape it belongs to
-  unsigned* d_item_cost = nullptr;
-  unsigned* d_cost_sorted = nullptr;
-  int* d_item_iota = nullptr;
-  int* d_item_perm = nullptr;
-  int* d_split_of = nullptr;        // split items: item -> split index (-1: whole)
-  float* d_split_pass = nullptr;    // split items: the later pieces' per-pass values
-  int* d_split_n = nullptr;         // split items: how many (from the last sort)
-  void* d_sort_tmp = nullptr;
-  size_t sort_tmp_bytes = 0;
-  long long item_cap = 0;
-  long long order_key[8] = {};
-  bool order_valid = false;
-  int order_age = 0;                // launches since the order was last sorted
+  // Render lanes (round 6): the sub-launches of render calls alternate between two lanes, each with
+  // its own HIP stream, segment-sum buffer and work-item order state, so that a launch's render
+  // kernel can start while the previous launch's last workgroups still run (its tail).  The
+  // combines stay in call order on `stream`; a lane's next render waits for the lane's previous
+  // combine (its buffers free).  Lane launches are only used once AUTO has settled, for launches
+  // of several pass segments (a one-segment launch adds into the accumulator itself).
+  struct Lane {
+    hipStream_t stream = nullptr;
+    hipEvent_t freed = nullptr;     // on `stream` after the lane's last combine: its buffers are free
+    hipEvent_t tail = nullptr;      // on the lane's stream after its last operation
+    float* d_partial = nullptr;     // pass-segment sums (launches spanning > 1 chunk)
+    size_t partial_bytes = 0;
+    // work-item order (mcpt_order.hip): item costs of the lane's last ordered launch, the order
+    // sorted from them (costliest first) and the launch shape it belongs to
+    unsigned* d_item_cost = nullptr;
+    unsigned* d_cost_sorted = nullptr;
+    int* d_item_iota = nullptr;
+    int* d_item_perm = nullptr;
+    int* d_split_of = nullptr;      // split items: item -> split index (-1: whole)
+    float* d_split_pass = nullptr;  // split items: the later pieces' per-pass values
+    int* d_split_n = nullptr;       // split items: how many (from the last sort)
+    void* d_sort_tmp = nullptr;
+    size_t sort_tmp_bytes = 0;
+    long long item_cap = 0;
+    long long order_key[8] = {};
+    bool order_valid = false;
+    int order_age = 0;              // launches since the order was last sorted
+  };
+  Lane lanes[2];
+  int next_lane = 0;                // the lane of the next sub-launch
+  int overlap = 1;                  // MCPT_OVERLAP (0: every launch in order on `stream`)
+  int prev_lane = -1;               // the lane of the previous sub-launch if it was a lane launch, else -1
 };
 
 // events of sub-launch k of the last call: start / mid / stop
@@ -275,7 +290,7 @@ static int cand_traversal(int cand) { return cand >= kCandLaneSeg2 ? MCPT_TRAVER
 static int resolve_traversal(const mcpt_ctx* c) { return cand_traversal(resolve_candidate(c, c->meas_segs)); }
 
 static void reset_tuning(mcpt_ctx* c) {
-  c->order_valid = false;           // a new scene / target: item costs start over
+  for (auto& L : c->lanes) L.order_valid = false;   // a new scene / target: item costs start over
   c->tune_pending = 0;
   c->tune_samples = 0.0;
   c->tune_shape[0] = c->tune_shape[1] = c->meas_shape[0] = c->meas_shape[1] = 0;
@@ -381,6 +396,17 @@ int mcpt_create(int device_ordinal, mcpt_ctx** out) {
       c->n_cu <= 0)
     c->n_cu = 256;
   hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+  for (auto& L : c->lanes) {
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&L.freed, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&L.tail, hipEventDisableTiming);
+  }
+  // (recorded once, so that the first waits on them are satisfied)
+  for (auto& L : c->lanes) {
+    if (e == hipSuccess) e = hipEventRecord(L.freed, c->own_stream);
+    if (e == hipSuccess) e = hipEventRecord(L.tail, L.stream);
+  }
+  c->overlap = env_int("MCPT_OVERLAP", 1);
   if (e == hipSuccess) e = ensure_events(c, 0, 1);
   if (const char* pb = std::getenv("MCPT_PARTIAL_BYTES")) c->partial_budget = (size_t)std::strtoull(pb, nullptr, 10);
 #ifdef MCPT_BLOCKTIMES
@@ -421,15 +447,21 @@ int mcpt_destroy(mcpt_ctx* c) {
   (void)hipFree(c->d_accum);
   (void)hipFree(c->d_rows);
   (void)hipFree(c->d_events);
-  (void)hipFree(c->d_partial);
-  (void)hipFree(c->d_item_cost);
-  (void)hipFree(c->d_cost_sorted);
-  (void)hipFree(c->d_item_iota);
-  (void)hipFree(c->d_item_perm);
-  (void)hipFree(c->d_split_of);
-  (void)hipFree(c->d_split_pass);
-  (void)hipFree(c->d_split_n);
-  (void)hipFree(c->d_sort_tmp);
+  for (auto& L : c->lanes) {
+    if (L.stream) (void)hipStreamSynchronize(L.stream);
+    (void)hipFree(L.d_partial);
+    (void)hipFree(L.d_item_cost);
+    (void)hipFree(L.d_cost_sorted);
+    (void)hipFree(L.d_item_iota);
+    (void)hipFree(L.d_item_perm);
+    (void)hipFree(L.d_split_of);
+    (void)hipFree(L.d_split_pass);
+    (void)hipFree(L.d_split_n);
+    (void)hipFree(L.d_sort_tmp);
+    if (L.freed) (void)hipEventDestroy(L.freed);
+    if (L.tail) (void)hipEventDestroy(L.tail);
+    if (L.stream) (void)hipStreamDestroy(L.stream);
+  }
   (void)hipFree(c->d_slots);
   (void)hipFree(c->d_queue);
   (void)hipFree(c->d_sctr);
@@ -683,7 +715,7 @@ static int set_target_rows(mcpt_ctx* c, int W, int H, const int* rows, int n_row
   if (n_rows) HIP_OR_RETURN(hipMemcpy(c->d_rows, rows, sizeof(int) * (size_t)n_rows, hipMemcpyHostToDevice));
   c->W = W; c->H = H; c->band_rows = band_rows; c->world = world; c->rank = rank; c->n_local_rows = n_rows;
   c->has_target = true;
-  c->order_valid = false;   // other pixels: the item costs start over
+  for (auto& L : c->lanes) L.order_valid = false;   // other pixels: the item costs start over
   return mcpt_clear_accum(c);
 }
 
@@ -946,56 +978,44 @@ static int free_stream_pools(mcpt_ctx* c) {
 
 // Buffers of the work-item order for `items` items (grown on demand, with the identity values
 // the sort permutes and its temporary storage)
-static hipError_t ensure_item_order(mcpt_ctx* c, long long items) {
-  if (items <= c->item_cap) return hipSuccess;
+static hipError_t ensure_item_order(mcpt_ctx* c, mcpt_ctx::Lane& L, long long items) {
+  if (items <= L.item_cap) return hipSuccess;
   hipError_t e = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(L.stream);
   if (e != hipSuccess) return e;
-  (void)hipFree(c->d_item_cost); (void)hipFree(c->d_cost_sorted); (void)hipFree(c->d_item_iota);
-  (void)hipFree(c->d_item_perm); (void)hipFree(c->d_sort_tmp); (void)hipFree(c->d_split_of);
-  c->d_item_cost = c->d_cost_sorted = nullptr; c->d_item_iota = c->d_item_perm = nullptr; c->d_sort_tmp = nullptr;
-  c->d_split_of = nullptr;
-  c->item_cap = 0; c->sort_tmp_bytes = 0; c->order_valid = false;
+  (void)hipFree(L.d_item_cost); (void)hipFree(L.d_cost_sorted); (void)hipFree(L.d_item_iota);
+  (void)hipFree(L.d_item_perm); (void)hipFree(L.d_sort_tmp); (void)hipFree(L.d_split_of);
+  L.d_item_cost = L.d_cost_sorted = nullptr; L.d_item_iota = L.d_item_perm = nullptr; L.d_sort_tmp = nullptr;
+  L.d_split_of = nullptr;
+  L.item_cap = 0; L.sort_tmp_bytes = 0; L.order_valid = false;
   const size_t n = (size_t)items;
   size_t tmp = 0;
-  if ((e = hipMalloc(&c->d_item_cost, sizeof(unsigned) * n)) != hipSuccess) return e;
-  if ((e = hipMalloc(&c->d_cost_sorted, sizeof(unsigned) * n)) != hipSuccess) return e;
-  if ((e = hipMalloc(&c->d_item_iota, sizeof(int) * n)) != hipSuccess) return e;
-  if ((e = hipMalloc(&c->d_item_perm, sizeof(int) * n)) != hipSuccess) return e;
-  if ((e = hipMalloc(&c->d_split_of, sizeof(int) * n)) != hipSuccess) return e;
-  if (!c->d_split_n && (e = hipMalloc(&c->d_split_n, sizeof(int))) != hipSuccess) return e;
-  if ((e = hipMemsetAsync(c->d_split_n, 0, sizeof(int), c->stream)) != hipSuccess) return e;
+  if ((e = hipMalloc(&L.d_item_cost, sizeof(unsigned) * n)) != hipSuccess) return e;
+  if ((e = hipMalloc(&L.d_cost_sorted, sizeof(unsigned) * n)) != hipSuccess) return e;
+  if ((e = hipMalloc(&L.d_item_iota, sizeof(int) * n)) != hipSuccess) return e;
+  if ((e = hipMalloc(&L.d_item_perm, sizeof(int) * n)) != hipSuccess) return e;
+  if ((e = hipMalloc(&L.d_split_of, sizeof(int) * n)) != hipSuccess) return e;
+  if (!L.d_split_n && (e = hipMalloc(&L.d_split_n, sizeof(int))) != hipSuccess) return e;
+  if ((e = hipMemset(L.d_split_n, 0, sizeof(int))) != hipSuccess) return e;
   if ((e = mcpt_order_items(nullptr, nullptr, nullptr, nullptr, (int)items, nullptr, &tmp, c->stream)) != hipSuccess)
     return e;
-  if ((e = hipMalloc(&c->d_sort_tmp, std::max<size_t>(tmp, 1))) != hipSuccess) return e;
-  if ((e = mcpt_iota(c->d_item_iota, (int)items, c->stream)) != hipSuccess) return e;
-  c->sort_tmp_bytes = tmp;
-  c->item_cap = items;
+  if ((e = hipMalloc(&L.d_sort_tmp, std::max<size_t>(tmp, 1))) != hipSuccess) return e;
+  if ((e = mcpt_iota(L.d_item_iota, (int)items, c->stream)) != hipSuccess) return e;
+  if ((e = hipStreamSynchronize(c->stream)) != hipSuccess) return e;
+  L.sort_tmp_bytes = tmp;
+  L.item_cap = items;
   return hipSuccess;
 }
 
-#ifdef MCPT_CHECKED
-// checked build (mcpt_internal.h, kCheckedCountSlot): wait for sub-launch k of n_sub and report a
-// HIP fault or an out-of-range index the kernels counted, naming the sub-launch and its shape
-static int checked_sub_launch(mcpt_ctx* c, int k, int n_sub, const mcpt::RenderParams& p) {
-  char what[200];
-  std::snprintf(what, sizeof(what),
-                "checked build: sub-launch %d of %d (passes %d+%d, %d segments, %d items, K %d, tail %d, split max %d)",
-                k, n_sub, p.first_pass, p.n_passes, p.n_segments, p.n_items, p.seg_per_item, p.tail_m, p.split_max);
-  hipError_t e = hipStreamSynchronize(c->stream);
-  if (e != hipSuccess) return set_err(MCPT_ERR_HIP, what, e);
-  unsigned long long v[2] = {0, 0};
-  e = hipMemcpy(v, c->d_events + mcpt::kCheckedCountSlot, sizeof(v), hipMemcpyDeviceToHost);
-  if (e != hipSuccess) return set_err(MCPT_ERR_HIP, what, e);
-  if (v[0] != 0) {
-    char msg[256];
-    std::snprintf(msg, sizeof(msg), "%s: %llu out-of-range indices, first at site %llu index %lld", what, v[0],
-                  v[1] >> 48, (long long)(v[1] & 0xffffffffffffull));
-    (void)hipMemset(c->d_events + mcpt::kCheckedCountSlot, 0, sizeof(v));
-    return set_err(MCPT_ERR_HIP, msg);
-  }
-  return MCPT_OK;
+// every render lane's queued work finished (before buffers they use are freed or reallocated)
+static hipError_t sync_lanes(mcpt_ctx* c) {
+  for (auto& L : c->lanes)
+    if (L.stream) {
+      const hipError_t e = hipStreamSynchronize(L.stream);
+      if (e != hipSuccess) return e;
+    }
+  return hipSuccess;
 }
-#endif
 
 static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_pass, int n_passes, float date,
                   int bounces, float refract_ind, int variant, bool count, unsigned long long* events) {
@@ -1099,17 +1119,9 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   }
   const int slot = (c->ring_pos + 1) % kTimingRing;   // this call's events (ring of calls)
   HIP_OR_RETURN(ensure_events(c, slot, std::max(n_sub, 1)));
-  const long long segs = split ? n_passes : std::min(max_seg, total_seg);   // most segments of one sub-launch
-  if (segs > 1 && (size_t)segs * (size_t)seg_bytes > c->partial_bytes) {
-    const size_t need = (size_t)segs * (size_t)seg_bytes;
-    HIP_OR_RETURN(hipStreamSynchronize(c->stream));
-    (void)hipFree(c->d_partial);
-    c->d_partial = nullptr;
-    c->partial_bytes = 0;
-    HIP_OR_RETURN(hipMalloc(&c->d_partial, need));
-    c->partial_bytes = need;
-  }
-  p.partial = c->d_partial;
+  // lane launches (mcpt_ctx::Lane): once AUTO has settled (its trials are timed one at a time)
+  const bool lanes_ok = c->overlap != 0 && !count && !stream &&
+                        (c->traversal != MCPT_TRAVERSAL_AUTO || c->tune_choice != 0);
   if (count) HIP_OR_RETURN(hipMemsetAsync(c->d_events, 0, sizeof(unsigned long long) * mcpt::EV_COUNT, c->stream));
   const double samples = (double)p.n_local_px * n_passes;
   // The call's events go to ring slot `slot`; the ring position (what mcpt_last_render_ms and
@@ -1144,10 +1156,30 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
     const bool split_items = order && c->n_meshes > 0 && !p.wave_traversal && kseg == 1 && !p.pass_split &&
                              p.n_segments > 1 && (p.first_pass - 1) % mcpt::kPassChunk == 0 &&
                              p.n_passes % mcpt::kPassChunk == 0 && env_int("MCPT_SPLIT_ITEMS", 1) != 0;
+    // the sub-launch's lane: its segment-sum buffer and work-item order state.  A lane launch
+    // (several segments: the render writes only the lane's buffers) runs its set-up and render on
+    // the lane's stream once the lane's previous combine is done, so it can start while the
+    // previous launch's last workgroups still run; the combine follows on `stream` in call order.
+    const int li = c->next_lane;
+    c->next_lane ^= 1;
+    mcpt_ctx::Lane& L = c->lanes[li];
+    const bool lane = lanes_ok && p.n_segments > 1;
+    hipStream_t ws = lane ? L.stream : c->stream;   // the stream of the render and its set-up
+    if (p.n_segments > 1 && (size_t)p.n_segments * (size_t)seg_bytes > L.partial_bytes) {
+      const size_t need = (size_t)p.n_segments * (size_t)seg_bytes;
+      HIP_OR_RETURN(hipStreamSynchronize(c->stream));   // (ordered after every lane's work)
+      (void)hipFree(L.d_partial);
+      L.d_partial = nullptr;
+      L.partial_bytes = 0;
+      HIP_OR_RETURN(hipMalloc(&L.d_partial, need));
+      L.partial_bytes = need;
+    }
+    p.partial = L.d_partial;
+    if (order) HIP_OR_RETURN(ensure_item_order(c, L, items));
+    if (lane) HIP_OR_RETURN(hipStreamWaitEvent(L.stream, L.freed, 0));
     if (order) {
-      HIP_OR_RETURN(ensure_item_order(c, items));
-      if (c->order_valid && std::equal(key, key + 8, c->order_key)) {
-        p.item_perm = c->d_item_perm;
+      if (L.order_valid && std::equal(key, key + 8, L.order_key)) {
+        p.item_perm = L.d_item_perm;
         // items of several segments: the cheapest (last) one workgroup-generation of the order
         // runs one segment per workgroup, so the launch does not end on whole long items
         if (kseg > 1 && !p.pass_split && c->n_meshes == 0 && env_int("MCPT_TAIL_PIECES", 1) != 0) {   // (the mesh kernels split items their own way)
@@ -1158,45 +1190,56 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
           p.tail_m = (int)std::min(items / 2, per_cu * c->n_cu);
         }
       }
-      HIP_OR_RETURN(hipMemsetAsync(c->d_item_cost, 0, sizeof(unsigned) * (size_t)items, c->stream));
-      p.item_cost = c->d_item_cost;
+      HIP_OR_RETURN(hipMemsetAsync(L.d_item_cost, 0, sizeof(unsigned) * (size_t)items, ws));
+      p.item_cost = L.d_item_cost;
     }
     if (split_items) {
-      if (!c->d_split_pass) {
-        HIP_OR_RETURN(hipMalloc(&c->d_split_pass, sizeof(float) * 3 * (size_t)kSplitMax * mcpt::kPassChunk *
-                                                      mcpt::kTileThreads));
+      if (!L.d_split_pass) {
+        HIP_OR_RETURN(hipMalloc(&L.d_split_pass, sizeof(float) * 3 * (size_t)kSplitMax * mcpt::kPassChunk *
+                                                     mcpt::kTileThreads));
       }
-      HIP_OR_RETURN(hipMemsetAsync(c->d_split_of, 0xff, sizeof(int) * (size_t)items, c->stream));
-      p.split_of = c->d_split_of;
-      p.split_pass = c->d_split_pass;
+      HIP_OR_RETURN(hipMemsetAsync(L.d_split_of, 0xff, sizeof(int) * (size_t)items, ws));
+      p.split_of = L.d_split_of;
+      p.split_pass = L.d_split_pass;
       p.split_max = kSplitMax;
-      if (p.item_perm) p.split_n = c->d_split_n;
+      if (p.item_perm) p.split_n = L.d_split_n;
     }
-    HIP_OR_RETURN(hipEventRecord(ev_at(c, slot, (int)k, 0), c->stream));
+    // The timed interval of a lane launch that follows one on the other lane starts where that
+    // launch's render ended (recorded on its stream): the launches overlap, and each is charged
+    // its period, not its whole span (which would count the overlapped tails twice)
+    const bool period = lane && c->prev_lane >= 0 && c->prev_lane != li;
+    HIP_OR_RETURN(hipEventRecord(ev_at(c, slot, (int)k, 0), period ? c->lanes[c->prev_lane].stream : ws));
     if (stream) {
       const int st = stream_run(c, p);
       if (st != MCPT_OK) return st;
     } else {
-      HIP_OR_RETURN(mcpt_launch_render(p, count, c->stream));
+      HIP_OR_RETURN(mcpt_launch_render(p, count, ws));
     }
-    HIP_OR_RETURN(hipEventRecord(ev_at(c, slot, (int)k, 1), c->stream));
+    HIP_OR_RETURN(hipEventRecord(ev_at(c, slot, (int)k, 1), ws));
+    if (lane) HIP_OR_RETURN(hipStreamWaitEvent(c->stream, ev_at(c, slot, (int)k, 1), 0));
     HIP_OR_RETURN(mcpt_launch_combine(p, c->stream));
     HIP_OR_RETURN(hipEventRecord(ev_at(c, slot, (int)k, 2), c->stream));
-    if (order && (!p.item_perm || ++c->order_age >= kOrderRefresh)) {
-      // sorted after this launch (outside its timed events); the next launch of this shape
-      // reads the order in stream order, so no host wait
-      size_t tmp = c->sort_tmp_bytes;
-      HIP_OR_RETURN(mcpt_order_items(c->d_item_cost, c->d_cost_sorted, c->d_item_iota, c->d_item_perm, (int)items,
-                                     c->d_sort_tmp, &tmp, c->stream));
+    if (order && (!p.item_perm || ++L.order_age >= kOrderRefresh)) {
+      // sorted after this launch's render (outside its timed events); the lane's next launch of
+      // this shape reads the order in stream order, so no host wait
+      size_t tmp = L.sort_tmp_bytes;
+      HIP_OR_RETURN(mcpt_order_items(L.d_item_cost, L.d_cost_sorted, L.d_item_iota, L.d_item_perm, (int)items,
+                                     L.d_sort_tmp, &tmp, ws));
       // mesh scenes: how many of the costliest to split next time (the mesh kernels run 5
       // waves per SIMD: 20 per CU, in workgroups of tile_w / 8 waves)
       if (c->n_meshes > 0)
-        HIP_OR_RETURN(mcpt_split_count(c->d_cost_sorted, (int)items, 20 / (p.tile_w / 8) * c->n_cu, kSplitMax, c->d_split_n,
-                                       c->d_events + kDebugSplitSlot, c->stream));
-      std::copy(key, key + 8, c->order_key);
-      c->order_valid = true;
-      c->order_age = 0;
+        HIP_OR_RETURN(mcpt_split_count(L.d_cost_sorted, (int)items, 20 / (p.tile_w / 8) * c->n_cu, kSplitMax, L.d_split_n,
+                                       c->d_events + kDebugSplitSlot, ws));
+      std::copy(key, key + 8, L.order_key);
+      L.order_valid = true;
+      L.order_age = 0;
     }
+    if (lane) {   // `stream` stays ordered after all of the lane's work
+      HIP_OR_RETURN(hipEventRecord(L.tail, L.stream));
+      HIP_OR_RETURN(hipStreamWaitEvent(c->stream, L.tail, 0));
+    }
+    HIP_OR_RETURN(hipEventRecord(L.freed, c->stream));
+    c->prev_lane = lane ? li : -1;
 #ifdef MCPT_CHECKED
     {
       // checked build: the sub-launch (render, combine, order sort) is waited for here, so a fault
@@ -1520,6 +1563,15 @@ int mcpt_set_stream_pool(mcpt_ctx* c, int slots, int refill) {
 int mcpt_stream_iterations(mcpt_ctx* c, long long* iterations) {
   if (!c || !iterations) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
   *iterations = c->stream_iters;
+  return MCPT_OK;
+}
+
+int mcpt_set_render_lanes(mcpt_ctx* c, int on) {
+  if (!c) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
+  HIP_OR_RETURN(hipSetDevice(c->device));
+  HIP_OR_RETURN(hipStreamSynchronize(c->stream));   // (ordered after every lane's work)
+  c->overlap = on ? 1 : 0;
+  c->prev_lane = -1;
   return MCPT_OK;
 }
 

@@ -105,6 +105,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "mcpt_set_leaf_batch": (i, [_vp, i]),
         "mcpt_get_leaf_batch": (i, [_vp, ip]),
         "mcpt_set_partial_budget": (i, [_vp, ctypes.c_size_t]),
+        "mcpt_set_render_lanes": (i, [_vp, i]),
         "mcpt_set_stream_pool": (i, [_vp, i, i]),
         "mcpt_stream_iterations": (i, [_vp, ctypes.POINTER(ctypes.c_longlong)]),
         "mcpt_last_launch_count": (i, [_vp, ip]),
@@ -659,6 +660,11 @@ class Renderer:
         """mcpt_set_partial_budget: bound of one launch's segment-sum buffer (calls spanning more
         32-pass chunks are split into launches at chunk boundaries; same bits)."""
         _check(lib().mcpt_set_partial_budget(self._h, int(nbytes)), "mcpt_set_partial_budget")
+
+    def set_render_lanes(self, on: bool) -> None:
+        """mcpt_set_render_lanes: consecutive launches on two alternating lanes (overlapping each
+        other's tails; the default) or every launch in order on the context's stream."""
+        _check(lib().mcpt_set_render_lanes(self._h, int(bool(on))), "mcpt_set_render_lanes")
 
     def last_launch_count(self) -> int:
         """Sub-launches the last render call was split into."""

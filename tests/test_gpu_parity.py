@@ -579,3 +579,44 @@ def test_tail_pieces_same_bits(mcpt_mod, renderer, monkeypatch, scene_id, traver
     monkeypatch.setenv("MCPT_ITEM_ORDER", "0")
     plain = _gpu(mcpt_mod, renderer, scene_id, W, H, 1, 384, B, split=[128, 128, 128], traversal=traversal)
     assert np.array_equal(ordered.view(np.uint32), plain.view(np.uint32))
+
+
+@pytest.mark.parametrize("scene_id,B,traversal", [(6, 8, 1), (8, 12, 1), (3, 8, 2), (0, 8, 1)])
+def test_render_lanes_same_bits(mcpt_mod, monkeypatch, scene_id, B, traversal):
+    """Render lanes (round 6): once the schedule is settled, consecutive launches alternate between
+    two lanes (streams, segment-sum buffers, work-item order state), each render starting while
+    the previous one's last workgroups run; the combines stay in call order.  Four 96-pass calls,
+    then one 384-pass call cut into four sub-launches by a small segment-sum budget (lanes
+    alternate inside a call), equal the same calls with the lanes off (MCPT_OVERLAP=0, every launch
+    in order on one stream), bit for bit.  Scene 0: the mesh workload (split items per lane)."""
+    W, H = (960, 540) if scene_id else (1920, 1080)
+    if scene_id == 0:
+        from mcpt import meshes
+        sc = meshes.big_mesh_scene(1_000_000)[0]
+    else:
+        sc = mcpt_mod.Scene.reference(scene_id)
+    ipv, iv = mcpt_mod.camera_canonical(W, H)
+    out = {}
+    for ov in ("1", "0"):
+        monkeypatch.setenv("MCPT_OVERLAP", ov)
+        r = mcpt_mod.Renderer(0)
+        try:
+            r.set_traversal(traversal)
+            r.upload_scene(sc)
+            r.set_target(W, H)
+            p = 1
+            for _ in range(4):
+                r.render(ipv, iv, p, 96, 0.0, B, 1.0, 0)
+                p += 96
+            a, n = r.read_accum()
+            r.clear_accum()
+            r.set_partial_budget(W * H * 12 * 3)   # three segments per sub-launch
+            r.render(ipv, iv, 1, 384, 0.0, B, 1.0, 0)
+            launches = r.last_launch_count()
+            b, n2 = r.read_accum()
+        finally:
+            r.close()
+        assert n == 384 and n2 == 384 and launches == 4
+        out[ov] = (a, b)
+    for k in range(2):
+        assert np.array_equal(out["1"][k].view(np.uint32), out["0"][k].view(np.uint32)), (scene_id, k)

@@ -7,7 +7,10 @@ from the moment the running-wave count falls below 90 % of its peak for good to 
 each XCD group's (blockIdx % 8) last end.
 
     MCPT_LIB=montecarlo-pathtracing_amd/mcpt/variants/libmcpt_blocktimes.so \\
-        python tools/blocktimes.py [c2] [c4] [mesh] [--seg K] [--auto]
+        python tools/blocktimes.py [c2] [c4] [mesh] [--seg K] [--auto] [--shard N]
+
+--shard N: rank 0's shard of an N-GPU strong run (mcpt_balanced_rows, 8-row bands) instead of the
+whole frame.
 """
 import ctypes
 import json
@@ -73,7 +76,12 @@ def main():
             r.upload_scene(meshes.big_mesh_scene(1_000_000)[0])
         else:
             r.upload_scene(mcpt.Scene.reference(sid))
-        r.set_target(W, H)
+        shard = int(sys.argv[sys.argv.index("--shard") + 1]) if "--shard" in sys.argv else 1
+        if shard > 1:
+            from mcpt.dist import local_rows
+            r.set_target_rows(W, H, local_rows(H, 8, shard, 0, "balanced"))
+        else:
+            r.set_target(W, H)
         auto = "--auto" in sys.argv
         r.set_traversal(mcpt.TRAVERSAL_AUTO if auto else mcpt.TRAVERSAL_LANE)
         if seg:
@@ -89,7 +97,7 @@ def main():
         sched = r.schedule()
         t = np.frombuffer(buf, dtype=np.uint64)
         res = {"workload": name, "scene": sid, "spp": S, "bounces": B, "seg_per_item_env": seg or None,
-               "traversal": "AUTO" if auto else "LANE", "schedule": sched}
+               "traversal": "AUTO" if auto else "LANE", "schedule": sched, "shard_of": shard}
         res.update(analyse(t, waves_per_item=1 if sid == 0 else 2))   # waves per workgroup (tile_w_for; records by workgroup)
         print(json.dumps(res), flush=True)
         r.close()

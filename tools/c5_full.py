@@ -3,8 +3,9 @@
 shards of an 8-GPU run (the balanced partition bench.py uses, mcpt_balanced_rows), each rendered on this GPU as ONE mcpt_render call of 84,000 passes
 (the library cuts it into chunk-aligned launches within its segment-sum budget).
 
-Whole frame (round 6, verdict r05 #6): the 3840x2160 frame as ONE mcpt_render call of 84,000
-passes on this GPU — the measured one-GPU time to target — and `--oracle-pixels` pixels of its
+Whole frame (round 6, verdict r05 #6): the 3840x2160 frame accumulated progressively in 1,024-pass
+calls (C5's step) up to 84,000 passes on this GPU — the measured one-GPU time to target — and
+`--oracle-pixels` pixels of its
 accumulator checked bit for bit against the CPU oracle's sums of the same 84,000 passes
 (oracle.render_pixels, the chunked accumulation contract), so the last passes are covered too.
 
@@ -42,37 +43,41 @@ def main():
     ap.add_argument("--traversal", type=int, default=0, help="0 AUTO (trials on 256-pass launches), 1 lane, 2 wave")
     ap.add_argument("--seg-per-item", type=int, default=0, help="> 0: MCPT_SEG_PER_ITEM for every launch")
     ap.add_argument("--no-whole", action="store_true", help="skip the whole-frame one-GPU run")
+    ap.add_argument("--step", type=int, default=1024, help="whole frame: passes per progressive call (C5's step)")
+    ap.add_argument("--one-call", action="store_true", help="whole frame: one call of all the passes")
     ap.add_argument("--oracle-pixels", type=int, default=256, help="whole-frame pixels checked against the oracle")
     a = ap.parse_args()
     if a.seg_per_item > 0:
         os.environ["MCPT_SEG_PER_ITEM"] = str(a.seg_per_item)
-    r = mcpt.Renderer(0)
-    r.set_traversal(a.traversal)
-    r.upload_scene(mcpt.Scene.reference(6))
     ipv, iv = mcpt.camera_canonical(W, H)
-    r.set_target_rows(W, H, local_rows(H, BAND, WORLD, 0, "balanced"))
-    # AUTO traversal trials on this launch shape first (same bits either way)
-    for _ in range(mcpt.AUTO_TRIALS):
-        r.render(ipv, iv, 1, 256, 0.0, B, 1.0, 0)
     whole = None
     if not a.no_whole:
-        # the whole frame in one call: the one-GPU time to target, measured
+        # the whole frame on this GPU, as C5 defines it: progressive accumulation in calls of
+        # `--step` passes (bench.py --config c5's step) up to the target — the one-GPU time to target,
+        # measured (with --one-call: ONE call of all the passes instead)
+        r = mcpt.Renderer(0)   # its own context: AUTO settles on this target's launches
+        r.set_traversal(a.traversal)
+        r.upload_scene(mcpt.Scene.reference(6))
         r.set_target(W, H)
-        for _ in range(mcpt.AUTO_TRIALS):   # AUTO's trials on this target's 256-pass launches
-            r.render(ipv, iv, 1, 256, 0.0, B, 1.0, 0)
+        step = a.passes if a.one_call else a.step
+        for _ in range(mcpt.AUTO_TRIALS):   # AUTO's trials on this target's step-sized launches
+            r.render(ipv, iv, 1, min(step, 1024), 0.0, B, 1.0, 0)
         r.clear_accum()
         r.synchronize()
         t0 = time.perf_counter()
-        r.render(ipv, iv, 1, a.passes, 0.0, B, 1.0, 0)
+        p, calls = 1, 0
+        while p <= a.passes:
+            k = min(step, a.passes - p + 1)
+            r.render(ipv, iv, p, k, 0.0, B, 1.0, 0)
+            p += k
+            calls += 1
         r.synchronize()
         wall = time.perf_counter() - t0
-        kms, cms = r.last_kernel_ms()
         acc, n = r.read_accum()
         assert n == a.passes and np.isfinite(acc).all()
         whole = {"config": "C5", "whole_frame": True, "width": W, "height": H, "spp": a.passes, "bounces": B,
-                 "launches": r.last_launch_count(), "kernel_ms": round(kms, 1), "combine_ms": round(cms, 2),
-                 "time_to_target_s": round(wall, 3), "msamples_s_wall": round(W * H * a.passes / wall / 1e6, 1),
-                 "schedule": r.schedule(),
+                 "calls": calls, "passes_per_call": step, "time_to_target_s": round(wall, 3),
+                 "msamples_s_wall": round(W * H * a.passes / wall / 1e6, 1), "schedule": r.schedule(),
                  "mean_radiance": [round(float(v), 5) for v in (acc.reshape(-1, 3).mean(0) / a.passes)]}
         if a.oracle_pixels > 0:
             sys.path.insert(0, REPO)
@@ -92,6 +97,14 @@ def main():
                                      "oracle_s": round(time.perf_counter() - t1, 1),
                                      "pixels_seed": 84000}
         print(json.dumps(whole), flush=True)
+        r.close()
+    r = mcpt.Renderer(0)
+    r.set_traversal(a.traversal)
+    r.upload_scene(mcpt.Scene.reference(6))
+    r.set_target_rows(W, H, local_rows(H, BAND, WORLD, 0, "balanced"))
+    # AUTO traversal trials on this launch shape first (same bits either way)
+    for _ in range(mcpt.AUTO_TRIALS):
+        r.render(ipv, iv, 1, 256, 0.0, B, 1.0, 0)
     shard_ms = []
     for rank in a.ranks:
         r.set_target_rows(W, H, local_rows(H, BAND, WORLD, rank, "balanced"))

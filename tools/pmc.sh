@@ -6,7 +6,8 @@ OUT=$1; shift
 export TMPDIR=/tmp
 mkdir -p "$OUT"
 # warm-up steps; the summary reads the timed step's launch (bench.py runs AUTO's timing trials first)
-ARGS="--steps 1 --warmup 2 --no-cpu-baseline --no-count --no-check $*"
+# (PMC_STEPS timed steps: pmc_summary.py --calls=PMC_STEPS averages their launches)
+ARGS="--steps ${PMC_STEPS:-1} --warmup 2 --no-cpu-baseline --no-count --no-check $*"
 run() {  # name counters...
   local name=$1; shift
   timeout -k 10 300 rocprofv3 --pmc "$@" --kernel-trace -d "$OUT/$name" -o run --output-format csv -- python3 bench.py $ARGS > "$OUT/$name.log" 2>&1

@@ -8,7 +8,7 @@ scene records served from L2, so the read side is tiny either way).  The SQ coun
 give the VALU issue picture (SQ_* wave counters are quad-cycle units; GRBM_GUI_ACTIVE is
 summed over the 8 XCDs).
 
-    python tools/pmc_summary.py gpurun_out/<run>/pmc <workload> profiles/pmc_records.json [--launches=K]
+    python tools/pmc_summary.py gpurun_out/<run>/pmc <workload> profiles/pmc_records.json [--launches=K] [--calls=N]
 
 The record carries the sha256 of the libmcpt.so that was profiled; bench.py uses a record only
 for that exact build (records of other builds are dropped from the file on merge).
@@ -26,7 +26,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(REPO, "montecarlo-pathtracing_amd", "mcpt", "libmcpt.so")
 
 
-def load(d, launches=1):
+def load(d, launches=1, calls=1):
     """Counters of the timed step's path-tracing launches in each pass, summed: the LAST
     `launches` dispatches (earlier ones are warm-up, including AUTO's timing trials).  A render
     call spanning more pass segments than the segment-sum budget holds runs as several
@@ -43,24 +43,28 @@ def load(d, launches=1):
                     float(r["Counter_Value"])
                 names[k] = r["Kernel_Name"]
         if per_dispatch:
-            last = sorted(per_dispatch)[-launches:]
+            # the last `calls` timed calls of `launches` dispatches each, averaged per call (the
+            # work-item order's tail pieces make a call's instruction count vary by a few %)
+            last = sorted(per_dispatch)[-launches * calls:]
             summed = collections.defaultdict(float)
             for k in last:
                 for n, v in per_dispatch[k].items():
-                    summed[n] += v
+                    summed[n] += v / calls
             out.update(summed)
             out["_kernel"] = names[last[-1]]
     return out
 
 
 def main():
-    args = [a for a in sys.argv[1:] if not a.startswith("--launches")]
-    launches = 1
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    launches, calls = 1, 1
     for a in sys.argv[1:]:
         if a.startswith("--launches="):
             launches = int(a.split("=", 1)[1])
+        if a.startswith("--calls="):
+            calls = int(a.split("=", 1)[1])
     d, workload, out = args[0], args[1], args[2]
-    c = load(d, launches)
+    c = load(d, launches, calls)
     kernel = c.pop("_kernel", "mcpt::render_kernel<false, *>")
     fetch_b = c["FETCH_SIZE"] * 1024 * 2          # gfx950: FETCH_SIZE = half the bytes
     write_b = c["WRITE_SIZE"] * 1024
@@ -70,6 +74,7 @@ def main():
         "kernel": kernel,
         "source": f"rocprofv3 --pmc passes of tools/pmc.sh ({os.path.basename(d.rstrip('/'))})",
         "launches_summed": launches,
+        "calls_averaged": calls,
         "hbm_bytes_per_launch": fetch_b + write_b,
         "fetch_bytes_per_launch_corrected": fetch_b,
         "write_bytes_per_launch": write_b,
