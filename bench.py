@@ -666,9 +666,9 @@ def run_point(args, sr, rough, S, world, barrier, stat_dev, wd):
         e1.record(stream)
         gather_ev.append((e0, e1))
         if (k - args.warmup + 1) % half == 0:
-            kernel_ms.extend(sr.r.kernel_ms_back(b) for b in reversed(range(half)))
+            kernel_ms.extend(sr.r.kernel_ms_back(b) + (sr.r.kernel_span_ms_back(b),) for b in reversed(range(half)))
     barrier()
-    kernel_ms.extend(sr.r.kernel_ms_back(b) for b in reversed(range(args.steps % half)))
+    kernel_ms.extend(sr.r.kernel_ms_back(b) + (sr.r.kernel_span_ms_back(b),) for b in reversed(range(args.steps % half)))
     elapsed = time.perf_counter() - t0
     wd.enter("stats")
     sched = sr.r.schedule()   # what AUTO picked for this rank's timed launches
@@ -685,8 +685,9 @@ def run_point(args, sr, rough, S, world, barrier, stat_dev, wd):
     if not args.no_count:
         ev_local = sr.r.render_counted(ipv, iv, args.warmup * S + 1, S, 0.0, B, args.ior, mcpt.MONTECARLO)
     bytes_local = float((ev_local.astype(np.float64) * mcpt.Renderer.event_bytes()).sum())
-    avg_trace_ms = float(np.mean([a for a, _ in kernel_ms]))
-    avg_combine_ms = float(np.mean([b for _, b in kernel_ms]))
+    avg_trace_ms = float(np.mean([a for a, _, _ in kernel_ms]))
+    avg_combine_ms = float(np.mean([b for _, b, _ in kernel_ms]))
+    avg_span_ms = float(np.mean([c for _, _, c in kernel_ms]))
     props = torch.cuda.get_device_properties(sr.device)
     stats = torch.tensor([bytes_local, avg_trace_ms, avg_combine_ms, float(ev_local[6]), gather_ms,
                           float(sr.g.n_local), float(props.pci_domain_id), float(props.pci_bus_id),
@@ -702,6 +703,7 @@ def run_point(args, sr, rough, S, world, barrier, stat_dev, wd):
     if args.rank == 0 and not args.no_check:
         check = self_check(args, scene, ipv, iv, frame, args.warmup + args.steps, S, args.local_rank)
     return dict(rough=rough, elapsed=elapsed, sched=sched, launches=launches, gather_ms=gather_ms, avg_trace_ms=avg_trace_ms,
+                avg_span_ms=avg_span_ms,
                 avg_combine_ms=avg_combine_ms, allstats=allstats, check=check, scene=scene,
                 events={n: int(v) for n, v in zip(mcpt.EVENT_NAMES, ev_local)})
 
@@ -874,6 +876,11 @@ def main():
                     "deterministic RNG seeds)",
             "config": config,
             "kernel_ms": {"trace_avg": round(main_pt["avg_trace_ms"], 3),
+                          # render lanes: consecutive launches overlap; trace_avg is
+                          # each launch's period (previous render end -> its end, what the roofline
+                          # divides by), span_avg its own start -> end (what a profiler's kernel
+                          # duration shows, the overlapped tails counted twice)
+                          "span_avg": round(main_pt["avg_span_ms"], 3),
                           "combine_avg": round(main_pt["avg_combine_ms"], 3),
                           "gather_avg": round(main_pt["gather_ms"], 3),
                           "per_rank_trace_avg": [round(float(x), 3) for x in a[:, 1]],

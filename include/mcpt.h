@@ -313,6 +313,12 @@ int mcpt_last_kernel_ms(mcpt_ctx* ctx, float* trace_ms, float* combine_ms);
  * events of its last 64 calls, so a caller can queue a run of calls and read their times
  * afterwards without waiting after each (waits for that call only). */
 int mcpt_kernel_ms_back(mcpt_ctx* ctx, int back, float* trace_ms, float* combine_ms);
+/* The path-tracing kernel's whole span (its own start on its stream -> its end), summed over the
+ * call's sub-launches, for the call `back` calls before the last (waits for it).  With render lanes
+ * (mcpt_set_render_lanes) consecutive launches overlap, and mcpt_kernel_ms_back charges each its
+ * period (from the previous launch's render end); the span also counts the overlapped tail, as a
+ * profiler's kernel duration does. */
+int mcpt_kernel_span_ms_back(mcpt_ctx* ctx, int back, float* span_ms);
 
 /* ---------------------------------------------------------------------------------
  * 2. host scene producer (BVH_GPU_Scene-compatible)

@@ -174,12 +174,16 @@ struct mcpt_ctx {
 };
 
 // events of sub-launch k of the last call: start / mid / stop
-static hipEvent_t ev_start(const mcpt_ctx* c, int k) { return c->evs[c->ring_pos][3 * k]; }
-static hipEvent_t ev_stop(const mcpt_ctx* c, int k) { return c->evs[c->ring_pos][3 * k + 2]; }
+// (4 per sub-launch: 0 the timed interval's start — for a lane launch that follows one on the
+// other lane, that launch's render end —, 1 the render's end, 2 the combine's end, 3 the render's
+// own start on its stream: 3 -> 1 is the kernel's whole span, overlapped tails included)
+constexpr int kEvPerSub = 4;
+static hipEvent_t ev_start(const mcpt_ctx* c, int k) { return c->evs[c->ring_pos][kEvPerSub * k]; }
+static hipEvent_t ev_stop(const mcpt_ctx* c, int k) { return c->evs[c->ring_pos][kEvPerSub * k + 2]; }
 // event i of sub-launch k in ring slot `slot` (0 start, 1 mid, 2 stop)
-static hipEvent_t ev_at(const mcpt_ctx* c, int slot, int k, int i) { return c->evs[slot][3 * k + i]; }
+static hipEvent_t ev_at(const mcpt_ctx* c, int slot, int k, int i) { return c->evs[slot][kEvPerSub * k + i]; }
 static hipError_t ensure_events(mcpt_ctx* c, int slot, int n_sub) {
-  while ((int)c->evs[slot].size() < 3 * n_sub) {
+  while ((int)c->evs[slot].size() < kEvPerSub * n_sub) {
     hipEvent_t e = nullptr;
     hipError_t r = hipEventCreate(&e);
     if (r != hipSuccess) return r;
@@ -194,9 +198,9 @@ static hipError_t slot_launch_ms(const mcpt_ctx* c, int slot, float* trace_ms, f
   const std::vector<hipEvent_t>& v = c->evs[slot];
   for (int k = 0; k < c->ring_n_sub[slot]; ++k) {
     float a = 0.0f, b = 0.0f;
-    hipError_t e = hipEventSynchronize(v[3 * k + 2]);
-    if (e == hipSuccess) e = hipEventElapsedTime(&a, v[3 * k], v[3 * k + 1]);
-    if (e == hipSuccess) e = hipEventElapsedTime(&b, v[3 * k + 1], v[3 * k + 2]);
+    hipError_t e = hipEventSynchronize(v[kEvPerSub * k + 2]);
+    if (e == hipSuccess) e = hipEventElapsedTime(&a, v[kEvPerSub * k], v[kEvPerSub * k + 1]);
+    if (e == hipSuccess) e = hipEventElapsedTime(&b, v[kEvPerSub * k + 1], v[kEvPerSub * k + 2]);
     if (e != hipSuccess) return e;
     *trace_ms += a; *combine_ms += b;
   }
@@ -1007,15 +1011,29 @@ static hipError_t ensure_item_order(mcpt_ctx* c, mcpt_ctx::Lane& L, long long it
   return hipSuccess;
 }
 
-// every render lane's queued work finished (before buffers they use are freed or reallocated)
-static hipError_t sync_lanes(mcpt_ctx* c) {
-  for (auto& L : c->lanes)
-    if (L.stream) {
-      const hipError_t e = hipStreamSynchronize(L.stream);
-      if (e != hipSuccess) return e;
-    }
-  return hipSuccess;
+#ifdef MCPT_CHECKED
+// checked build (mcpt_internal.h, kCheckedCountSlot): wait for sub-launch k of n_sub and report a
+// HIP fault or an out-of-range index the kernels counted, naming the sub-launch and its shape
+static int checked_sub_launch(mcpt_ctx* c, int k, int n_sub, const mcpt::RenderParams& p) {
+  char what[200];
+  std::snprintf(what, sizeof(what),
+                "checked build: sub-launch %d of %d (passes %d+%d, %d segments, %d items, K %d, tail %d, split max %d)",
+                k, n_sub, p.first_pass, p.n_passes, p.n_segments, p.n_items, p.seg_per_item, p.tail_m, p.split_max);
+  hipError_t e = hipStreamSynchronize(c->stream);   // (ordered after the sub-launch's lane work)
+  if (e != hipSuccess) return set_err(MCPT_ERR_HIP, what, e);
+  unsigned long long v[2] = {0, 0};
+  e = hipMemcpy(v, c->d_events + mcpt::kCheckedCountSlot, sizeof(v), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return set_err(MCPT_ERR_HIP, what, e);
+  if (v[0] != 0) {
+    char msg[256];
+    std::snprintf(msg, sizeof(msg), "%s: %llu out-of-range indices, first at site %llu index %lld", what, v[0],
+                  v[1] >> 48, (long long)(v[1] & 0xffffffffffffull));
+    (void)hipMemset(c->d_events + mcpt::kCheckedCountSlot, 0, sizeof(v));
+    return set_err(MCPT_ERR_HIP, msg);
+  }
+  return MCPT_OK;
 }
+#endif
 
 static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_pass, int n_passes, float date,
                   int bounces, float refract_ind, int variant, bool count, unsigned long long* events) {
@@ -1128,7 +1146,7 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   // the AUTO timing read) moves there only once every event of the call has been recorded, so a
   // call that fails part-way leaves the previous call's complete timings in place.
   if (n_sub == 0) {   // no passes: an empty timed interval
-    for (int i = 0; i < 3; ++i) HIP_OR_RETURN(hipEventRecord(ev_at(c, slot, 0, i), c->stream));
+    for (int i = 0; i < kEvPerSub; ++i) HIP_OR_RETURN(hipEventRecord(ev_at(c, slot, 0, i), c->stream));
   }
   for (long long lo = first_pass, end = (long long)first_pass + n_passes, k = 0; lo < end; ++k) {
     const long long c0 = fdiv((int)(lo - 1), mcpt::kPassChunk);
@@ -1209,6 +1227,7 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
     // its period, not its whole span (which would count the overlapped tails twice)
     const bool period = lane && c->prev_lane >= 0 && c->prev_lane != li;
     HIP_OR_RETURN(hipEventRecord(ev_at(c, slot, (int)k, 0), period ? c->lanes[c->prev_lane].stream : ws));
+    HIP_OR_RETURN(hipEventRecord(ev_at(c, slot, (int)k, 3), ws));
     if (stream) {
       const int st = stream_run(c, p);
       if (st != MCPT_OK) return st;
@@ -1660,6 +1679,24 @@ int mcpt_kernel_ms_back(mcpt_ctx* c, int back, float* trace_ms, float* combine_m
     return set_err(MCPT_ERR_INVALID_ARG, "mcpt_kernel_ms_back: no such call in the timing ring");
   HIP_OR_RETURN(hipSetDevice(c->device));
   HIP_OR_RETURN(slot_launch_ms(c, (c->ring_pos - back + kTimingRing) % kTimingRing, trace_ms, combine_ms));
+  return MCPT_OK;
+}
+
+int mcpt_kernel_span_ms_back(mcpt_ctx* c, int back, float* span_ms) {
+  if (!c || !span_ms) return mcpt_err_bare(MCPT_ERR_INVALID_ARG);
+  if (back < 0 || back >= kTimingRing || back >= c->n_timed)
+    return set_err(MCPT_ERR_INVALID_ARG, "mcpt_kernel_span_ms_back: no such call in the timing ring");
+  HIP_OR_RETURN(hipSetDevice(c->device));
+  const int slot = (c->ring_pos - back + kTimingRing) % kTimingRing;
+  const std::vector<hipEvent_t>& v = c->evs[slot];
+  float tot = 0.0f;
+  for (int k = 0; k < c->ring_n_sub[slot]; ++k) {
+    float a = 0.0f;
+    HIP_OR_RETURN(hipEventSynchronize(v[kEvPerSub * k + 1]));
+    HIP_OR_RETURN(hipEventElapsedTime(&a, v[kEvPerSub * k + 3], v[kEvPerSub * k + 1]));
+    tot += a;
+  }
+  *span_ms = tot;
   return MCPT_OK;
 }
 

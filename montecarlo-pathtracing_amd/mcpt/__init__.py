@@ -115,6 +115,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "mcpt_last_render_ms": (i, [_vp, fp]),
         "mcpt_last_kernel_ms": (i, [_vp, fp, fp]),
         "mcpt_kernel_ms_back": (i, [_vp, ctypes.c_int, fp, fp]),
+        "mcpt_kernel_span_ms_back": (i, [_vp, ctypes.c_int, fp]),
         "mcpt_scene_create": (i, [ctypes.POINTER(_vp)]),
         "mcpt_scene_destroy": (i, [_vp]),
         "mcpt_scene_clear": (i, [_vp]),
@@ -713,6 +714,14 @@ class Renderer:
 
     # render calls whose kernel times a context keeps (mcpt_kernel_ms_back)
     TIMING_RING = 64
+
+    def kernel_span_ms_back(self, back: int) -> float:
+        """mcpt_kernel_span_ms_back: the path-tracing kernel's whole span (own start -> end) of the
+        call `back` calls before the last; with render lanes the launches overlap, and
+        kernel_ms_back charges each its period instead."""
+        a = ctypes.c_float()
+        _check(lib().mcpt_kernel_span_ms_back(self._h, int(back), ctypes.byref(a)), "mcpt_kernel_span_ms_back")
+        return a.value
 
     def kernel_ms_back(self, back: int) -> Tuple[float, float]:
         """mcpt_kernel_ms_back: (path-tracing ms, combine ms) of the render call `back` calls
