@@ -115,9 +115,17 @@ struct mcpt_ctx {
   // pass segments per work item, and for BVH depth >= 8 per-lane walks with the deep knobs (leaf
   // batch 16, walk exit 40) and 4 (6) or 8 (7, >= 8 segments) segments per item.  (3, the stream
   // schedule, is only run when selected explicitly.)
-  int tune_pending = 0;             // candidate of the launch whose timing is not collected yet
-  double tune_samples = 0.0;        // samples of that launch
-  long long tune_shape[2] = {0, 0};      // (local pixels, passes) of that launch
+  // trial launches whose timing is not collected yet, oldest first: a trial's time is read when the
+  // call after the next one starts, so that consecutive trials overlap on the render lanes as the
+  // settled launches do (its period is then measured as the settled launches' is)
+  struct TunePending {
+    int cand = 0;                   // its candidate
+    double samples = 0.0;           // its samples
+    long long shape[2] = {0, 0};    // its (local pixels, passes)
+    int slot = 0;                   // its timing-ring slot
+  };
+  TunePending pend[2];
+  int n_pend = 0;
   long long meas_shape[2] = {0, 0};      // shape the measurements below were taken on
   int meas_segs = 0;                // pass segments of that shape (which candidates apply)
   double tune_ns[8] = {0.0};       // best ns per sample measured, by candidate (same shape)
@@ -274,19 +282,32 @@ static bool cand_deep_knobs(int cand) { return cand == kCandDeepSeg4 || cand == 
 // picked two- or four-segment items run to run on scene 6, 1-2.5 % apart)
 constexpr int kTuneRounds = 2;
 
+// trials of candidate k issued so far on the measured shape (collected + pending)
+static int tune_issued(const mcpt_ctx* c, int k) {
+  int n = c->tune_cnt[k];
+  for (int i = 0; i < c->n_pend; ++i) n += c->pend[i].cand == k ? 1 : 0;
+  return n;
+}
+
 // schedule candidate of the next launch (`segs`: its pass segments)
 static int resolve_candidate(const mcpt_ctx* c, long long segs) {
   if (c->traversal != MCPT_TRAVERSAL_AUTO) return c->traversal;
   if (c->tune_choice) return c->tune_choice;
-  // next trial: in the current round (the fewest trials of any applicable candidate), the
-  // first candidate of the round's order not yet timed that often on the measured shape
+  // next trial: in the current round (the fewest issued trials of any applicable candidate), the
+  // first candidate of the round's order not yet tried that often on the measured shape
   int round = kTuneRounds;
   for (int k = 1; k <= kCandLast; ++k)
-    if (cand_applies(c, k, segs)) round = std::min(round, c->tune_cnt[k]);
-  if (round >= kTuneRounds) return MCPT_TRAVERSAL_LANE;
+    if (cand_applies(c, k, segs)) round = std::min(round, tune_issued(c, k));
+  if (round >= kTuneRounds) {   // every trial issued, the last ones not collected yet: the best so far
+    int best = MCPT_TRAVERSAL_LANE;
+    for (int k = 1; k <= kCandLast; ++k)
+      if (cand_applies(c, k, segs) && c->tune_cnt[k] > 0 && (c->tune_cnt[best] == 0 || c->tune_ns[k] < c->tune_ns[best]))
+        best = k;
+    return best;
+  }
   for (int i = 0; i < kCandLast; ++i) {
     const int k = (round % 2 == 0) ? 1 + i : kCandLast - i;
-    if (cand_applies(c, k, segs) && c->tune_cnt[k] == round) return k;
+    if (cand_applies(c, k, segs) && tune_issued(c, k) == round) return k;
   }
   return MCPT_TRAVERSAL_LANE;
 }
@@ -295,43 +316,49 @@ static int resolve_traversal(const mcpt_ctx* c) { return cand_traversal(resolve_
 
 static void reset_tuning(mcpt_ctx* c) {
   for (auto& L : c->lanes) L.order_valid = false;   // a new scene / target: item costs start over
-  c->tune_pending = 0;
-  c->tune_samples = 0.0;
-  c->tune_shape[0] = c->tune_shape[1] = c->meas_shape[0] = c->meas_shape[1] = 0;
+  c->n_pend = 0;
+  c->meas_shape[0] = c->meas_shape[1] = 0;
   c->meas_segs = 0;
   for (double& t : c->tune_ns) t = 0.0;
   for (int& n : c->tune_cnt) n = 0;
   c->tune_choice = 0;
 }
 
-// collect the timing of the last trial launch (waits for it), decide once both are measured
-static hipError_t collect_tuning(mcpt_ctx* c) {
-  if (!c->tune_pending || !c->timed) return hipSuccess;
-  float ms = 0.0f, ms_combine = 0.0f;
-  hipError_t e = sub_launch_ms(c, &ms, &ms_combine);
-  if (e != hipSuccess) return e;
-  // per-sample times are compared only between launches of the same shape (pixels, passes):
-  // a launch of another shape restarts the comparison
-  if (c->tune_shape[0] != c->meas_shape[0] || c->tune_shape[1] != c->meas_shape[1]) {
-    for (double& t : c->tune_ns) t = 0.0;
-    for (int& n : c->tune_cnt) n = 0;
-    c->meas_shape[0] = c->tune_shape[0];
-    c->meas_shape[1] = c->tune_shape[1];
+// collect the timing of the oldest pending trial (waits for it) while more than `keep` are
+// pending; decide once every applicable candidate is measured kTuneRounds times
+static hipError_t collect_tuning(mcpt_ctx* c, int keep) {
+  while (c->n_pend > keep) {
+    const mcpt_ctx::TunePending t0 = c->pend[0];
+    for (int i = 1; i < c->n_pend; ++i) c->pend[i - 1] = c->pend[i];
+    c->n_pend--;
+    float ms = 0.0f, ms_combine = 0.0f;
+    hipError_t e = slot_launch_ms(c, t0.slot, &ms, &ms_combine);
+    if (e != hipSuccess) return e;
+    // per-sample times are compared only between launches of the same shape (pixels, passes):
+    // a launch of another shape restarts the comparison
+    if (t0.shape[0] != c->meas_shape[0] || t0.shape[1] != c->meas_shape[1]) {
+      for (double& t : c->tune_ns) t = 0.0;
+      for (int& n : c->tune_cnt) n = 0;
+      c->meas_shape[0] = t0.shape[0];
+      c->meas_shape[1] = t0.shape[1];
+    }
+    const double ns = (double)ms * 1e6 / t0.samples;
+    const int k0 = t0.cand;
+    c->tune_ns[k0] = (c->tune_cnt[k0] == 0) ? ns : std::min(c->tune_ns[k0], ns);
+    c->tune_cnt[k0]++;
+    const double* t = c->tune_ns;
+    bool all = true;
+    int best = MCPT_TRAVERSAL_LANE;
+    for (int k = 1; k <= kCandLast; ++k) {
+      if (!cand_applies(c, k, c->meas_segs)) continue;
+      if (c->tune_cnt[k] < kTuneRounds) all = false;
+      else if (t[k] < t[best]) best = k;
+    }
+    if (all) {
+      c->tune_choice = best;
+      c->n_pend = 0;   // (trials of another shape still pending are dropped with the decision)
+    }
   }
-  const double ns = (double)ms * 1e6 / c->tune_samples;
-  const int k0 = c->tune_pending;
-  c->tune_ns[k0] = (c->tune_cnt[k0] == 0) ? ns : std::min(c->tune_ns[k0], ns);
-  c->tune_cnt[k0]++;
-  c->tune_pending = 0;
-  const double* t = c->tune_ns;
-  bool all = true;
-  int best = MCPT_TRAVERSAL_LANE;
-  for (int k = 1; k <= kCandLast; ++k) {
-    if (!cand_applies(c, k, c->meas_segs)) continue;
-    if (c->tune_cnt[k] < kTuneRounds) all = false;
-    else if (t[k] < t[best]) best = k;
-  }
-  if (all) c->tune_choice = best;
   return hipSuccess;
 }
 constexpr double kTuneMinSamples = 1 << 24;   // launches smaller than this are not timed
@@ -399,7 +426,11 @@ int mcpt_create(int device_ordinal, mcpt_ctx** out) {
   if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device_ordinal) != hipSuccess ||
       c->n_cu <= 0)
     c->n_cu = 256;
-  hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+  // the context's own stream (combines, copies) at the device's greatest priority: with render
+  // lanes its short kernels are dispatched ahead of the next render's waiting workgroups
+  int prio_least = 0, prio_greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) prio_greatest = 0;
+  hipError_t e = hipStreamCreateWithPriority(&c->own_stream, hipStreamNonBlocking, prio_greatest);
   for (auto& L : c->lanes) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&L.freed, hipEventDisableTiming);
@@ -1059,7 +1090,14 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   }
   p.minfo = c->d_minfo; p.mpairs = c->d_mpairs; p.mleaftris = c->d_mleaftris; p.mtris = c->d_mtris;
   p.mverts = c->d_mverts; p.mnorms = c->d_mnorms; p.n_meshes = c->n_meshes; p.flat_face = c->flat_face;
-  HIP_OR_RETURN(collect_tuning(c));
+  {
+    // AUTO: the trial before the last call is collected now (its render has ended while the last
+    // call's runs); all of them first when this call's shape differs from theirs
+    const long long px = (long long)c->n_local_rows * c->W;
+    bool other = false;
+    for (int i = 0; i < c->n_pend; ++i) other |= c->pend[i].shape[0] != px || c->pend[i].shape[1] != n_passes;
+    HIP_OR_RETURN(collect_tuning(c, (other || count) ? 0 : 1));
+  }
   // (the counting build is not timed: AUTO counts with the per-lane walk)
   p.tile_w = mcpt::tile_w_for(c->n_meshes > 0, p.lds_scene_bytes);
   p.n_tiles = ((c->W + p.tile_w - 1) / p.tile_w) * ((c->n_local_rows + mcpt::kTileH - 1) / mcpt::kTileH);
@@ -1137,9 +1175,9 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   }
   const int slot = (c->ring_pos + 1) % kTimingRing;   // this call's events (ring of calls)
   HIP_OR_RETURN(ensure_events(c, slot, std::max(n_sub, 1)));
-  // lane launches (mcpt_ctx::Lane): once AUTO has settled (its trials are timed one at a time)
-  const bool lanes_ok = c->overlap != 0 && !count && !stream &&
-                        (c->traversal != MCPT_TRAVERSAL_AUTO || c->tune_choice != 0);
+  // lane launches (mcpt_ctx::Lane); AUTO's trials run on them too (each trial's period is read
+  // one call later, collect_tuning)
+  const bool lanes_ok = c->overlap != 0 && !count && !stream;
   if (count) HIP_OR_RETURN(hipMemsetAsync(c->d_events, 0, sizeof(unsigned long long) * mcpt::EV_COUNT, c->stream));
   const double samples = (double)p.n_local_px * n_passes;
   // The call's events go to ring slot `slot`; the ring position (what mcpt_last_render_ms and
@@ -1235,7 +1273,11 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
       HIP_OR_RETURN(mcpt_launch_render(p, count, ws));
     }
     HIP_OR_RETURN(hipEventRecord(ev_at(c, slot, (int)k, 1), ws));
-    if (lane) HIP_OR_RETURN(hipStreamWaitEvent(c->stream, ev_at(c, slot, (int)k, 1), 0));
+    if (lane) {   // the combine after the render; (the period's start too, so that the events a
+                  // caller reads once the combine's end has completed are all complete)
+      HIP_OR_RETURN(hipStreamWaitEvent(c->stream, ev_at(c, slot, (int)k, 1), 0));
+      if (period) HIP_OR_RETURN(hipStreamWaitEvent(c->stream, ev_at(c, slot, (int)k, 0), 0));
+    }
     HIP_OR_RETURN(mcpt_launch_combine(p, c->stream));
     HIP_OR_RETURN(hipEventRecord(ev_at(c, slot, (int)k, 2), c->stream));
     if (order && (!p.item_perm || ++L.order_age >= kOrderRefresh)) {
@@ -1269,12 +1311,14 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
 #endif
     lo = hi;
   }
-  if (!count && c->traversal == MCPT_TRAVERSAL_AUTO && !c->tune_choice && samples >= kTuneMinSamples) {
+  if (!count && c->traversal == MCPT_TRAVERSAL_AUTO && !c->tune_choice && samples >= kTuneMinSamples && c->n_pend < 2) {
     if (p.n_local_px != c->meas_shape[0] || n_passes != c->meas_shape[1]) c->meas_segs = (int)total_seg;
-    c->tune_pending = cand;
-    c->tune_samples = samples;
-    c->tune_shape[0] = p.n_local_px;
-    c->tune_shape[1] = n_passes;
+    mcpt_ctx::TunePending& t = c->pend[c->n_pend++];
+    t.cand = cand;
+    t.samples = samples;
+    t.shape[0] = p.n_local_px;
+    t.shape[1] = n_passes;
+    t.slot = slot;
   }
   c->n_sub = std::max(n_sub, 1);
   c->ring_pos = slot;

@@ -33,8 +33,10 @@ __all__ = [
 MONTECARLO, MAT, MAT_TR = 0, 1, 2
 TRAVERSAL_AUTO, TRAVERSAL_LANE, TRAVERSAL_WAVE, TRAVERSAL_STREAM = 0, 1, 2, 3
 # launches of one shape AUTO spends on its timing trials before it settles (up to five candidate
-# schedules, each timed twice: mcpt_capi.hip kTuneRounds); callers that measure run these first
-AUTO_TRIALS = 10
+# schedules, each timed twice: mcpt_capi.hip kTuneRounds; a trial's time is read when the call
+# after the next one starts, so the decision comes two calls after the last trial); callers that
+# measure run these first
+AUTO_TRIALS = 12
 EVENT_NAMES = ("node", "leaf", "prim", "cand", "geom", "colmat", "sample", "trav", "mesh", "tri", "mgeom")
 # key bindings of montecarlo.cpp:251-290: scene id -> key
 SCENE_KEYS = {1: "Q", 2: "W", 3: "E", 4: "R", 5: "T", 6: "Y", 7: "U", 8: "I"}

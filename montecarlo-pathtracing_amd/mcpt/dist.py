@@ -140,7 +140,9 @@ class ShardedRenderer:
         # ordered on ONE stream: a torch stream created here and handed to the library.  (Handing
         # over torch's default stream, handle 0, would leave the library on its own non-blocking
         # stream, and the gather would read the send buffer before the copy landed.)
-        self.stream = torch.cuda.Stream(self.device)
+        # (the greatest priority: with the library's render lanes, the combines and the gather on
+        # this stream are dispatched ahead of the next render's waiting workgroups)
+        self.stream = torch.cuda.Stream(self.device, priority=torch.cuda.Stream.priority_range()[1])
         self.r.set_stream(self.stream.cuda_stream)
         if partition == "bands":
             self.r.set_target(W, H, band_rows, world, rank)

@@ -49,7 +49,7 @@ def main():
         else:
             r.set_target(W, H)
         ipv, iv = mcpt.camera_canonical(W, H)
-        for _ in range(mcpt.AUTO_TRIALS):   # AUTO settles (lanes are used once it has)
+        for _ in range(mcpt.AUTO_TRIALS):   # AUTO settles
             r.render(ipv, iv, 1, S, 0.0, B, 1.0, 0)
         p = 1
         ms = {1: [], 0: []}
