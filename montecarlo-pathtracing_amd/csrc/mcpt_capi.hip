@@ -1175,9 +1175,12 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   }
   const int slot = (c->ring_pos + 1) % kTimingRing;   // this call's events (ring of calls)
   HIP_OR_RETURN(ensure_events(c, slot, std::max(n_sub, 1)));
-  // lane launches (mcpt_ctx::Lane); AUTO's trials run on them too (each trial's period is read
-  // one call later, collect_tuning)
-  const bool lanes_ok = c->overlap != 0 && !count && !stream;
+  // lane launches (mcpt_ctx::Lane) once AUTO has settled.  (AUTO's trials run in order on
+  // `stream`: on the lanes a trial's period would be charged its own tail and discounted the
+  // previous trial's, which favours the candidates with short items — C2 / C5 picked two segments
+  // per item where four are 3 % faster on the lanes, tools/seg_ab.py, profiles/r06_seg_ab.jsonl)
+  const bool lanes_ok = c->overlap != 0 && !count && !stream &&
+                        (c->traversal != MCPT_TRAVERSAL_AUTO || c->tune_choice != 0);
   if (count) HIP_OR_RETURN(hipMemsetAsync(c->d_events, 0, sizeof(unsigned long long) * mcpt::EV_COUNT, c->stream));
   const double samples = (double)p.n_local_px * n_passes;
   // The call's events go to ring slot `slot`; the ring position (what mcpt_last_render_ms and
@@ -1233,6 +1236,24 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
     p.partial = L.d_partial;
     if (order) HIP_OR_RETURN(ensure_item_order(c, L, items));
     if (lane) HIP_OR_RETURN(hipStreamWaitEvent(L.stream, L.freed, 0));
+    if (order && !(L.order_valid && std::equal(key, key + 8, L.order_key))) {
+      // the other lane holds this shape's order (AUTO's trials alternate candidates between the
+      // lanes; a new shape's first launches): copied once its last sort is done, so that a trial
+      // runs the order a settled launch of its candidate would
+      mcpt_ctx::Lane& O = c->lanes[li ^ 1];
+      if (O.order_valid && std::equal(key, key + 8, O.order_key) && O.item_cap >= items) {
+        HIP_OR_RETURN(hipStreamWaitEvent(ws, O.tail, 0));
+        HIP_OR_RETURN(hipStreamWaitEvent(ws, O.freed, 0));
+        HIP_OR_RETURN(hipMemcpyAsync(L.d_item_perm, O.d_item_perm, sizeof(int) * (size_t)items, hipMemcpyDeviceToDevice, ws));
+        HIP_OR_RETURN(hipMemcpyAsync(L.d_split_n, O.d_split_n, sizeof(int), hipMemcpyDeviceToDevice, ws));
+        // (the other lane's next sort, which rewrites its order, waits for the copy)
+        HIP_OR_RETURN(hipEventRecord(L.tail, ws));
+        HIP_OR_RETURN(hipStreamWaitEvent(O.stream, L.tail, 0));
+        std::copy(key, key + 8, L.order_key);
+        L.order_valid = true;
+        L.order_age = O.order_age;
+      }
+    }
     if (order) {
       if (L.order_valid && std::equal(key, key + 8, L.order_key)) {
         p.item_perm = L.d_item_perm;
