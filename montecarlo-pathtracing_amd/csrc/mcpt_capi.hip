@@ -101,6 +101,7 @@ struct mcpt_ctx {
   // calls without waiting after each; ring_pos = the last call's slot.
   std::vector<hipEvent_t> evs[kTimingRing];
   int ring_n_sub[kTimingRing] = {};
+  std::vector<char> ring_lane[kTimingRing];   // per sub-launch: a lane launch
   int ring_pos = 0;
   long long n_timed = 0;            // render calls timed so far
   int n_sub = 0;                    // sub-launches of the last render call
@@ -156,6 +157,8 @@ struct mcpt_ctx {
   struct Lane {
     hipStream_t stream = nullptr;
     hipEvent_t freed = nullptr;     // on `stream` after the lane's last combine: its buffers are free
+    bool freed_stale = false;       // launches in order on `stream` used the lane since (not recorded:
+                                    // launch-bound calls skip the record; the next waiter records it)
     hipEvent_t tail = nullptr;      // on the lane's stream after its last operation
     float* d_partial = nullptr;     // pass-segment sums (launches spanning > 1 chunk)
     size_t partial_bytes = 0;
@@ -191,6 +194,7 @@ static hipEvent_t ev_stop(const mcpt_ctx* c, int k) { return c->evs[c->ring_pos]
 // event i of sub-launch k in ring slot `slot` (0 start, 1 mid, 2 stop)
 static hipEvent_t ev_at(const mcpt_ctx* c, int slot, int k, int i) { return c->evs[slot][kEvPerSub * k + i]; }
 static hipError_t ensure_events(mcpt_ctx* c, int slot, int n_sub) {
+  if ((int)c->ring_lane[slot].size() < n_sub) c->ring_lane[slot].resize(n_sub, 0);
   while ((int)c->evs[slot].size() < kEvPerSub * n_sub) {
     hipEvent_t e = nullptr;
     hipError_t r = hipEventCreate(&e);
@@ -1188,6 +1192,7 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   // call that fails part-way leaves the previous call's complete timings in place.
   if (n_sub == 0) {   // no passes: an empty timed interval
     for (int i = 0; i < kEvPerSub; ++i) HIP_OR_RETURN(hipEventRecord(ev_at(c, slot, 0, i), c->stream));
+    c->ring_lane[slot][0] = 0;
   }
   for (long long lo = first_pass, end = (long long)first_pass + n_passes, k = 0; lo < end; ++k) {
     const long long c0 = fdiv((int)(lo - 1), mcpt::kPassChunk);
@@ -1235,7 +1240,12 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
     }
     p.partial = L.d_partial;
     if (order) HIP_OR_RETURN(ensure_item_order(c, L, items));
-    if (lane) HIP_OR_RETURN(hipStreamWaitEvent(L.stream, L.freed, 0));
+    // (a lane whose last launches ran in order on `stream` is free once `stream`'s work so far is)
+    auto freed = [&](mcpt_ctx::Lane& X) -> hipEvent_t {
+      if (X.freed_stale && hipEventRecord(X.freed, c->stream) == hipSuccess) X.freed_stale = false;
+      return X.freed;
+    };
+    if (lane) HIP_OR_RETURN(hipStreamWaitEvent(L.stream, freed(L), 0));
     if (order && !(L.order_valid && std::equal(key, key + 8, L.order_key))) {
       // the other lane holds this shape's order (AUTO's trials alternate candidates between the
       // lanes; a new shape's first launches): copied once its last sort is done, so that a trial
@@ -1243,7 +1253,7 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
       mcpt_ctx::Lane& O = c->lanes[li ^ 1];
       if (O.order_valid && std::equal(key, key + 8, O.order_key) && O.item_cap >= items) {
         HIP_OR_RETURN(hipStreamWaitEvent(ws, O.tail, 0));
-        HIP_OR_RETURN(hipStreamWaitEvent(ws, O.freed, 0));
+        HIP_OR_RETURN(hipStreamWaitEvent(ws, freed(O), 0));
         HIP_OR_RETURN(hipMemcpyAsync(L.d_item_perm, O.d_item_perm, sizeof(int) * (size_t)items, hipMemcpyDeviceToDevice, ws));
         HIP_OR_RETURN(hipMemcpyAsync(L.d_split_n, O.d_split_n, sizeof(int), hipMemcpyDeviceToDevice, ws));
         // (the other lane's next sort, which rewrites its order, waits for the copy)
@@ -1286,7 +1296,8 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
     // its period, not its whole span (which would count the overlapped tails twice)
     const bool period = lane && c->prev_lane >= 0 && c->prev_lane != li;
     HIP_OR_RETURN(hipEventRecord(ev_at(c, slot, (int)k, 0), period ? c->lanes[c->prev_lane].stream : ws));
-    HIP_OR_RETURN(hipEventRecord(ev_at(c, slot, (int)k, 3), ws));
+    if (lane) HIP_OR_RETURN(hipEventRecord(ev_at(c, slot, (int)k, 3), ws));   // (in order: the span is 0 -> 1)
+    c->ring_lane[slot][k] = lane;
     if (stream) {
       const int st = stream_run(c, p);
       if (st != MCPT_OK) return st;
@@ -1320,7 +1331,12 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
       HIP_OR_RETURN(hipEventRecord(L.tail, L.stream));
       HIP_OR_RETURN(hipStreamWaitEvent(c->stream, L.tail, 0));
     }
-    HIP_OR_RETURN(hipEventRecord(L.freed, c->stream));
+    if (lane) {
+      HIP_OR_RETURN(hipEventRecord(L.freed, c->stream));
+      L.freed_stale = false;
+    } else {
+      L.freed_stale = true;
+    }
     c->prev_lane = lane ? li : -1;
 #ifdef MCPT_CHECKED
     {
@@ -1758,7 +1774,7 @@ int mcpt_kernel_span_ms_back(mcpt_ctx* c, int back, float* span_ms) {
   for (int k = 0; k < c->ring_n_sub[slot]; ++k) {
     float a = 0.0f;
     HIP_OR_RETURN(hipEventSynchronize(v[kEvPerSub * k + 1]));
-    HIP_OR_RETURN(hipEventElapsedTime(&a, v[kEvPerSub * k + 3], v[kEvPerSub * k + 1]));
+    HIP_OR_RETURN(hipEventElapsedTime(&a, v[kEvPerSub * k + (c->ring_lane[slot][k] ? 3 : 0)], v[kEvPerSub * k + 1]));
     tot += a;
   }
   *span_ms = tot;

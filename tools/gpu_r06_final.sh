@@ -15,16 +15,17 @@ tests)
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
   tail -3 $O/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && echo "smoke ok" ;;
-pmc)
+pmc)   # each record averages the last 4 timed calls' launches (PMC_STEPS, --calls)
   cp profiles/pmc_records.json $O/pmc_records.json
+  export PMC_STEPS=4
   for spec in "c2 scene6_1920x1080_256spp_B8" "c4 scene8_1920x1080_512spp_B12" "c1 scene1_256x256_4spp_B3"; do
     set -- $spec
-    bash tools/pmc.sh $O/pmc_$1 --config $1 && python tools/pmc_summary.py $O/pmc_$1 $2 $O/pmc_records.json > /dev/null && echo "pmc $1 ok" || exit 1
+    bash tools/pmc.sh $O/pmc_$1 --config $1 && python tools/pmc_summary.py $O/pmc_$1 $2 $O/pmc_records.json --calls=4 > /dev/null && echo "pmc $1 ok" || exit 1
   done
-  bash tools/pmc.sh $O/pmc_c3 --config c3 --rough 0 && python tools/pmc_summary.py $O/pmc_c3 scene6_1920x1080_1024spp_B8_ior1.5_rough0 $O/pmc_records.json > /dev/null && echo "pmc c3 ok" &&
-  bash tools/pmc.sh $O/pmc_c5 --config c5 && python tools/pmc_summary.py $O/pmc_c5 scene6_3840x2160_1024spp_B8 $O/pmc_records.json --launches=1 > /dev/null && echo "pmc c5 ok" &&
-  PMC_MEM=1 bash tools/pmc.sh $O/pmc_mesh --config mesh && python tools/pmc_summary.py $O/pmc_mesh mesh1000k_1920x1080_64spp_B8 $O/pmc_records.json > /dev/null && echo "pmc mesh ok" &&
-  PMC_MEM=1 bash tools/pmc.sh $O/pmc_mesh_big --config mesh_big && python tools/pmc_summary.py $O/pmc_mesh_big mesh4x1000k_1920x1080_64spp_B8 $O/pmc_records.json > /dev/null && echo "pmc mesh_big ok" ;;
+  bash tools/pmc.sh $O/pmc_c3 --config c3 --rough 0 && python tools/pmc_summary.py $O/pmc_c3 scene6_1920x1080_1024spp_B8_ior1.5_rough0 $O/pmc_records.json --calls=4 > /dev/null && echo "pmc c3 ok" &&
+  bash tools/pmc.sh $O/pmc_c5 --config c5 && python tools/pmc_summary.py $O/pmc_c5 scene6_3840x2160_1024spp_B8 $O/pmc_records.json --launches=1 --calls=4 > /dev/null && echo "pmc c5 ok" &&
+  PMC_MEM=1 bash tools/pmc.sh $O/pmc_mesh --config mesh && python tools/pmc_summary.py $O/pmc_mesh mesh1000k_1920x1080_64spp_B8 $O/pmc_records.json --calls=4 > /dev/null && echo "pmc mesh ok" &&
+  PMC_MEM=1 bash tools/pmc.sh $O/pmc_mesh_big --config mesh_big && python tools/pmc_summary.py $O/pmc_mesh_big mesh4x1000k_1920x1080_64spp_B8 $O/pmc_records.json --calls=4 > /dev/null && echo "pmc mesh_big ok" ;;
 bench)
   for c in c2 c4 mesh mesh_big c1 c3 c5; do
     timeout -k 10 600 python bench.py --config $c > $O/bench_$c.json 2> $O/bench_$c.err && echo "bench $c ok: $(python -c "import json;d=json.load(open('$O/bench_$c.json'));print(d['value'], d['roofline'].get('frac'))")" || exit 1
