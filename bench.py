@@ -556,7 +556,7 @@ def self_check(args, scene, ipv, iv, frame: torch.Tensor, n_calls: int, S: int, 
 
 
 def roofline(workload: str, sha: str, avg_trace_ms: float, ref_bytes: float, bytes_per_sample: float, world: int,
-             launches: int = 1, bound: str = "valu"):
+             launches: int = 1, bound: str = "valu", sched=None):
     """`avg_trace_ms` is one timed call's kernel time, summed over its `launches` sub-launches; a
     PMC record is used only if it sums the same number of launches.
     bound "valu" (the LDS/L2-resident reference scenes): achieved = VALU lane-instructions / s
@@ -568,6 +568,13 @@ def roofline(workload: str, sha: str, avg_trace_ms: float, ref_bytes: float, byt
     rec = pmc_record(workload, sha) if world == 1 else None
     if rec is not None and int(rec.get("launches_summed", 1)) != int(launches):
         rec = None
+    # (a record states the schedule its counter passes ran, tools/pmc_summary.py: used only for the
+    # same schedule as this run's timed launches; None there = its passes ran different ones)
+    other_sched = False
+    if rec is not None and sched is not None and "schedule" in rec:
+        mine = {"traversal": sched.get("traversal"), "seg_per_item": sched.get("seg_per_item")}
+        if rec["schedule"] != mine:
+            rec, other_sched = None, True
     t_s = avg_trace_ms / 1e3
     valu = {"achieved": None, "peak": VALU_PEAK_T, "unit": "T lane-instr/s", "frac": None,
             "lane_utilisation": None, "useful_frac": None}
@@ -585,8 +592,11 @@ def roofline(workload: str, sha: str, avg_trace_ms: float, ref_bytes: float, byt
             gbs = traffic / t_s / 1e9
             hbm.update(achieved=round(gbs, 2), frac=round(gbs / HBM_PEAK_GBS, 5))
     pmc = {"workload": workload, "lib_sha256": sha, "matched": rec is not None,
+           "schedule": rec.get("schedule") if rec else None,
            "source": rec.get("source") if rec else None,
-           "note": None if rec else ("no rocprofv3 PMC record of this workload for this libmcpt.so "
+           "note": None if rec else ("the PMC record of this workload and build was measured under another "
+                                     "schedule than this run's: PMC fields left null" if other_sched else
+                                     "no rocprofv3 PMC record of this workload for this libmcpt.so "
                                      "build (summing this call's launches) in profiles/pmc_records.json: "
                                      "PMC fields left null"
                                      if world == 1 else "PMC records are single-GPU measurements")}
@@ -828,7 +838,7 @@ def main():
             a = pt["allstats"]
             pt["roof"] = roofline(workload_key(args, S, pt["rough"]), sha, pt["avg_trace_ms"], float(a[0, 0]),
                                   float(a[:, 0].sum() / max(a[:, 3].sum(), 1.0)), world, pt["launches"],
-                                  bound="hbm" if args.scene in ("mesh", "mesh4") else "valu")
+                                  bound="hbm" if args.scene in ("mesh", "mesh4") else "valu", sched=pt["sched"])
         config = {
             "workload": workload_key(args, S, main_pt["rough"] if len(points) == 1 else None)
                         + ("_rough-sweep" if len(points) > 1 else ""),

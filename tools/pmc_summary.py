@@ -72,7 +72,7 @@ def main():
         "workload": workload,
         "lib_sha256": hashlib.sha256(open(LIB, "rb").read()).hexdigest(),
         "kernel": kernel,
-        "source": f"rocprofv3 --pmc passes of tools/pmc.sh ({os.path.basename(d.rstrip('/'))})",
+        "source": "rocprofv3 --pmc passes of tools/pmc.sh (session %s)" % "/".join(d.rstrip("/").split("/")[-2:]),
         "launches_summed": launches,
         "calls_averaged": calls,
         "hbm_bytes_per_launch": fetch_b + write_b,
@@ -80,6 +80,21 @@ def main():
         "write_bytes_per_launch": write_b,
         "counters_per_launch": c,
     }
+    # the schedule AUTO settled on in each counter pass (each pass is its own bench process): a
+    # record combines passes only when they all ran the same one (bench.py uses a record only for
+    # its own settled schedule)
+    scheds = {}
+    for f in sorted(glob.glob(os.path.join(d, "*.log"))):
+        try:
+            line = [ln for ln in open(f) if ln.startswith("{")][-1]
+            sc = json.loads(line)["kernel_ms"]["schedule_rank0"]
+            scheds[os.path.basename(f)[:-4]] = {"traversal": sc["traversal"], "seg_per_item": sc["seg_per_item"]}
+        except (IndexError, KeyError, ValueError, OSError):
+            pass
+    distinct = {json.dumps(v, sort_keys=True) for v in scheds.values()}
+    rec["schedule"] = json.loads(distinct.pop()) if len(distinct) == 1 else None
+    if len(scheds) and rec["schedule"] is None:
+        rec["schedules_by_pass"] = scheds
     if "SQ_INSTS_VALU" in c and "GRBM_GUI_ACTIVE" in c:
         cycles = c["GRBM_GUI_ACTIVE"] / 8.0                     # per-XCD clock cycles of the launch
         simds = 256 * 4
