@@ -209,7 +209,9 @@ int mcpt_gather_rows(mcpt_ctx* frame, mcpt_ctx* const* shards, int n_shards);
  * depth >= 8 also the per-lane walk with the deep knobs (leaf batch 16, walk exit 40, min-done 8)
  * at four and at eight segments per item — at most five candidates, each timed twice (forward,
  * then reverse order; each one's best time per sample kept), compared only between launches of
- * the same shape: at most 10 trial launches (mcpt.AUTO_TRIALS).  It never times the stream
+ * the same shape: at most 10 trial launches, run in order on the context's stream (not on the
+ * render lanes); a trial's time is read when the call after the next one starts, so AUTO settles
+ * two calls after its last trial (mcpt.AUTO_TRIALS = 12 calls).  It never times the stream
  * schedule, which runs only when selected explicitly (MCPT_TRAVERSAL_STREAM).  Later launches of
  * that shape use the fastest.  mcpt_get_walk_exit / mcpt_get_leaf_batch report the knobs of the
  * candidate the next launch uses.
