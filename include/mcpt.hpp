@@ -385,6 +385,8 @@ class Renderer {
     check(mcpt_gather_rows(c_, h.data(), (int)h.size()), "mcpt_gather_rows");
   }
   void set_traversal(int mode) { check(mcpt_set_traversal(c_, mode), "mcpt_set_traversal"); }
+  // render lanes (consecutive launches overlapping each other's tails; same bits): on by default
+  void set_render_lanes(bool on) { check(mcpt_set_render_lanes(c_, on ? 1 : 0), "mcpt_set_render_lanes"); }
   // stream schedule knobs (MCPT_TRAVERSAL_STREAM): path slots (0: default), refill threshold (-1: default)
   void set_stream_pool(int slots, int refill) { check(mcpt_set_stream_pool(c_, slots, refill), "mcpt_set_stream_pool"); }
   int width() const { return W_; }
