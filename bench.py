@@ -99,6 +99,11 @@ from mcpt.dist import ShardedRenderer, local_rows  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 VALU_PEAK_T = 78.64     # 256 CUs x 4 SIMD-32 x 32 lanes/clk x 2.4 GHz (a wave64 VALU op = 2 clk)
+# fabric requests per second that lanes running dependent chains of random 64-B record reads (the
+# mesh walk's access pattern, without its arithmetic) sustain at 5 waves per SIMD, by working set
+# (tools/microbench/gather_ceiling.hip, profiles/r06_gather_ceiling.json: one 128-B request per
+# record; 128 MB: 3.53 / 3.66 TB/s of records in two sessions, 640 MB: 3.59 TB/s)
+GATHER_CEILING_REQ_S = {"mesh1000k": 56.2e9, "mesh4x1000k": 56.1e9}
 METRIC = "Msamples/s (W×H×spp/s) + achieved HBM GB/s, 1080p scene6, 1/2/4/8 GPU"
 PMC_RECORDS = os.path.join(REPO, "profiles", "pmc_records.json")
 C3_ROUGHNESS = (0.0, 0.5, 0.9, 0.99, 1.0)
@@ -622,6 +627,15 @@ def roofline(workload: str, sha: str, avg_trace_ms: float, ref_bytes: float, byt
                                "note": ("frac prices the algorithmic bytes against the HBM peak (the north "
                                         "star's roofline); bound_by says which measured rate is closer to its "
                                         "own peak: VALU lane-instructions / 78.64 T, or fabric bytes (L3 + HBM) / 8 TB/s")}
+            # the fabric's own ceiling on this access pattern (measured, not a spec figure)
+            req = (rec.get("memory") or {}).get("fabric_reads")
+            ceil = GATHER_CEILING_REQ_S.get(workload.split("_")[0])
+            if req and ceil and t_s > 0:
+                roof["limiter"]["fabric_request_ceiling"] = {
+                    "walk_requests_per_s": round(req / t_s / 1e9, 2), "ceiling_requests_per_s": round(ceil / 1e9, 2),
+                    "unit": "G/s", "frac": round(req / t_s / ceil, 4),
+                    "source": "tools/microbench/gather_ceiling.hip (profiles/r06_gather_ceiling.json): dependent "
+                              "random 64-B record chains over the same working set, one 128-B fabric request per record"}
     else:
         roof = dict(bound="valu", **{k: valu[k] for k in ("achieved", "peak", "unit", "frac", "lane_utilisation",
                                                            "useful_frac")})

@@ -37,6 +37,26 @@ def test_pmc_record_keyed_by_library_hash(tmp_path, monkeypatch):
     assert bench.pmc_record("scene6_1920x1080_256spp_B8", "aa") is None
 
 
+def test_mesh_roofline_fabric_request_ceiling(tmp_path, monkeypatch):
+    """The mesh workloads' `limiter` prices the PMC fabric requests per second against the measured
+    ceiling of their access pattern (tools/microbench/gather_ceiling.hip), keyed by the workload."""
+    rec = {"workload": "mesh4x1000k_1920x1080_64spp_B8", "lib_sha256": "aa", "launches_summed": 1,
+           "counters_per_launch": {"SQ_INSTS_VALU": 1e9}, "hbm_bytes_per_launch": 4e11,
+           "valu_lane_utilisation": 0.25, "memory": {"fabric_reads": 3.0e9}}
+    f = tmp_path / "pmc_records.json"
+    f.write_text(json.dumps({"records": [rec]}))
+    monkeypatch.setattr(bench, "PMC_RECORDS", str(f))
+    roof = bench.roofline("mesh4x1000k_1920x1080_64spp_B8", "aa", 100.0, 4e11, 3000.0, 1, bound="hbm")
+    c = roof["limiter"]["fabric_request_ceiling"]
+    assert c["walk_requests_per_s"] == 30.0                      # 3 G requests in 100 ms
+    assert c["frac"] == round(30e9 / bench.GATHER_CEILING_REQ_S["mesh4x1000k"], 4)
+    # a workload without a measured ceiling (or a record without memory counters) carries none
+    rec["workload"] = "mesh999k_1920x1080_64spp_B8"
+    f.write_text(json.dumps({"records": [rec]}))
+    roof = bench.roofline("mesh999k_1920x1080_64spp_B8", "aa", 100.0, 4e11, 3000.0, 1, bound="hbm")
+    assert "fabric_request_ceiling" not in roof["limiter"]
+
+
 def test_workload_keys():
     class A:
         scene, width, height, bounces = 6, 1920, 1080, 8
