@@ -464,7 +464,7 @@ int mcpt_create(int device_ordinal, mcpt_ctx** out) {
 }
 
 static void free_meshes(mcpt_ctx* c) {
-  (void)hipFree(c->d_minfo); (void)hipFree(c->d_mpairs); (void)hipFree(c->d_mleaftris);
+  (void)hipFree(c->d_minfo); (void)hipFree(c->d_mpairs);   // (d_mleaftris points into d_mpairs)
   (void)hipFree(c->d_mtris); (void)hipFree(c->d_mverts); (void)hipFree(c->d_mnorms);
   c->d_minfo = nullptr; c->d_mpairs = nullptr; c->d_mleaftris = nullptr;
   c->d_mtris = nullptr; c->d_mverts = nullptr; c->d_mnorms = nullptr;
@@ -707,8 +707,12 @@ int mcpt_upload_meshes(mcpt_ctx* c, int n_meshes, const int* info, int n_nodes, 
     }
   }
   HIP_OR_RETURN(hipMalloc(&c->d_minfo, hi.size() * sizeof(int4)));
-  HIP_OR_RETURN(hipMalloc(&c->d_mpairs, hn.size() * sizeof(float4)));
-  HIP_OR_RETURN(hipMalloc(&c->d_mleaftris, hl.size() * sizeof(float4)));
+  // one allocation: the pair slots, then the leaf records (walk_run_mesh addresses both by 32-bit
+  // byte offsets from d_mpairs)
+  if ((hn.size() + hl.size()) * sizeof(float4) > (size_t(1) << 32))
+    return set_err(MCPT_ERR_BAD_SCENE, "mesh BVH records exceed 4 GiB");
+  HIP_OR_RETURN(hipMalloc(&c->d_mpairs, (hn.size() + hl.size()) * sizeof(float4)));
+  c->d_mleaftris = c->d_mpairs + hn.size();
   HIP_OR_RETURN(hipMalloc(&c->d_mtris, ht.size() * sizeof(int4)));
   HIP_OR_RETURN(hipMalloc(&c->d_mverts, hv.size() * sizeof(float4)));
   HIP_OR_RETURN(hipMalloc(&c->d_mnorms, hm.size() * sizeof(float4)));

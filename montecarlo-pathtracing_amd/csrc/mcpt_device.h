@@ -101,7 +101,8 @@ struct SceneT {
   // (c_right, has_right) (w_right, 0)
   const float4* __restrict__ mpairs;
   // 4 rows per mesh leaf at its global leaf index: (A, t) (B - A, 0) (C - A, 0) (0) of the
-  // leaf's triangle, t = the mesh-local triangle id as int bits (-1: empty leaf)
+  // leaf's triangle, t = the mesh-local triangle id as int bits (-1: empty leaf).  In the same
+  // allocation as mpairs, after its slots (walk_run_mesh addresses both from mpairs)
   const float4* __restrict__ mleaftris;
   const int4* __restrict__ mtris;     // global vertex ids (a, b, c, 0) (intersection_info)
   const float4* __restrict__ mverts;  // (x, y, z, 0)
@@ -886,7 +887,15 @@ __device__ __forceinline__ bool walk_run_mesh(const SR& s, f3 O, f3 D, Hit& h, W
   const int leaf0 = (1 << s.depth) - 1;
   const int n0 = SUSPEND ? __builtin_popcountll(__ballot(1)) : 0;
   for (;;) {
+    // the suspension test at the loop head rather than its tail (the same test between the same
+    // iterations: lanes whose walk ended have returned): the compiler's copies of the walk state
+    // at the back edge shrink (mesh workload +3.7 %, profiles/r06_ab_mesh_walk_copies.jsonl)
+    if (SUSPEND) {   // wave-uniform
+      const int n = __builtin_popcountll(__ballot(1));
+      if (n <= exit && n < n0) return false;
+    }
     bool pop = false;   // the scene walk pops its stack this iteration
+    int enter_p = -1;   // this lane starts the mesh walk of instance enter_p (set up below)
     if (w.mprim >= 0) {
       // one step of the instance's mesh walk (mesh_test's loop body)
       const int4 mi = w.mi;
@@ -901,16 +910,24 @@ __device__ __forceinline__ bool walk_run_mesh(const SR& s, f3 O, f3 D, Hit& h, W
       // triangle record), issued before the lanes split into the node and leaf blocks: the wave
       // waits once per iteration instead of once per block (measured neutral on the mesh
       // workload, r05_ab_mesh_prefetch.jsonl session r05x; kept as the simpler form)
+      // Both kinds of record live in one allocation, the leaf records after the pair slots
+      // (mcpt_upload_meshes), so a record is a 32-bit byte offset from the wave-uniform base: the
+      // load takes the base from SGPRs (global_load ... saddr) and the step computes one 32-bit
+      // offset instead of two 64-bit addresses and a select of the bases.  The mesh workload
+      // +3.4 %, mesh_big +3.2 % (profiles/r06_ab_mesh_rec32.jsonl: ro vs main); records < 4 GiB.
       const bool mleaf = w.mnode >= mleaf0;
-      const size_t j = 2 * (size_t)w.mnode + 1;
-      const float4* q = mleaf ? s.mleaftris + ((size_t)mi.y + (w.mnode - mleaf0)) * 4
-                              : s.mpairs + ((size_t)mi.x + mesh_pair_slot(w.mnode)) * 4;
+      const unsigned j = 2u * (unsigned)w.mnode + 1u;
+      const unsigned lslot0 = (unsigned)(s.mleaftris - s.mpairs) >> 2;   // first leaf record (uniform)
+      const unsigned rec = mleaf ? lslot0 + (unsigned)(mi.y + (w.mnode - mleaf0))
+                                 : (unsigned)mi.x + mesh_pair_slot((unsigned)w.mnode);
       // node lanes also request their children's line (both pair records, or the two leaf
       // records of the last level), consumed one step later: +0.9..1.4 % on the mesh workload;
       // the grandchildren's two lines as well: -5..8 % (profiles/r05_ab_mesh_prefetch.jsonl)
-      const float4* qc = mleaf ? q
-                               : ((w.mlevel + 1 < mi.z) ? s.mpairs + ((size_t)mi.x + mesh_pair_slot((unsigned)j)) * 4
-                                                        : s.mleaftris + ((size_t)mi.y + (j - mleaf0)) * 4);
+      const unsigned recc = mleaf ? rec
+                                  : ((w.mlevel + 1 < mi.z) ? (unsigned)mi.x + mesh_pair_slot(j)
+                                                           : lslot0 + (unsigned)mi.y + (j - (unsigned)mleaf0));
+      const float4* q = (const float4*)((const char*)s.mpairs + rec * 64u);
+      const float4* qc = (const float4*)((const char*)s.mpairs + recc * 64u);
       const float4 a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
       asm volatile("" ::"v"(w.mpf));
       w.mpf = *(const int*)qc;
@@ -954,15 +971,12 @@ __device__ __forceinline__ bool walk_run_mesh(const SR& s, f3 O, f3 D, Hit& h, W
       if (p >= 0) {
         const int pt = s.ptype[p];
         if (pt >= 0 && (pt & 15) == CODE_MESH) {
-          // intersect_prim's transforms, then the mesh walk starts with the next iteration
+          // the mesh walk starts with the next iteration; its set-up (intersect_prim's
+          // transforms) runs after the step blocks, below
           ev.inc(EV_PRIM);
           ev.inc(EV_MESH);
-          const size_t b = (size_t)p * 8;
-          const float4 r0 = s.prims[b], r1 = s.prims[b + 1], r2 = s.prims[b + 2];
-          w.Om = xpoint(r0, r1, r2, O);
-          w.Dm = wnormalize3<SR::kFastNorm>(xdir(r0, r1, r2, D));
-          w.invDm = mk(rcp_rn(w.Dm.x), rcp_rn(w.Dm.y), rcp_rn(w.Dm.z));
-          w.mprim = p; w.mi = s.minfo[pt >> 4];
+          enter_p = p;
+          w.mprim = p;
           w.mnode = 0; w.mlevel = 0; w.mpending = 0;
           pop = false;
         } else {
@@ -985,16 +999,34 @@ __device__ __forceinline__ bool walk_run_mesh(const SR& s, f3 O, f3 D, Hit& h, W
         w.node = (int)j; w.level++;
       }
     }
+    // The mesh entry's set-up (intersect_prim's transforms, :681-705) in a wave-uniform block
+    // where every path of the iteration meets: each walking lane computes it (from its own
+    // instance, else from prim 0's records) and keeps it by a select.  Assigned inside the
+    // scene-leaf block, the twelve values of the mesh-space ray and mesh info were joined there
+    // and the compiler copied all twelve into other registers and back on every iteration (24
+    // v_mov per iteration); as selects they stay in place.  The entering lanes compute the same
+    // values as before (same bits).  Mesh workload +6.3 %, mesh_big +6.7 % with the head test
+    // above (r06_ab_mesh_walk_copies.jsonl: t13 vs main).
+    if (__ballot(enter_p >= 0)) {
+      const bool e = enter_p >= 0;
+      const int pe = e ? enter_p : w.mprim >= 0 ? w.mprim : 0;
+      const size_t b = (size_t)pe * 8;
+      const float4 r0 = s.prims[b], r1 = s.prims[b + 1], r2 = s.prims[b + 2];
+      const f3 nOm = xpoint(r0, r1, r2, O);
+      const f3 nDm = wnormalize3<SR::kFastNorm>(xdir(r0, r1, r2, D));
+      const f3 niD = mk(rcp_rn(nDm.x), rcp_rn(nDm.y), rcp_rn(nDm.z));
+      const int4 nmi = s.minfo[e ? (s.ptype[pe] >> 4) : 0];
+      w.Om.x = e ? nOm.x : w.Om.x; w.Om.y = e ? nOm.y : w.Om.y; w.Om.z = e ? nOm.z : w.Om.z;
+      w.Dm.x = e ? nDm.x : w.Dm.x; w.Dm.y = e ? nDm.y : w.Dm.y; w.Dm.z = e ? nDm.z : w.Dm.z;
+      w.invDm.x = e ? niD.x : w.invDm.x; w.invDm.y = e ? niD.y : w.invDm.y; w.invDm.z = e ? niD.z : w.invDm.z;
+      w.mi.x = e ? nmi.x : w.mi.x; w.mi.y = e ? nmi.y : w.mi.y; w.mi.z = e ? nmi.z : w.mi.z; w.mi.w = e ? nmi.w : w.mi.w;
+    }
     if (pop) {
       if (w.pending == 0) return true;
       const int L = 31 - __builtin_clz(w.pending);
       w.pending &= ~(1u << L);
       w.node = ((w.node + 1) >> (w.level - L)) - 2;
       w.level = L;
-    }
-    if (SUSPEND) {   // wave-uniform
-      const int n = __builtin_popcountll(__ballot(1));
-      if (n <= exit && n < n0) return false;
     }
   }
 }
