@@ -622,8 +622,15 @@ static void pack_mesh_pairs(const float* nodes, const int* leaves, int depth, fl
     const float4* l = &rec[(size_t)(2 * i + 1) * 3];
     const float4* r = &rec[(size_t)(2 * i + 2) * 3];
     float4* o = out + (size_t)mcpt::mesh_pair_slot((unsigned)i) * 4;
+    // row 1's w: 1 when all six half-widths lie in rcp_core's exact range (rcp6_rn then skips
+    // its six range tests), else 0
+    bool in_range = true;
+    for (float v : {l[1].x, l[1].y, l[1].z, r[1].x, r[1].y, r[1].z}) {
+      const float a = std::fabs(v);
+      in_range = in_range && a >= 0x1p-126f && a < 0x1p126f;
+    }
     o[0] = l[0];
-    o[1] = make_float4(l[1].x, l[1].y, l[1].z, 0.0f);
+    o[1] = make_float4(l[1].x, l[1].y, l[1].z, in_range ? 1.0f : 0.0f);
     o[2] = r[0];
     o[3] = make_float4(r[1].x, r[1].y, r[1].z, 0.0f);
   }
