@@ -159,7 +159,10 @@ enum {
   LS_NODE_IT, LS_NODE_LN, LS_NE_WV, LS_NE_LN, LS_OUT_WV, LS_OUT_LN, LS_VAL_WV, LS_VAL_LN,
   LS_LEAF_IT, LS_LEAF_LN, LS_PRIM_LN, LS_SPH_WV, LS_SPH_LN, LS_CUBE_WV, LS_CUBE_LN, LS_CYL_WV,
   LS_CYL_LN, LS_QUAD_WV, LS_QUAD_LN, LS_WALK_IT, LS_WALK_LN, LS_WALK_CALLS, LS_ROUNDS, LS_ROUND_LN,
-  LS_SHADE_WV, LS_SHADE_LN, LS_RR2_WV, LS_RR2_LN, LS_WAVES, LS_FIT_IT, LS_TWO_IT, LS_COUNT
+  LS_SHADE_WV, LS_SHADE_LN, LS_RR2_WV, LS_RR2_LN, LS_WAVES, LS_FIT_IT, LS_TWO_IT,
+  // walk_run_mesh: the scene-node and scene-leaf blocks (LS_NODE / LS_LEAF count the mesh-node and
+  // mesh-leaf blocks there), and the lanes still walking when the wave leaves the walk
+  LS_SNODE_IT, LS_SNODE_LN, LS_SLEAF_IT, LS_SLEAF_LN, LS_EXIT_LN, LS_COUNT
 };
 __device__ __forceinline__ unsigned* ls_row() {
   __shared__ unsigned s_ls[16][LS_COUNT];
@@ -888,6 +891,9 @@ template <bool COUNT, bool SUSPEND, class SR>
 __device__ __forceinline__ bool walk_run_mesh(const SR& s, f3 O, f3 D, Hit& h, Walk& w, Ev<COUNT>& ev, int exit) {
   const int leaf0 = (1 << s.depth) - 1;
   const int n0 = SUSPEND ? __builtin_popcountll(__ballot(1)) : 0;
+#ifdef MCPT_LANESTATS
+  ls_add(LS_WALK_CALLS, 1u);
+#endif
   for (;;) {
     // the suspension test at the loop head rather than its tail (the same test between the same
     // iterations: lanes whose walk ended have returned): the compiler's copies of the walk state
@@ -896,8 +902,24 @@ __device__ __forceinline__ bool walk_run_mesh(const SR& s, f3 O, f3 D, Hit& h, W
     // vector one)
     if (SUSPEND) {   // wave-uniform
       const int n = __builtin_popcountll(__ballot(1));
-      if (n <= exit && n != n0) return false;
+      if (n <= exit && n != n0) {
+#ifdef MCPT_LANESTATS
+        ls_add(LS_EXIT_LN, (unsigned)n);
+#endif
+        return false;
+      }
     }
+#ifdef MCPT_LANESTATS
+    {   // which block each walking lane takes this iteration
+      const bool inm = w.mprim >= 0, ml = inm && w.mnode >= (1 << w.mi.z) - 1, sl = !inm && w.node >= leaf0;
+      ls_add(LS_WALK_IT, 1u);
+      ls_add(LS_WALK_LN, ls_pop(true));
+      ls_cond(LS_NODE_IT, LS_NODE_LN, inm && !ml);
+      ls_cond(LS_LEAF_IT, LS_LEAF_LN, ml);
+      ls_cond(LS_SNODE_IT, LS_SNODE_LN, !inm && !sl);
+      ls_cond(LS_SLEAF_IT, LS_SLEAF_LN, sl);
+    }
+#endif
     bool pop = false;   // the scene walk pops its stack this iteration
     int enter_p = -1;   // this lane starts the mesh walk of instance enter_p (set up below)
     if (w.mprim >= 0) {

@@ -33,9 +33,9 @@ def run(sid, B, spp, seg, leaf_batch, walk_exit, W=1920, H=1080):
     os.environ["MCPT_LEAF_BATCH"] = str(leaf_batch)   # read when a context is created
     r = mcpt.Renderer(0)
     r.set_traversal(1)
-    if sid == 0:   # the mesh workload (walk_run_mesh: node / leaf = mesh-node / mesh-leaf steps)
+    if sid in (0, -1):   # the mesh workloads (walk_run_mesh: node / leaf = mesh-node / mesh-leaf steps)
         from mcpt import meshes
-        r.upload_scene(meshes.big_mesh_scene(1_000_000)[0])
+        r.upload_scene((meshes.big_mesh_scene if sid == 0 else meshes.big_mesh4_scene)(1_000_000)[0])
     else:
         r.upload_scene(mcpt.Scene.reference(sid))
     r.set_target(W, H)
@@ -72,9 +72,9 @@ def run(sid, B, spp, seg, leaf_batch, walk_exit, W=1920, H=1080):
 
 
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "mesh":   # the mesh workload (walk_run_mesh), walk exits
-        for wx in (24, 40):
-            run(0, 8, 64, 1, -1, wx)
+    if len(sys.argv) > 1 and sys.argv[1] == "mesh":   # the mesh workloads (walk_run_mesh) at walk exit 24
+        run(0, 8, 64, 1, -1, 24)
+        run(-1, 8, 64, 1, -1, 24)
         sys.exit(0)
     run(8, 12, 256, 8, 16, 40)      # C4 shape: deep knobs, eight segments per item
     run(8, 12, 256, 1, 16, 40)
