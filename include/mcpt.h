@@ -106,7 +106,10 @@ int mcpt_upload_scene(mcpt_ctx* ctx, const float* prims, int n_prims, const floa
 /* Upload the scene's meshes (replaces the tex_tri_/tex_p_/tex_n_ textures and the per-mesh
  * BVH rows of tex_bb_/tex_ind_, gpu_bvh_scene.cpp:87-118, 160-186).  Layouts: see
  * mcpt_scene_get_mesh_buffers.  n_meshes = 0 removes them.  Call after mcpt_upload_scene;
- * a CODE_MESH primitive's record holds its mesh id (texel 12 .y, "mesh_line"). */
+ * a CODE_MESH primitive's record holds its mesh id (texel 12 .y, "mesh_line").  Limits (else
+ * MCPT_ERR_BAD_SCENE): BVH depth <= 24 per mesh, and the device's mesh BVH records (64 B per
+ * internal node + 64 B per leaf, all meshes) within 4 GiB — the walk addresses them by 32-bit
+ * offsets — i.e. about 33 M triangles in all. */
 int mcpt_upload_meshes(mcpt_ctx* ctx, int n_meshes, const int* info, int n_nodes, const float* nodes, int n_leaves,
                        const int* leaves, int n_tris, const int* tris, int n_verts, const float* verts,
                        const float* normals);
