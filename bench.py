@@ -406,17 +406,22 @@ def lib_sha256() -> str:
         return hashlib.sha256(f.read()).hexdigest()
 
 
-def pmc_record(workload: str, sha: str):
-    """The PMC record of this workload measured on this exact library build, or None."""
+def pmc_record(workload: str, sha: str, sched=None):
+    """The PMC record of this workload measured on this exact library build, or None.  A workload
+    may hold records of several schedules (AUTO can settle on either of two close candidates):
+    with `sched` ({"traversal", "seg_per_item"}) the record of that schedule is preferred."""
     try:
         with open(PMC_RECORDS) as f:
             recs = json.load(f)["records"]
     except (OSError, ValueError, KeyError):
         return None
-    for rec in recs:
-        if rec.get("workload") == workload and rec.get("lib_sha256") == sha:
-            return rec
-    return None
+    mine = [r for r in recs if r.get("workload") == workload and r.get("lib_sha256") == sha]
+    if sched is not None:
+        want = {"traversal": sched.get("traversal"), "seg_per_item": sched.get("seg_per_item")}
+        for rec in mine:
+            if rec.get("schedule") == want:
+                return rec
+    return mine[0] if mine else None
 
 
 def host_cpu():
@@ -570,7 +575,7 @@ def roofline(workload: str, sha: str, avg_trace_ms: float, ref_bytes: float, byt
     achieved = the SURVEY §8d algorithmic bytes of one launch (counting build) / its time,
     against 8 TB/s; `traffic` = the PMC fabric bytes of one launch, `traffic_ratio` = traffic /
     algorithmic (> 1: re-reads); the VALU side under `valu`."""
-    rec = pmc_record(workload, sha) if world == 1 else None
+    rec = pmc_record(workload, sha, sched) if world == 1 else None
     if rec is not None and int(rec.get("launches_summed", 1)) != int(launches):
         rec = None
     # (a record states the schedule its counter passes ran, tools/pmc_summary.py: used only for the

@@ -37,6 +37,48 @@ def test_pmc_record_keyed_by_library_hash(tmp_path, monkeypatch):
     assert bench.pmc_record("scene6_1920x1080_256spp_B8", "aa") is None
 
 
+def test_pmc_record_by_schedule(tmp_path, monkeypatch):
+    """Records of one workload under two schedules sit side by side; the run's own schedule picks
+    its record, and a schedule with no record gets one whose schedule roofline() then rejects."""
+    s2 = {"traversal": "lane", "seg_per_item": 2}
+    s4 = {"traversal": "lane", "seg_per_item": 4}
+    recs = {"records": [
+        {"workload": "scene6_1920x1080_256spp_B8", "lib_sha256": "aa", "schedule": s4, "counters_per_launch": {"SQ_INSTS_VALU": 4}},
+        {"workload": "scene6_1920x1080_256spp_B8", "lib_sha256": "aa", "schedule": s2, "counters_per_launch": {"SQ_INSTS_VALU": 2}},
+    ]}
+    f = tmp_path / "pmc_records.json"
+    f.write_text(json.dumps(recs))
+    monkeypatch.setattr(bench, "PMC_RECORDS", str(f))
+    w = "scene6_1920x1080_256spp_B8"
+    assert bench.pmc_record(w, "aa", dict(s2, settled=True))["counters_per_launch"]["SQ_INSTS_VALU"] == 2
+    assert bench.pmc_record(w, "aa", s4)["counters_per_launch"]["SQ_INSTS_VALU"] == 4
+    roof = bench.roofline(w, "aa", 10.0, 1e9, 100.0, 1, sched={"traversal": "wave", "seg_per_item": 2})
+    assert roof["pmc"]["matched"] is False and roof["frac"] is None
+    roof = bench.roofline(w, "aa", 10.0, 1e9, 100.0, 1, sched=dict(s2, settled=True))
+    assert roof["pmc"]["matched"] is True and roof["valu_instructions_per_launch"] == 2
+
+
+def test_pmc_summary_keeps_other_schedules():
+    """tools/pmc_summary.py's merge: a new record replaces its own (workload, schedule) slot only;
+    a mixed-schedule record (None) takes the whole workload; other builds' records are dropped."""
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import importlib
+    merge = importlib.import_module("pmc_summary").merge_record
+    s2, s4 = {"traversal": "lane", "seg_per_item": 2}, {"traversal": "lane", "seg_per_item": 4}
+    w, v = "scene6_1920x1080_256spp_B8", "scene8_1920x1080_512spp_B12"
+    def r(wl, sc, sha="aa", tag=0):
+        return {"workload": wl, "lib_sha256": sha, "schedule": sc, "tag": tag}
+    recs = merge([r(w, s4, tag=1), r(v, s4), r(w, s4, sha="old")], r(w, s2, tag=2))
+    assert sorted((x["workload"], x["schedule"]["seg_per_item"], x["tag"]) for x in recs) == \
+        [(w, 2, 2), (w, 4, 1), (v, 4, 0)]
+    recs = merge(recs, r(w, s4, tag=3))                 # same slot: replaced
+    assert sorted(x["tag"] for x in recs if x["workload"] == w) == [2, 3]
+    recs = merge(recs, r(w, None, tag=4))               # mixed schedules: the workload's only record
+    assert [x["tag"] for x in recs if x["workload"] == w] == [4]
+    recs = merge(recs, r(w, s2, tag=5))                 # and a settled one replaces it
+    assert [x["tag"] for x in recs if x["workload"] == w] == [5]
+
+
 def test_mesh_roofline_fabric_request_ceiling(tmp_path, monkeypatch):
     """The mesh workloads' `limiter` prices the PMC fabric requests per second against the measured
     ceiling of their access pattern (tools/microbench/gather_ceiling.hip), keyed by the workload."""

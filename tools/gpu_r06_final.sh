@@ -39,10 +39,11 @@ dist)
   MCPT_DIST_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 8 --steps 2 --warmup 1 --no-cpu-baseline --scaling weak > $O/bench_gloo8_weak.json 2> $O/bench_gloo8_weak.err && echo "gloo8 weak ok" &&
   MCPT_DIST_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 --steps 2 --warmup 1 --no-cpu-baseline --config c4 > $O/bench_gloo2_c4.json 2> $O/bench_gloo2_c4.err && echo "gloo2 c4 ok" &&
   MCPT_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 2 --warmup 1 --no-cpu-baseline > $O/bench_gloo2_torchrun.json 2> $O/bench_gloo2_torchrun.err && echo "gloo2 torchrun ok" ;;
-pmc2)   # the headline's record again: every counter pass on the schedule the bench settles on (lane
-  # walk, 4 segments per item: AUTO picked 2 in one of r06x's five passes), 4 timed calls averaged
+pmc2)   # the headline's record again: every counter pass on one schedule (lane walk, PMC_SEG segments
+  # per item, default 4: AUTO settles on 4, or on 2 in some runs — r06x, r06q), 4 timed calls
+  # averaged; records of other schedules stay beside it (pmc_summary.merge_record)
   cp profiles/pmc_records.json $O/pmc_records.json
-  MCPT_SEG_PER_ITEM=4 PMC_STEPS=4 bash tools/pmc.sh $O/pmc_c2 && python tools/pmc_summary.py $O/pmc_c2 scene6_1920x1080_256spp_B8 $O/pmc_records.json --calls=4 > $O/pmc_c2_summary.json && echo "pmc c2 ok" ;;
+  MCPT_SEG_PER_ITEM=${PMC_SEG:-4} PMC_STEPS=4 bash tools/pmc.sh $O/pmc_c2 && python tools/pmc_summary.py $O/pmc_c2 scene6_1920x1080_256spp_B8 $O/pmc_records.json --calls=4 > $O/pmc_c2_summary.json && echo "pmc c2 ok" ;;
 c5full)
   timeout -k 10 400 python tools/c5_full.py > $O/c5_full.jsonl 2> $O/c5_full.err && echo "c5 full ok" && head -1 $O/c5_full.jsonl && tail -1 $O/c5_full.jsonl ;;
 esac

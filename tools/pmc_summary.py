@@ -26,6 +26,18 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(REPO, "montecarlo-pathtracing_amd", "mcpt", "libmcpt.so")
 
 
+def merge_record(recs, rec):
+    """The records file after adding `rec`: records of other builds are dropped, and there is one
+    record per (workload, schedule) of this build — a record of another schedule stays beside the
+    new one (bench.py uses the one of the schedule its run settled on); a record of mixed
+    schedules (None) replaces, and is replaced by, every record of its workload."""
+    def same_slot(r):
+        if r.get("workload") != rec.get("workload"):
+            return False
+        a, b = r.get("schedule"), rec.get("schedule")
+        return a is None or b is None or a == b
+    return [r for r in recs if r.get("lib_sha256") == rec["lib_sha256"] and not same_slot(r)] + [rec]
+
 def load(d, launches=1, calls=1):
     """Counters of the timed step's path-tracing launches in each pass, summed: the LAST
     `launches` dispatches (earlier ones are warm-up, including AUTO's timing trials).  A render
@@ -136,8 +148,7 @@ def main():
             recs = json.load(f)["records"]
     except (OSError, ValueError, KeyError):
         recs = []
-    recs = [r for r in recs if r.get("lib_sha256") == rec["lib_sha256"] and r.get("workload") != workload]
-    recs.append(rec)
+    recs = merge_record(recs, rec)
     with open(out, "w") as f:
         json.dump({"records": recs}, f, indent=1)
     print(json.dumps(rec, indent=1))
