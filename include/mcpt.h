@@ -216,7 +216,10 @@ int mcpt_gather_rows(mcpt_ctx* frame, mcpt_ctx* const* shards, int n_shards);
  * render lanes); a trial's time is read when the call after the next one starts, so AUTO settles
  * two calls after its last trial (mcpt.AUTO_TRIALS = 12 calls).  It never times the stream
  * schedule, which runs only when selected explicitly (MCPT_TRAVERSAL_STREAM).  Later launches of
- * that shape use the fastest.  mcpt_get_walk_exit / mcpt_get_leaf_batch report the knobs of the
+ * that shape use the fastest — except that, with render lanes on, two segments per item give way
+ * to four when the four-segment trials are within 2 % (on the lanes, longer items overlap the
+ * previous launch's tail better than the in-order trials show).  mcpt_get_walk_exit /
+ * mcpt_get_leaf_batch report the knobs of the
  * candidate the next launch uses.
  * mcpt_get_traversal reports the strategy the next render uses (a trial candidate until AUTO
  * has settled: see mcpt_get_schedule's `settled`).  Every strategy gives the same bits. */

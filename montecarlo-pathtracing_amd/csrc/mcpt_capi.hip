@@ -286,6 +286,21 @@ static bool cand_deep_knobs(int cand) { return cand == kCandDeepSeg4 || cand == 
 // picked two- or four-segment items run to run on scene 6, 1-2.5 % apart)
 constexpr int kTuneRounds = 2;
 
+// The decision's one tie-break: the per-lane walk with two segments per item gives way to four
+// when the four-segment trials are within kSegMargin of it (render lanes on).  The trials run in
+// order, the settled schedule on the render lanes, where an item of four segments overlaps the
+// previous launch's tail better: on the lanes four are 3.1 % (C2) and 3.4 % (C5) faster than two
+// (profiles/r06_seg_ab.jsonl), while the in-order trials put the two within ~1-2 % of each other
+// either way, so AUTO settled on two in some runs (the r06w bench: 14,585 against 14,814
+// Msamples/s with four).
+constexpr double kSegMargin = 0.02;
+static int prefer_longer_items(const mcpt_ctx* c, int best, long long segs) {
+  if (c->overlap && best == kCandLaneSeg2 && cand_applies(c, kCandLaneSeg4, segs) && c->tune_cnt[kCandLaneSeg4] > 0 &&
+      c->tune_ns[kCandLaneSeg4] <= c->tune_ns[kCandLaneSeg2] * (1.0 + kSegMargin))
+    return kCandLaneSeg4;
+  return best;
+}
+
 // trials of candidate k issued so far on the measured shape (collected + pending)
 static int tune_issued(const mcpt_ctx* c, int k) {
   int n = c->tune_cnt[k];
@@ -307,7 +322,7 @@ static int resolve_candidate(const mcpt_ctx* c, long long segs) {
     for (int k = 1; k <= kCandLast; ++k)
       if (cand_applies(c, k, segs) && c->tune_cnt[k] > 0 && (c->tune_cnt[best] == 0 || c->tune_ns[k] < c->tune_ns[best]))
         best = k;
-    return best;
+    return prefer_longer_items(c, best, segs);
   }
   for (int i = 0; i < kCandLast; ++i) {
     const int k = (round % 2 == 0) ? 1 + i : kCandLast - i;
@@ -359,7 +374,7 @@ static hipError_t collect_tuning(mcpt_ctx* c, int keep) {
       else if (t[k] < t[best]) best = k;
     }
     if (all) {
-      c->tune_choice = best;
+      c->tune_choice = prefer_longer_items(c, best, c->meas_segs);
       c->n_pend = 0;   // (trials of another shape still pending are dropped with the decision)
     }
   }
