@@ -170,6 +170,8 @@ struct mcpt_ctx {
     int* d_item_perm = nullptr;
     int* d_split_of = nullptr;      // split items: item -> split index (-1: whole)
     float* d_split_pass = nullptr;  // split items: the later pieces' per-pass values
+    float* d_steal = nullptr;       // pass stealing: every pass's value (RenderParams::steal_vals)
+    size_t steal_bytes = 0;
     int* d_split_n = nullptr;       // split items: how many (from the last sort)
     void* d_sort_tmp = nullptr;
     size_t sort_tmp_bytes = 0;
@@ -510,6 +512,7 @@ int mcpt_destroy(mcpt_ctx* c) {
     (void)hipFree(L.d_item_perm);
     (void)hipFree(L.d_split_of);
     (void)hipFree(L.d_split_pass);
+    (void)hipFree(L.d_steal);
     (void)hipFree(L.d_split_n);
     (void)hipFree(L.d_sort_tmp);
     if (L.freed) (void)hipEventDestroy(L.freed);
@@ -1237,6 +1240,7 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
     p.item_perm = nullptr;
     p.item_cost = nullptr;
     p.split_n = nullptr; p.split_of = nullptr; p.split_pass = nullptr; p.split_max = 0;
+    p.steal_vals = nullptr;
     p.n_items = (int)items;
     p.tail_m = 0;
 #ifdef MCPT_CHECKED
@@ -1316,6 +1320,19 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
       p.split_pass = L.d_split_pass;
       p.split_max = kSplitMax;
       if (p.item_perm) p.split_n = L.d_split_n;
+      // pass stealing (kernel: steal_next; MCPT_STEAL=0: off, tests and A/B; the same bits either way)
+      if (env_int("MCPT_STEAL", 1) != 0) {
+        const size_t need = sizeof(float) * 3 * (size_t)items * mcpt::kPassChunk * mcpt::kTileThreads;
+        if (need > L.steal_bytes) {
+          HIP_OR_RETURN(hipStreamSynchronize(c->stream));   // (ordered after every lane's work)
+          (void)hipFree(L.d_steal);
+          L.d_steal = nullptr;
+          L.steal_bytes = 0;
+          HIP_OR_RETURN(hipMalloc(&L.d_steal, need));
+          L.steal_bytes = need;
+        }
+        p.steal_vals = L.d_steal;
+      }
     }
     // The timed interval of a lane launch that follows one on the other lane starts where that
     // launch's render ended (recorded on its stream): the launches overlap, and each is charged

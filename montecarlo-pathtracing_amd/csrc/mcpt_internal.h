@@ -126,6 +126,12 @@ struct RenderParams {
   const int* split_n;
   int* split_of;
   float* split_pass;
+  // pass stealing (mesh kernels with split items; null: off): every pass's value of the launch goes
+  // to steal_vals (n_items x kPassChunk x kTileThreads x 3 floats, by the pass's offset in its
+  // segment and its pixel's thread), a lane done with its own pixel takes the next unstarted pass
+  // of any pixel of its workgroup, and combine_steal_kernel sums each segment's passes from 0 in
+  // pass order: the bits of the per-lane sums
+  float* steal_vals;
   int n_items;                  // work items of the launch (its grid may hold spare workgroups)
   int tail_m;                   // seg_per_item > 1: the last tail_m items of item_perm run one segment per workgroup
   int tile_w;                   // the launch's tile width (tile_w_for)
@@ -218,6 +224,7 @@ hipError_t mcpt_iota(int* a, int n, hipStream_t stream);
 hipError_t mcpt_split_count(const unsigned* cost_sorted, int n, int capacity, int split_max, int* out,
                             unsigned long long* dbg, hipStream_t stream);
 constexpr int kDebugSplitSlot = 63;   // debug counter slot: items split by the last sort (mesh scenes)
+constexpr int kDebugStealSlot = 62;   // debug counter slot: passes rendered by pass stealing (summed)
 
 // Checked diagnostic build (make checked: -DMCPT_CHECKED; never timed).  Every index the render
 // and combine kernels derive from the work-item order, the split items and the segment slots is

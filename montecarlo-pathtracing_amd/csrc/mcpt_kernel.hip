@@ -153,6 +153,7 @@ __global__ __launch_bounds__(TW * kTileH, MESH && !WAVE ? kMinWavesMesh
     pass_begin = p.first_pass + seg_lo;
     pass_end = pass_begin + 1;
   }
+  const int seg_first = pass_begin;   // the segment's first pass (pass stealing: value slots)
   int b1 = 0;   // a split item's first pass of piece 1 (its later pieces store per-pass values)
   if (kSplit && piece >= 0) {   // (split launches: full 32-pass segments, one per item)
     const int n = pass_end - pass_begin;
@@ -180,6 +181,19 @@ __global__ __launch_bounds__(TW * kTileH, MESH && !WAVE ? kMinWavesMesh
     s.prims = s_scene + 3 * n_nodes;
     s.leaves = s_int;
     s.ptype = s_int + n_leaves;
+  }
+  // pass stealing (mesh kernels, steal_vals set): the workgroup's units are (pass offset, thread)
+  // = (u / TT, u % TT) for u < TT x (pass_end - pass_begin); thread t starts with unit t (its own
+  // pixel's first pass) and every lane claims the next one when its pass ends (s_claim)
+  static_assert(!kSplit || TT == 64, "pass stealing: one wave per workgroup (LDS order, unit mapping)");
+  const bool steal = kSplit && p.steal_vals != nullptr;
+  __shared__ int s_claim;
+  __shared__ unsigned s_stolen;   // passes this workgroup's lanes rendered for other lanes' pixels
+  if constexpr (kSplit) {
+    if (steal) {
+      if (tid == 0) { s_claim = TT; s_stolen = 0u; }
+      __syncthreads();
+    }
   }
   Ev<COUNT> ev;
   ev.init();
@@ -220,9 +234,11 @@ __global__ __launch_bounds__(TW * kTileH, MESH && !WAVE ? kMinWavesMesh
     s_pix[18][tid] = u; s_pix[19][tid] = v;
     if constexpr (kPxLds) s_pix[20][tid] = __int_as_float(lr * p.W + x);   // < n_local_px <= 2^31 - 1 (mcpt_set_target*)
   }
+  // the thread whose pixel this lane renders: its own, except for passes taken by pass stealing
+  int pj = tid;
   // (u, v) of this pixel for the seed of a new pass (seed_for): the same values as u, v above
   auto pix_seed = [&](int ps) {
-    if constexpr (kPixLds) return seed_for(s_pix[18][tid], s_pix[19][tid], ps, p.date);
+    if constexpr (kPixLds) return seed_for(s_pix[18][pj], s_pix[19][pj], ps, p.date);
     else return seed_for(((float)x + 0.5f) / (float)p.W, ((float)y + 0.5f) / (float)p.H, ps, p.date);
   };
   s_pix[12][tid] = 0.0f; s_pix[13][tid] = 0.0f; s_pix[14][tid] = 0.0f;   // this segment's sum
@@ -268,7 +284,7 @@ __global__ __launch_bounds__(TW * kTileH, MESH && !WAVE ? kMinWavesMesh
 #endif
   // this segment's sum -> accumulator (one-segment launch) or its segment slot
   auto flush_sum = [&]() {
-    if (kSplit && piece > 0) return;   // a later piece's passes are stored one by one (add_pass)
+    if (kSplit && (piece > 0 || steal)) return;   // passes stored one by one (add_pass)
     // the pixel's address is recomputed at each flush (an empty asm makes the row opaque):
     // hoisted out of the render loop, its 64-bit index and pointer were 4 spilled VGPRs
     size_t px;
@@ -295,6 +311,15 @@ __global__ __launch_bounds__(TW * kTileH, MESH && !WAVE ? kMinWavesMesh
   // a finished pass's value: into this segment's sum, or (a split item's later pieces) stored
   // for the combine, which adds it after piece 0's sum in pass order
   auto add_pass = [&](f3 v) {
+    if (kSplit && steal) {
+      if constexpr (kChecked) {
+        if (!idx_ok(p.events, CK_SPLIT_PASS, pass - seg_first, kPassChunk) || !idx_ok(p.events, CK_SPLIT_PASS, pj, kTileThreads))
+          return;
+      }
+      float* q = p.steal_vals + (((size_t)item * kPassChunk + (pass - seg_first)) * kTileThreads + pj) * 3;
+      q[0] = v.x; q[1] = v.y; q[2] = v.z;
+      return;
+    }
     if (kSplit && piece > 0) {
       if constexpr (kChecked) {
         if (!idx_ok(p.events, CK_SPLIT_PASS, sj, p.split_max) || !idx_ok(p.events, CK_SPLIT_PASS, pass - b1, kPassChunk) ||
@@ -309,7 +334,27 @@ __global__ __launch_bounds__(TW * kTileH, MESH && !WAVE ? kMinWavesMesh
       s_pix[14][tid] = s_pix[14][tid] + v.z;
     }
   };
+  // pass stealing: after a pass (pass++ done by the caller), the lane's next unit.  Units whose
+  // pixel lies outside the frame are skipped; none left: pass = pass_end, the lane is done.
+  const int steal_n = pass_end - pass_begin;
+  auto steal_next = [&]() {
+    for (;;) {
+      const int u = atomicAdd(&s_claim, 1);
+      if (u >= TT * steal_n) { pass = pass_end; return; }
+      const int t = u % TT;
+      const int xt = bx0 + (t & 7), lt = by0 + (t >> 3);   // (one 8x8 wave per workgroup: TW = 8)
+      if (xt < p.W && lt < p.n_local_rows) {
+        pj = t; pass = pass_begin + u / TT;
+        if (t != tid) atomicAdd(&s_stolen, 1u);
+        return;
+      }
+    }
+  };
   auto next_chunk = [&]() {
+    if (kSplit && steal) {
+      steal_next();
+      return;
+    }
     if (pass >= pass_end) {
       flush_sum();
       if (seg + 1 < seg_lo + seg_n) {
@@ -344,7 +389,7 @@ __global__ __launch_bounds__(TW * kTileH, MESH && !WAVE ? kMinWavesMesh
       done = true;   // for(i=0; i<NB_BOUNCES ...) never runs: black
     } else {
       if (first) {
-        h.code = s_hit0[tid];
+        h.code = s_hit0[pj];
       } else if (WAVE) {
         traverse<COUNT, WAVE>(s, O, D, h, ev);
       } else {
@@ -398,10 +443,10 @@ __global__ __launch_bounds__(TW * kTileH, MESH && !WAVE ? kMinWavesMesh
       next_chunk();
       if (pass < pass_end) {
         rng = pix_seed(pass);
-        O = Ocam; D = mk(s_pix[0][tid], s_pix[1][tid], s_pix[2][tid]);
+        O = Ocam; D = mk(s_pix[0][pj], s_pix[1][pj], s_pix[2][pj]);
         att = mk(0.8f, 0.8f, 0.8f); total = mk(0.0f, 0.0f, 0.0f);
         bounce = 0;
-        h.code = s_hit0[tid];
+        h.code = s_hit0[pj];
         first = true;
       } else {
         ready = false;   // unit finished: the lane claims another at the end of the round
@@ -414,8 +459,8 @@ __global__ __launch_bounds__(TW * kTileH, MESH && !WAVE ? kMinWavesMesh
           res = mk(0.0f, 0.0f, 0.2f);
         } else {
           if (first) {
-            N = mk(s_pix[3][tid], s_pix[4][tid], s_pix[5][tid]);
-            P = mk(s_pix[6][tid], s_pix[7][tid], s_pix[8][tid]);
+            N = mk(s_pix[3][pj], s_pix[4][pj], s_pix[5][pj]);
+            P = mk(s_pix[6][pj], s_pix[7][pj], s_pix[8][pj]);
           }
           else geom_info<COUNT>(s, h, N, P, ev);
           ev.inc(EV_COLMAT);
@@ -437,8 +482,8 @@ __global__ __launch_bounds__(TW * kTileH, MESH && !WAVE ? kMinWavesMesh
           done = true;
         } else {
           if (first) {
-            N = mk(s_pix[3][tid], s_pix[4][tid], s_pix[5][tid]);
-            P = mk(s_pix[6][tid], s_pix[7][tid], s_pix[8][tid]);
+            N = mk(s_pix[3][pj], s_pix[4][pj], s_pix[5][pj]);
+            P = mk(s_pix[6][pj], s_pix[7][pj], s_pix[8][pj]);
           }
           else geom_info<COUNT>(s, h, N, P, ev);
           ev.inc(EV_COLMAT);
@@ -528,7 +573,7 @@ __global__ __launch_bounds__(TW * kTileH, MESH && !WAVE ? kMinWavesMesh
       pass++;
       next_chunk();
       rng = pix_seed(pass);   // = (u, v)
-      O = Ocam; D = mk(s_pix[0][tid], s_pix[1][tid], s_pix[2][tid]);
+      O = Ocam; D = mk(s_pix[0][pj], s_pix[1][pj], s_pix[2][pj]);
       att = mk(0.8f, 0.8f, 0.8f); total = mk(0.0f, 0.0f, 0.0f);
       bounce = 0; phase = 0;
     }
@@ -568,6 +613,10 @@ __global__ __launch_bounds__(TW * kTileH, MESH && !WAVE ? kMinWavesMesh
   }
 #endif
 
+  if constexpr (kSplit) {   // (one wave: its LDS operations are in order)
+    if (steal && p.events && (int)__lane_id() == __builtin_ffsll((long long)__ballot(1)) - 1 && s_stolen)
+      atomicAdd(p.events + kDebugStealSlot, (unsigned long long)s_stolen);
+  }
   if (p.item_cost && (int)__lane_id() == __builtin_ffsll((long long)__ballot(1)) - 1) {
     // this item's cost for the next launch's order: its longest wave (100 MHz ticks)
     unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t_item0;
@@ -659,6 +708,31 @@ __global__ __launch_bounds__(256) void combine_items_kernel(float* __restrict__ 
         const float* v = split_pass + (((size_t)j * kPassChunk + k) * kTileThreads + t) * 3;
         s0 = s0 + v[0]; s1 = s1 + v[1]; s2 = s2 + v[2];
       }
+    }
+    a0 = a0 + s0; a1 = a1 + s1; a2 = a2 + s2;
+  }
+  accum[i * 3] = a0; accum[i * 3 + 1] = a1; accum[i * 3 + 2] = a2;
+}
+
+// launches with pass stealing (RenderParams::steal_vals): every pass's value is stored; per pixel
+// and segment the passes are summed from 0 in pass order (as the lane's segment sum was), and the
+// segment sums are added to the accumulator in segment order — the bits of combine_items_kernel's
+// launches (one segment per item, full 32-pass segments)
+__global__ __launch_bounds__(256) void combine_steal_kernel(float* __restrict__ accum, long long n_px, int n_seg,
+                                                            int W, int TW, const float* __restrict__ vals) {
+  long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n_px) return;
+  const int lr = (int)(i / W), x = (int)(i - (long long)lr * W);
+  const int tiles_x = (W + TW - 1) / TW;
+  const int tile = (lr / kTileH) * tiles_x + x / TW;
+  const int t = (((lr % kTileH) / 8) * (TW / 8) + (x % TW) / 8) * 64 + (lr % 8) * 8 + (x % 8);   // its thread
+  float a0 = accum[i * 3], a1 = accum[i * 3 + 1], a2 = accum[i * 3 + 2];
+  for (int s = 0; s < n_seg; ++s) {
+    const size_t item = (size_t)tile * n_seg + s;
+    float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f;
+    for (int k = 0; k < kPassChunk; ++k) {
+      const float* v = vals + ((item * kPassChunk + k) * kTileThreads + t) * 3;
+      s0 = s0 + v[0]; s1 = s1 + v[1]; s2 = s2 + v[2];
     }
     a0 = a0 + s0; a1 = a1 + s1; a2 = a2 + s2;
   }
@@ -787,8 +861,14 @@ hipError_t mcpt_launch_render(const mcpt::RenderParams& p, bool count, hipStream
 }
 
 hipError_t mcpt_launch_combine(const mcpt::RenderParams& p, hipStream_t stream) {
-  if (p.n_segments <= 1 || p.n_local_px <= 0) return hipSuccess;
+  if (p.n_local_px <= 0) return hipSuccess;
   dim3 block(256), grid((unsigned)((p.n_local_px + 255) / 256));
+  if (p.steal_vals) {   // (also for one segment: the render stored passes, no sums)
+    hipLaunchKernelGGL(mcpt::combine_steal_kernel, grid, block, 0, stream, p.accum, p.n_local_px, p.n_segments, p.W,
+                       p.tile_w, p.steal_vals);
+    return hipGetLastError();
+  }
+  if (p.n_segments <= 1) return hipSuccess;
   if (p.pass_split)
     hipLaunchKernelGGL(mcpt::combine_split_kernel, grid, block, 0, stream, p.accum, p.partial, p.n_local_px,
                        p.first_pass, p.n_passes);

@@ -155,6 +155,27 @@ def test_mesh_split_items_same_bits(mcpt_mod, renderer, big_mesh, monkeypatch):
     assert np.array_equal(bits(a), bits(b))
 
 
+def test_mesh_pass_stealing_same_bits(mcpt_mod, renderer, big_mesh, monkeypatch):
+    """Pass stealing on the 1 M-triangle mesh workload (RenderParams::steal_vals): a lane whose
+    pixel's passes are done renders the next unstarted pass of another pixel of its workgroup,
+    every pass's value is stored and combine_steal_kernel sums each segment's passes from 0 in pass
+    order.  Three 64-pass calls equal the same calls with MCPT_STEAL=0 bit for bit; debug slot 62
+    counts the passes rendered for another lane's pixel."""
+    W, H, B = 1920, 1080, 8
+    renderer.set_traversal(1)
+    try:
+        monkeypatch.setenv("MCPT_STEAL", "1")
+        renderer.debug_counters(reset=True)
+        a = render(mcpt_mod, renderer, big_mesh, W, H, 1, 192, B, split=[64, 64, 64])
+        n_stolen = int(renderer.debug_counters()[62])
+        monkeypatch.setenv("MCPT_STEAL", "0")
+        b = render(mcpt_mod, renderer, big_mesh, W, H, 1, 192, B, split=[64, 64, 64])
+    finally:
+        renderer.set_traversal(0)
+    assert n_stolen > 0
+    assert np.array_equal(bits(a), bits(b))
+
+
 @pytest.fixture(scope="module")
 def big_mesh4(mcpt_mod):
     from mcpt import meshes
