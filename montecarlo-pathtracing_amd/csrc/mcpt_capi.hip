@@ -1187,7 +1187,11 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   const long long spare = (long long)kSplitMax * (mcpt::kSplitPieces - 1) + 28LL * c->n_cu * (kseg_max - 1);
   const long long max_items = (1LL << 32) / (p.tile_w * mcpt::kTileH) - 1 - spare;
   if (p.n_tiles > max_items) return set_err(MCPT_ERR_INVALID_ARG, "render target too large for one launch");
-  long long max_seg = seg_bytes > 0 ? (long long)(c->partial_budget / (size_t)seg_bytes) : (1LL << 30);
+  // (mesh launches that may steal passes also store every pass's value, kPassChunk per segment
+  // and pixel, in the same budget: 1080p, 4 GiB: 5 segments per sub-launch)
+  const bool may_steal = c->n_meshes > 0 && !p.wave_traversal && kseg_max == 1 && env_int("MCPT_STEAL", 1) != 0;
+  const size_t seg_cost = (size_t)seg_bytes * (may_steal ? 1 + mcpt::kPassChunk : 1);
+  long long max_seg = seg_bytes > 0 ? (long long)(c->partial_budget / seg_cost) : (1LL << 30);
   max_seg = std::max(1LL, std::min(max_seg, p.n_tiles > 0 ? max_items / p.n_tiles : max_items));
   // Pass split: a launch with too few work items to fill the chip (C1: 256 tiles x 1 segment
   // on 256 CUs, one wave per SIMD running every pass of its pixels in turn) runs one segment per
