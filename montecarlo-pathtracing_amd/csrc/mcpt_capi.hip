@@ -55,6 +55,8 @@ int mcpt_err_bare(int status) {
 // is one launch: +0.7 % against four launches under a 1 GiB bound, whose grid tails add up,
 // profiles/r03_ab_partial_budget_c5.jsonl; mcpt_set_partial_budget / MCPT_PARTIAL_BYTES)
 constexpr size_t kDefaultPartialBudget = size_t(4) << 30;
+// per-pass value store of pass stealing (mesh launches), per render lane
+constexpr size_t kStealBudget = size_t(8) << 30;
 // render calls whose events a context keeps (mcpt_kernel_ms_back)
 constexpr int kTimingRing = 64;
 // work-item order (mcpt_order.hip): launches with at least this many work items run in the
@@ -1187,11 +1189,13 @@ static int launch(mcpt_ctx* c, const float* invPV, const float* invV, int first_
   const long long spare = (long long)kSplitMax * (mcpt::kSplitPieces - 1) + 28LL * c->n_cu * (kseg_max - 1);
   const long long max_items = (1LL << 32) / (p.tile_w * mcpt::kTileH) - 1 - spare;
   if (p.n_tiles > max_items) return set_err(MCPT_ERR_INVALID_ARG, "render target too large for one launch");
-  // (mesh launches that may steal passes also store every pass's value, kPassChunk per segment
-  // and pixel, in the same budget: 1080p, 4 GiB: 5 segments per sub-launch)
+  long long max_seg = seg_bytes > 0 ? (long long)(c->partial_budget / (size_t)seg_bytes) : (1LL << 30);
+  // mesh launches that may steal passes also store every pass's value (kPassChunk per segment and
+  // pixel): at most kStealBudget of them per render lane, but two segments at least, so that
+  // split items and stealing still apply (1080p: 10 segments per sub-launch; 4K: 2, 6.4 GB)
   const bool may_steal = c->n_meshes > 0 && !p.wave_traversal && kseg_max == 1 && env_int("MCPT_STEAL", 1) != 0;
-  const size_t seg_cost = (size_t)seg_bytes * (may_steal ? 1 + mcpt::kPassChunk : 1);
-  long long max_seg = seg_bytes > 0 ? (long long)(c->partial_budget / seg_cost) : (1LL << 30);
+  if (may_steal && seg_bytes > 0)
+    max_seg = std::min(max_seg, std::max(2LL, (long long)(kStealBudget / ((size_t)seg_bytes * mcpt::kPassChunk))));
   max_seg = std::max(1LL, std::min(max_seg, p.n_tiles > 0 ? max_items / p.n_tiles : max_items));
   // Pass split: a launch with too few work items to fill the chip (C1: 256 tiles x 1 segment
   // on 256 CUs, one wave per SIMD running every pass of its pixels in turn) runs one segment per
